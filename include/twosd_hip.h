@@ -1,0 +1,163 @@
+/*
+ * twosd_hip.h -- C ABI of libtwosd_hip.so, the MI355X (gfx950) implementation of the
+ * TwoSD per-iteration scenario-subproblem + cut-generation hot path.
+ *
+ * Reference: yhz0/SQLP (module TwoSD, pure Julia) @ 2025-02-19.  The reference has no
+ * FFI/plugin API for this path (src/sd_algorithm/plugin/ holds 0-byte files); the
+ * entry points below are what a Julia `ccall` shim binds to add
+ * accelerated methods for the same generic functions.  Each entry cites the reference
+ * function it replaces.
+ *
+ * Conventions
+ *   - All calls are synchronous: outputs are valid on return.  Host buffers are owned by
+ *     the caller; the library copies in and out.  Device memory is owned by the context.
+ *   - Return value: TWOSD_OK (0) or a negative TWOSD_E_* code; twosd_last_error() gives a
+ *     thread-local message.  A context is not re-entrant; distinct contexts are
+ *     independent (one context per GPU / process).
+ *   - Indices: `index_base` = 1 accepts Julia's 1-based SparseMatrixCSC arrays directly.
+ *   - Stage-2 LP of one scenario w at first-stage x (smps_routines.jl:50-62):
+ *         min q'y  s.t.  W y  (G: >=, L: <=, E: ==)  r_w - T_w x,   y >= 0
+ *     duals pi follow JuMP's MIN convention (G rows >= 0, L rows <= 0, E free;
+ *     pi = d obj / d rhs), so obj = pi . (r_w - T_w x).
+ *   - Variables of the simplex basis ("head"): j < n2 is structural y_j; j = n2 + i is the
+ *     slack of row i.
+ */
+#ifndef TWOSD_HIP_H
+#define TWOSD_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct twosd_ctx twosd_ctx;
+
+enum {
+    TWOSD_OK = 0,
+    TWOSD_E_ARG = -1,        /* bad argument (sizes, indices, NULL)          */
+    TWOSD_E_DEVICE = -2,     /* HIP runtime / kernel launch failure           */
+    TWOSD_E_STATE = -3,      /* call out of order (e.g. no template yet)      */
+    TWOSD_E_LP = -4,         /* LP not solved to optimality (see status[])    */
+    TWOSD_E_UNSUPPORTED = -5 /* template outside the kernel's envelope        */
+};
+
+/* per-scenario LP status (status[] outputs) */
+enum { TWOSD_LP_OPTIMAL = 0, TWOSD_LP_INFEASIBLE = 1, TWOSD_LP_ITER_LIMIT = 2, TWOSD_LP_NUMERIC = 3 };
+
+/* Thread-local message for the last failing call on this thread. */
+const char *twosd_last_error(void);
+
+/* Library version string. */
+const char *twosd_version(void);
+
+/* Create a context on HIP device `device` (one context per GPU / rank). */
+int twosd_create(int device, twosd_ctx **out);
+int twosd_destroy(twosd_ctx *ctx);
+
+/*
+ * Stage-2 template (replaces extract_coefficients, subprob.jl:15-69, and the JuMP model
+ * held by spStageProblem, prob.jl:10-15).
+ *   T: m2 x n1 CSC (colptr[n1+1], rowval[nnzT], nzval[nnzT]); W: m2 x n2 CSC.
+ *   q[n2], r[m2], sense[m2] in {'G','L','E'}, ylb/yub[n2] (only [0, +inf) is supported:
+ *   the reference warns on other bounds, subprob.jl:19-26).
+ * Re-setting the template clears basis, scenarios, dual vertex set and cuts.
+ */
+int twosd_set_template(twosd_ctx *ctx, int m2, int n1, int n2,
+                       const int64_t *T_colptr, const int64_t *T_rowval, const double *T_nzval,
+                       const int64_t *W_colptr, const int64_t *W_rowval, const double *W_nzval,
+                       const double *q, const double *r, const char *sense,
+                       const double *ylb, const double *yub, int index_base);
+
+/*
+ * Random element positions of a scenario (spSmpsScenario entries, smps_sto.jl:135):
+ * element e sits at stage-2 row row[e]; col[e] = -1 for an RHS entry, else the
+ * first-stage column of a T entry (delta_coefficients, subprob.jl:104-121).
+ */
+int twosd_set_random_positions(twosd_ctx *ctx, int k, const int *row, const int *col, int index_base);
+
+/*
+ * Warm-start basis shared by every scenario (dual feasible for all RHS).
+ * twosd_compute_basis solves the LP at x for the scenario `values` (k entries; NULL =
+ * template rhs) from the slack basis once on the host and installs its optimal basis.
+ * twosd_set_basis installs a caller-provided basis (m2 variable indices, 0-based).
+ */
+int twosd_compute_basis(twosd_ctx *ctx, const double *x, const double *values);
+int twosd_set_basis(twosd_ctx *ctx, const int *head);
+int twosd_get_basis(twosd_ctx *ctx, int *head);
+
+/* Epigraphs (sdEpigraph, epigraph.jl:17-61): per-epigraph scenario pool + weights. */
+int twosd_epigraph_create(twosd_ctx *ctx, int *epi_out);
+/* add_scenario!(epi, w, weight) batched (epigraph.jl:81-96): values[N*k] are the
+ * scenario's element values in position order; weights[N] (NULL = all 1.0). */
+int twosd_add_scenarios(twosd_ctx *ctx, int epi, int N, const double *values, const double *weights);
+int twosd_epigraph_info(twosd_ctx *ctx, int epi, int *num_scenarios, double *total_weight);
+
+/*
+ * solve_problem! (smps_routines.jl:50-62) for scenarios [first, first+count) of epigraph
+ * `epi` at first-stage x[n1].  obj[count], status[count] required; pi[count*m2] and
+ * y[count*n2] nullable.  Returns TWOSD_E_LP if any status != OPTIMAL (outputs still set).
+ */
+int twosd_solve_batch(twosd_ctx *ctx, int epi, const double *x, int first, int count,
+                      double *obj, double *pi, double *y, int *status);
+
+/* Same for scenarios given by value (evaluate(), smps_routines.jl:67-82): values[N*k]. */
+int twosd_solve_values(twosd_ctx *ctx, const double *x, int N, const double *values,
+                       double *obj, double *pi, double *y, int *status);
+
+/*
+ * push!(::sdDualVertexSet, pi) batched (dual_set.jl:84-94): pis[count*m2] are pushed in
+ * order; out_index[count] (nullable) receives the 0-based vertex index each one maps to;
+ * *new_size the set size afterwards.  Exact reference dedup semantics: 16-significant-bit
+ * L1 hash + component-wise 16-bit rounding compare, first occurrence kept.
+ */
+int twosd_dvs_push(twosd_ctx *ctx, int count, const double *pis, int *out_index, int *new_size);
+int twosd_dvs_size(twosd_ctx *ctx, int *size);
+int twosd_dvs_get(twosd_ctx *ctx, int first, int count, double *out /* count*m2 */);
+int twosd_dvs_clear(twosd_ctx *ctx);
+/* Truncate the set to its first `size` vertices (rollback of a speculative push). */
+int twosd_dvs_truncate(twosd_ctx *ctx, int size);
+
+/*
+ * sd_iteration! hot segment for one epigraph (algorithm.jl:45-55): solve scenarios
+ * [first, first+count) at x and push their duals into the vertex set on the device
+ * (no host round trip).  obj/status nullable.
+ */
+int twosd_solve_push(twosd_ctx *ctx, int epi, const double *x, int first, int count,
+                     double *obj, int *status, int *new_size);
+
+/*
+ * build_sasa_cut (epigraph.jl:125-146) incl. argmax_procedure (subprob.jl:141-169) over
+ * every scenario of epigraph `epi` and the current vertex set, at x:
+ *   alpha, beta[n1], weight_mark (= total scenario weight); max_val[N], max_arg[N]
+ *   (0-based vertex index) nullable.  Ties: lowest vertex index among scores within
+ *   tie_rel*(1+|max|) of the maximum (tie_rel = 0 -> strict '>' as the reference).
+ */
+int twosd_build_cut(twosd_ctx *ctx, int epi, const double *x, double tie_rel,
+                    double *alpha, double *beta, double *weight_mark,
+                    double *max_val, int *max_arg);
+
+/*
+ * Multi-GPU split of twosd_build_cut: each rank computes partial sums over its own
+ * scenarios into a caller-provided DEVICE buffer (layout in twosd_cut_partial_len),
+ * the caller all-reduces it (sum; e.g. torch.distributed / RCCL), then finalize.
+ * The partial holds the vertex weight histogram as uint64 fixed point (exact, order
+ * independent) followed by fp64 sums.  total_weight is the global total scenario weight.
+ */
+int twosd_cut_partial_len(twosd_ctx *ctx, int64_t *n_u64, int64_t *n_f64);
+int twosd_cut_partial(twosd_ctx *ctx, int epi, const double *x, double tie_rel, double total_weight,
+                      uint64_t *d_hist_u64, double *d_sums_f64, double *max_val, int *max_arg);
+int twosd_cut_finalize(twosd_ctx *ctx, const double *x, const uint64_t *d_hist_u64, const double *d_sums_f64,
+                       double *alpha, double *beta);
+
+/* Timing of the last kernel phases on the context's stream (HIP events), microseconds:
+ * [0] LP batch, [1] dedup push, [2] argmax+cut partial, [3] cut finalize. */
+int twosd_last_timings(twosd_ctx *ctx, double *us4);
+
+/* Statistics of the last LP batch: sum of simplex pivots, max pivots. */
+int twosd_last_lp_stats(twosd_ctx *ctx, int64_t *pivots_sum, int *pivots_max);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TWOSD_HIP_H */

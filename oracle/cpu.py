@@ -1,0 +1,125 @@
+"""ctypes wrapper for oracle/cpu_lp.c (TEST INFRASTRUCTURE ONLY -- see oracle/__init__.py).
+
+``CpuLP`` is the CPU restatement of the per-scenario LP solve (solve_problem!,
+src/smps/smps_routines.jl:50-62) and ``build_cut`` the reference-order
+argmax_procedure + build_sasa_cut (subprob.jl:141-169, epigraph.jl:125-146).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle_cpu.so")
+_lib = None
+
+ST_OPTIMAL, ST_INFEASIBLE, ST_ITER_LIMIT, ST_NUMERIC = 0, 1, 2, 3
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        P = C.c_void_p
+        L.oracle_lp_create.restype = P
+        L.oracle_lp_create.argtypes = [C.c_int, C.c_int, P, P, P, P, P]
+        L.oracle_lp_destroy.argtypes = [P]
+        L.oracle_lp_set_basis.argtypes = [P, P]
+        L.oracle_lp_basis_dual_infeas.argtypes = [P]
+        L.oracle_lp_basis_dual_infeas.restype = C.c_double
+        L.oracle_lp_solve_from_slack.argtypes = [P, P, P, P, P]
+        L.oracle_lp_solve_batch.argtypes = [P, C.c_int, C.c_int, P, P, P, C.c_int, P, P, P, P, P, C.c_int]
+        L.oracle_build_cut.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P, P, P,
+                                       C.c_double, P, P, P, P, C.c_int]
+        L.oracle_dense_inverse.argtypes = [C.c_int, P, P]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def dense_to_csc(W):
+    W = np.asarray(W, dtype=np.float64)
+    m, n = W.shape
+    colptr = [0]
+    rows, vals = [], []
+    for j in range(n):
+        nz = np.nonzero(W[:, j])[0]
+        rows.extend(nz.tolist())
+        vals.extend(W[nz, j].tolist())
+        colptr.append(len(rows))
+    return (np.array(colptr, dtype=np.int32), np.array(rows, dtype=np.int32),
+            np.array(vals, dtype=np.float64))
+
+
+class CpuLP:
+    """Warm-started dual simplex on min q'y, W y (senses) b, y >= 0."""
+
+    def __init__(self, W, q, senses):
+        self.m, self.n = W.shape
+        self.colptr, self.rowidx, self.val = dense_to_csc(W)
+        self.q = np.ascontiguousarray(q, dtype=np.float64)
+        self.sense = np.frombuffer("".join(senses).encode(), dtype=np.int8).copy()
+        self.h = lib().oracle_lp_create(self.m, self.n, _p(self.colptr), _p(self.rowidx), _p(self.val),
+                                        _p(self.q), _p(self.sense))
+        self.head0 = None
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.oracle_lp_destroy(self.h)
+            self.h = None
+
+    def solve_from_slack(self, b):
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        head = np.zeros(self.m, dtype=np.int32)
+        obj = C.c_double(); it = C.c_int()
+        st = lib().oracle_lp_solve_from_slack(self.h, _p(b), _p(head), C.byref(obj), C.byref(it))
+        return st, obj.value, head, it.value
+
+    def set_basis(self, head0):
+        self.head0 = np.ascontiguousarray(head0, dtype=np.int32)
+        rc = lib().oracle_lp_set_basis(self.h, _p(self.head0))
+        if rc != 0:
+            raise RuntimeError("singular basis")
+        return lib().oracle_lp_basis_dual_infeas(self.h)
+
+    def solve_batch(self, rows, base, DR, kmax=512, want_y=False, nthreads=0):
+        DR = np.ascontiguousarray(DR, dtype=np.float64)
+        N, k = DR.shape
+        rows = np.ascontiguousarray(rows, dtype=np.int32)
+        base = np.ascontiguousarray(base, dtype=np.float64)
+        obj = np.zeros(N); pi = np.zeros((N, self.m)); st = np.zeros(N, dtype=np.int32)
+        it = np.zeros(N, dtype=np.int32)
+        y = np.zeros((N, self.n)) if want_y else None
+        lib().oracle_lp_solve_batch(self.h, N, k, _p(rows), _p(base), _p(DR), kmax, _p(obj), _p(pi),
+                                    _p(y), _p(st), _p(it), nthreads)
+        return obj, pi, y, st, it
+
+
+def build_cut(r, T, x, V, rows, DR, w, tie_rel=0.0, nthreads=0):
+    r = np.ascontiguousarray(r, dtype=np.float64)
+    T = np.ascontiguousarray(T, dtype=np.float64)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    V = np.ascontiguousarray(V, dtype=np.float64)
+    DR = np.ascontiguousarray(DR, dtype=np.float64)
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    rows = np.ascontiguousarray(rows, dtype=np.int32)
+    m, n1 = T.shape
+    N, k = DR.shape
+    nv = V.shape[0]
+    alpha = C.c_double()
+    beta = np.zeros(n1)
+    mv = np.zeros(N); ma = np.zeros(N, dtype=np.int32)
+    lib().oracle_build_cut(m, n1, nv, N, k, _p(rows), _p(r), _p(T), _p(x), _p(V), _p(DR), _p(w),
+                           float(tie_rel), C.byref(alpha), _p(beta), _p(mv), _p(ma), nthreads)
+    return alpha.value, beta, mv, ma

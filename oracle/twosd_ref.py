@@ -1,0 +1,196 @@
+"""TwoSD hot-path restatement (oracle; TEST INFRASTRUCTURE ONLY -- see oracle/__init__.py).
+
+Pure-numpy restatement of the reference's Julia, in the reference's loop order:
+  * ``round16``             <- Julia ``round(x; base=2, sigdigits=16)`` as used at
+                               src/sd_algorithm/dual_set.jl:32-33,51 (Base._round_sigdigits)
+  * ``hash_dual_vector``    <- dual_set.jl:46-53
+  * ``dual_isequal``        <- dual_set.jl:24-40
+  * ``DualVertexSet.push``  <- dual_set.jl:84-94 (linear scan, first occurrence kept)
+  * ``Coefficients``        <- subprob.jl:4-12 / extract_coefficients subprob.jl:15-69
+  * ``delta_coefficients``  <- subprob.jl:104-121
+  * ``eval_dual``           <- subprob.jl:128-131
+  * ``argmax_procedure``    <- subprob.jl:141-169
+  * ``build_sasa_cut``      <- epigraph.jl:125-146
+  * ``add_cut_discount`` / ``evaluate_epigraph`` <- epigraph.jl:101-117, 177-203
+"""
+from __future__ import annotations
+
+import math
+import struct
+import numpy as np
+
+SIGNIFICANT_DIGITS = 16          # dual_set.jl:4
+
+
+def round16(x: float) -> float:
+    """Julia round(x; base=2, sigdigits=16): digits = 16 - (1 + exponent(x)); scale by
+    an exact power of two, round half-to-even, scale back.  Returns x itself when the
+    scale overflows (Julia's _round_digits non-finite guard)."""
+    x = float(x)
+    if x == 0.0:
+        return x
+    m, e2 = math.frexp(x)           # x = m * 2**e2, 0.5 <= |m| < 1  -> exponent(x) = e2-1
+    digits = SIGNIFICANT_DIGITS - e2
+    try:
+        if digits >= 0:
+            sc = 2.0 ** digits
+            r = round(x * sc) / sc
+        else:
+            isc = 2.0 ** (-digits)
+            r = round(x / isc) * isc
+    except OverflowError:
+        return x
+    if not math.isfinite(r):
+        return x
+    return float(r)
+
+
+def round16_array(v) -> np.ndarray:
+    return np.array([round16(t) for t in np.asarray(v, dtype=np.float64)], dtype=np.float64)
+
+
+def hash_dual_vector(vec) -> int:
+    s = 0.0
+    for v in np.asarray(vec, dtype=np.float64):   # sequential sum, dual_set.jl:47-50
+        s += abs(float(v))
+    return struct.unpack("<Q", struct.pack("<d", round16(s)))[0]
+
+
+def dual_isequal(h1, d1, h2, d2) -> bool:
+    if len(d1) != len(d2) or h1 != h2:
+        return False
+    for a, b in zip(d1, d2):
+        if round16(a) != round16(b):
+            return False
+    return True
+
+
+class DualVertexSet:
+    """sdDualVertexSet: insertion-ordered unique vertices (dual_set.jl:69-127)."""
+
+    def __init__(self, data=None):
+        self.hashes: list[int] = []
+        self.data: list[np.ndarray] = []
+        if data is not None:
+            for d in data:
+                self.push(d)
+
+    def push(self, vec) -> int:
+        """Returns the index of the (existing or new) vertex equal to vec."""
+        vec = np.asarray(vec, dtype=np.float64)
+        h = hash_dual_vector(vec)
+        for i, (hv, dv) in enumerate(zip(self.hashes, self.data)):
+            if dual_isequal(h, vec, hv, dv):
+                return i
+        self.hashes.append(h)
+        self.data.append(vec)
+        return len(self.data) - 1
+
+    def __len__(self):
+        return len(self.data)
+
+    def __iter__(self):
+        return iter(self.data)
+
+    def matrix(self, m=None) -> np.ndarray:
+        if not self.data:
+            return np.zeros((0, m or 0))
+        return np.vstack(self.data)
+
+
+class Coefficients:
+    """sdSubprobCoefficients (subprob.jl:4-12): r, T, W + name lookups."""
+
+    def __init__(self, sp):
+        self.rhs = sp.r.copy()
+        self.transfer = sp.T.copy()
+        self.recourse = sp.W.copy()
+        self.col_lookup = {n: i for i, n in enumerate(sp.last_names)}
+        self.row_lookup = {n: i for i, n in enumerate(sp.row_names)}
+
+
+def delta_coefficients(coef: Coefficients, scenario):
+    """subprob.jl:104-121.  scenario = [((col_name,row_name), value), ...].
+    Raises KeyError for unknown rows/columns exactly like the Dict lookups."""
+    dr = np.zeros(len(coef.rhs))
+    dT = np.zeros(coef.transfer.shape)
+    for (col, row), val in scenario:
+        i = coef.row_lookup[row]
+        if col == "RHS" or col == "rhs":
+            dr[i] = val - coef.rhs[i]
+        else:
+            j = coef.col_lookup[col]
+            dT[i, j] = val - coef.transfer[i, j]
+    return dr, dT
+
+
+def eval_dual(coef: Coefficients, delta, x, dual) -> float:
+    dr, dT = delta
+    return float(np.dot(dual, (coef.rhs + dr) - (coef.transfer + dT) @ x))
+
+
+def tie_tolerance(M: float, rel: float) -> float:
+    return rel * (1.0 + abs(M))
+
+
+def argmax_procedure(coef: Coefficients, deltas, x, V, tie_rel: float = 0.0):
+    """subprob.jl:141-169 (MIN_SENSE).  tie_rel == 0 is the reference rule exactly (strict
+    '>' so the first maximum in insertion order wins).  tie_rel > 0 is the build's
+    documented near-tie rule: the lowest vertex index whose score is within
+    tie_rel*(1+|max|) of the maximum."""
+    x = np.asarray(x, dtype=np.float64)
+    base = coef.rhs - coef.transfer @ x
+    Vl = list(V)
+    vals, args = [], []
+    for dr, dT in deltas:
+        dvec = dr - dT @ x
+        scores = [float(np.dot(p, base) + np.dot(p, dvec)) for p in Vl]
+        if tie_rel == 0.0:
+            best, arg = -math.inf, -1
+            for i, s in enumerate(scores):
+                if s > best:
+                    best, arg = s, i
+        else:
+            M = max(scores)
+            tol = tie_tolerance(M, tie_rel)
+            arg = next(i for i, s in enumerate(scores) if s >= M - tol)
+            best = scores[arg]
+        vals.append(best)
+        args.append(arg)
+    return np.array(vals), np.array(args, dtype=np.int64)
+
+
+def build_sasa_cut(coef: Coefficients, deltas, weights, x, V, tie_rel: float = 0.0):
+    """epigraph.jl:125-146.  Returns (alpha, beta, weight_mark, max_val, max_arg)."""
+    max_val, max_arg = argmax_procedure(coef, deltas, x, V, tie_rel)
+    Vl = list(V)
+    total = float(sum(weights))           # epi.total_scenario_weight (epigraph.jl:89)
+    alpha = 0.0
+    beta = np.zeros(len(x))
+    for i, (dr, dT) in enumerate(deltas):
+        dual = Vl[max_arg[i]]
+        p = weights[i] / total
+        alpha += p * float(np.dot(dual, coef.rhs + dr))
+        beta += -p * ((coef.transfer + dT).T @ dual)
+    return alpha, beta, total, max_val, max_arg
+
+
+def add_cut_discount(alpha, beta, discount, lower_bound):
+    """epigraph.jl:105-106 (the rhs/coefficients add_cut_to_master! writes)."""
+    return discount * alpha + (1 - discount) * lower_bound, discount * np.asarray(beta)
+
+
+def evaluate_epigraph(cuts, incumbent_cut, x, total_scenario_weight, lower_bound):
+    """epigraph.jl:177-203 (MIN_SENSE).  cuts = [(alpha, beta, weight_mark)]."""
+    best = lower_bound
+    for a, b, wm in cuts:
+        d = wm / total_scenario_weight
+        v = d * (a + float(np.dot(b, x))) + (1 - d) * lower_bound
+        if v > best:
+            best = v
+    if incumbent_cut is not None:
+        a, b, _ = incumbent_cut
+        v = a + float(np.dot(b, x))
+        if v > best:
+            best = v
+    return best

@@ -1,0 +1,87 @@
+"""ctypes binding of libtwosd_hip.so (the C ABI declared in include/twosd_hip.h).
+
+The shared library is built in-tree (``sqlp_amd/libtwosd_hip.so``, see
+``__graft_entry__.build()``).  There is no CPU fallback: if the library is missing or
+cannot be loaded, every call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtwosd_hip.so")
+
+TWOSD_OK = 0
+ERRORS = {-1: "TWOSD_E_ARG", -2: "TWOSD_E_DEVICE", -3: "TWOSD_E_STATE", -4: "TWOSD_E_LP",
+          -5: "TWOSD_E_UNSUPPORTED"}
+LP_OPTIMAL, LP_INFEASIBLE, LP_ITER_LIMIT, LP_NUMERIC = 0, 1, 2, 3
+
+# (name, restype, argtypes) for every symbol declared in include/twosd_hip.h
+P = C.c_void_p
+I = C.c_int
+D = C.c_double
+SIGNATURES = [
+    ("twosd_last_error", C.c_char_p, []),
+    ("twosd_version", C.c_char_p, []),
+    ("twosd_create", I, [I, P]),
+    ("twosd_destroy", I, [P]),
+    ("twosd_set_template", I, [P, I, I, I, P, P, P, P, P, P, P, P, P, P, P, I]),
+    ("twosd_set_random_positions", I, [P, I, P, P, I]),
+    ("twosd_compute_basis", I, [P, P, P]),
+    ("twosd_set_basis", I, [P, P]),
+    ("twosd_get_basis", I, [P, P]),
+    ("twosd_epigraph_create", I, [P, P]),
+    ("twosd_add_scenarios", I, [P, I, I, P, P]),
+    ("twosd_epigraph_info", I, [P, I, P, P]),
+    ("twosd_solve_batch", I, [P, I, P, I, I, P, P, P, P]),
+    ("twosd_solve_values", I, [P, P, I, P, P, P, P, P]),
+    ("twosd_dvs_push", I, [P, I, P, P, P]),
+    ("twosd_dvs_size", I, [P, P]),
+    ("twosd_dvs_get", I, [P, I, I, P]),
+    ("twosd_dvs_clear", I, [P]),
+    ("twosd_dvs_truncate", I, [P, I]),
+    ("twosd_solve_push", I, [P, I, P, I, I, P, P, P]),
+    ("twosd_build_cut", I, [P, I, P, D, P, P, P, P, P]),
+    ("twosd_cut_partial_len", I, [P, P, P]),
+    ("twosd_cut_partial", I, [P, I, P, D, D, P, P, P, P]),
+    ("twosd_cut_finalize", I, [P, P, P, P, P, P]),
+    ("twosd_last_timings", I, [P, P]),
+    ("twosd_last_lp_stats", I, [P, P, P]),
+]
+
+_lib = None
+
+
+class TwoSDError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+def load():
+    """Load the in-tree HIP library (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run __graft_entry__.build() (make -C sqlp_amd/csrc)")
+        lib = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(lib, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(rc):
+    if rc != TWOSD_OK:
+        raise TwoSDError(rc, load().twosd_last_error().decode())
+    return rc
+
+
+def ptr(a):
+    """Pointer to a contiguous numpy array (or None)."""
+    if a is None:
+        return None
+    return a.ctypes.data_as(C.c_void_p)

@@ -1,0 +1,522 @@
+// api.hip -- C ABI of libtwosd_hip.so (declared in include/twosd_hip.h).
+//
+// Owns the device-resident state of the TwoSD hot path on one MI355X:
+//   template (W CSC, q, bound types), shared warm-start basis (B0^{-1}, pi0), per-epigraph
+//   scenario pools (deltas, weights), the dual vertex set, and the LP/cut workspaces.
+// Every call is synchronous on the context's own HIP stream.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+#include "twosd_internal.h"
+#include "twosd_ctx.h"
+
+using namespace twosd;
+
+static thread_local std::string g_err;
+
+int twosd::fail(int code, const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                            \
+    do {                                                                                        \
+        hipError_t _e = (expr);                                                                 \
+        if (_e != hipSuccess) return fail(TWOSD_E_DEVICE, "%s: %s", #expr, hipGetErrorString(_e)); \
+    } while (0)
+
+template <typename T>
+static int dalloc(T **p, size_t count) {
+    if (*p) { hipFree(*p); *p = nullptr; }
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc((void **)p, sizeof(T) * count);
+    if (e != hipSuccess) return fail(TWOSD_E_DEVICE, "hipMalloc(%zu bytes): %s", sizeof(T) * count, hipGetErrorString(e));
+    return TWOSD_OK;
+}
+template <typename T>
+static void dfree(T *&p) {
+    if (p) hipFree(p);
+    p = nullptr;
+}
+
+// grow a device array to at least `count` elements, keeping `keep` elements
+template <typename T>
+int twosd::dgrow(T **p, size_t *cap, size_t count, size_t keep, hipStream_t s) {
+    if (count <= *cap && *p) return TWOSD_OK;
+    size_t ncap = std::max<size_t>(count, *cap * 2 + 1024);
+    T *np = nullptr;
+    hipError_t e = hipMalloc((void **)&np, sizeof(T) * ncap);
+    if (e != hipSuccess) return fail(TWOSD_E_DEVICE, "hipMalloc(%zu bytes): %s", sizeof(T) * ncap, hipGetErrorString(e));
+    if (*p && keep) {
+        e = hipMemcpyAsync(np, *p, sizeof(T) * keep, hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess) return fail(TWOSD_E_DEVICE, "grow copy: %s", hipGetErrorString(e));
+        hipStreamSynchronize(s);
+    }
+    if (*p) hipFree(*p);
+    *p = np;
+    *cap = ncap;
+    return TWOSD_OK;
+}
+template int twosd::dgrow<double>(double **, size_t *, size_t, size_t, hipStream_t);
+template int twosd::dgrow<int>(int **, size_t *, size_t, size_t, hipStream_t);
+template int twosd::dgrow<uint64_t>(uint64_t **, size_t *, size_t, size_t, hipStream_t);
+
+extern "C" const char *twosd_last_error(void) { return g_err.c_str(); }
+extern "C" const char *twosd_version(void) { return "twosd-mi355x 0.1 (gfx950)"; }
+
+extern "C" int twosd_create(int device, twosd_ctx **out) {
+    if (!out) return fail(TWOSD_E_ARG, "twosd_create: out is NULL");
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(TWOSD_E_ARG, "twosd_create: device %d of %d", device, ndev);
+    HIPCHK(hipSetDevice(device));
+    twosd_ctx *c = new twosd_ctx();
+    c->device = device;
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (int i = 0; i < 8; ++i) HIPCHK(hipEventCreate(&c->ev[i]));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    c->num_cus = prop.multiProcessorCount;
+    const char *km = getenv("TWOSD_KMAX");
+    if (km) c->kmax_override = atoi(km);
+    *out = c;
+    return TWOSD_OK;
+}
+
+static void free_template(twosd_ctx *c) {
+    dfree(c->d_colptr); dfree(c->d_rowidx); dfree(c->d_val); dfree(c->d_q); dfree(c->d_btype);
+    dfree(c->d_fixedmask); dfree(c->d_ubmask);
+    dfree(c->d_hb0); dfree(c->d_basic0); dfree(c->d_B0inv); dfree(c->d_B0invT); dfree(c->d_pi0);
+    dfree(c->d_xbase); dfree(c->d_B0K); dfree(c->d_eta); dfree(c->d_queue);
+    dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_dvtmp);
+    for (auto &e : c->epis) { dfree(e.d_dv); dfree(e.d_w); }
+    c->epis.clear();
+    c->out_cap = 0; c->eta_slots = 0; c->dvtmp_cap = 0;
+    dvs_free(c);
+    cut_free(c);
+    c->has_template = c->has_basis = false;
+}
+
+extern "C" int twosd_destroy(twosd_ctx *c) {
+    if (!c) return TWOSD_OK;
+    hipSetDevice(c->device);
+    free_template(c);
+    for (int i = 0; i < 8; ++i) hipEventDestroy(c->ev[i]);
+    hipStreamDestroy(c->stream);
+    delete c;
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_set_template(twosd_ctx *c, int m2, int n1, int n2, const int64_t *Tcp, const int64_t *Trv,
+                                  const double *Tnz, const int64_t *Wcp, const int64_t *Wrv, const double *Wnz,
+                                  const double *q, const double *r, const char *sense, const double *ylb,
+                                  const double *yub, int base) {
+    if (!c) return fail(TWOSD_E_ARG, "ctx is NULL");
+    if (m2 <= 0 || n1 < 0 || n2 <= 0 || !Wcp || !Wrv || !Wnz || !q || !r || !sense || (n1 > 0 && (!Tcp || !Trv || !Tnz)))
+        return fail(TWOSD_E_ARG, "twosd_set_template: bad sizes or NULL arrays");
+    if (base != 0 && base != 1) return fail(TWOSD_E_ARG, "index_base must be 0 or 1");
+    HIPCHK(hipSetDevice(c->device));
+    free_template(c);
+    HostLP &L = c->L;
+    L = HostLP();
+    L.m = m2; L.n = n2;
+    L.colptr.resize(n2 + 1);
+    for (int j = 0; j <= n2; ++j) L.colptr[j] = (int)(Wcp[j] - base);
+    const int nnzW = L.colptr[n2];
+    if (L.colptr[0] != 0 || nnzW < 0) return fail(TWOSD_E_ARG, "W colptr malformed");
+    L.rowidx.resize(nnzW); L.val.resize(nnzW);
+    for (int p = 0; p < nnzW; ++p) {
+        L.rowidx[p] = (int)(Wrv[p] - base);
+        L.val[p] = Wnz[p];
+        if (L.rowidx[p] < 0 || L.rowidx[p] >= m2) return fail(TWOSD_E_ARG, "W row index %d out of range", L.rowidx[p] + base);
+    }
+    L.q.assign(q, q + n2);
+    L.sense.assign(sense, sense + m2);
+    for (int i = 0; i < m2; ++i)
+        if (L.sense[i] != 'G' && L.sense[i] != 'L' && L.sense[i] != 'E')
+            return fail(TWOSD_E_ARG, "sense[%d] = '%c' (expected G/L/E)", i, L.sense[i]);
+    for (int j = 0; j < n2; ++j) {
+        const double lo = ylb ? ylb[j] : 0.0, hi = yub ? yub[j] : INFINITY;
+        if (lo != 0.0 || !std::isinf(hi) || hi < 0)
+            return fail(TWOSD_E_UNSUPPORTED, "y[%d] bounds [%g, %g]: only [0, +inf) is supported (subprob.jl:19-26 warns on these)", j, lo, hi);
+    }
+    c->n1 = n1;
+    c->r.assign(r, r + m2);
+    c->T.assign((size_t)m2 * n1, 0.0);   // dense T (m2 x n1) on the host for per-x setup
+    for (int j = 0; j < n1; ++j)
+        for (int64_t p = Tcp[j] - base; p < Tcp[j + 1] - base; ++p) {
+            const int i = (int)(Trv[p] - base);
+            if (i < 0 || i >= m2) return fail(TWOSD_E_ARG, "T row index out of range");
+            c->T[(size_t)i * n1 + j] = Tnz[p];
+        }
+    const int R = lp_rows_per_lane(m2);
+    if (R < 0) return fail(TWOSD_E_UNSUPPORTED, "m2 = %d exceeds the LP kernel envelope (%d rows)", m2, 64 * 16);
+    const int C = (n2 + m2 + 63) / 64;
+    if (C > kMaxColsPerLane) return fail(TWOSD_E_UNSUPPORTED, "n2 + m2 = %d exceeds %d columns", n2 + m2, 64 * kMaxColsPerLane);
+    c->R = R; c->MP = 64 * R; c->C = C;
+    // device template
+    int rc;
+    if ((rc = dalloc(&c->d_colptr, n2 + 1)) || (rc = dalloc(&c->d_rowidx, nnzW)) || (rc = dalloc(&c->d_val, nnzW)) ||
+        (rc = dalloc(&c->d_q, n2)) || (rc = dalloc(&c->d_btype, n2 + m2)) || (rc = dalloc(&c->d_fixedmask, 64)) ||
+        (rc = dalloc(&c->d_ubmask, 64)))
+        return rc;
+    std::vector<int8_t> bt(n2 + m2);
+    std::vector<uint64_t> fixedm(64, 0), ubm(64, 0);
+    for (int j = 0; j < n2 + m2; ++j) {
+        int b = BT_Y;
+        if (j >= n2) { char s = L.sense[j - n2]; b = s == 'G' ? BT_G : (s == 'L' ? BT_L : BT_E); }
+        bt[j] = (int8_t)b;
+    }
+    for (int j = 0; j < 64 * C; ++j) {
+        const int lane = j & 63, cs = j >> 6;
+        if (j >= n2 + m2 || bt[j] == BT_E) fixedm[lane] |= 1ull << cs;
+        else if (bt[j] == BT_G) ubm[lane] |= 1ull << cs;
+    }
+    HIPCHK(hipMemcpy(c->d_colptr, L.colptr.data(), sizeof(int) * (n2 + 1), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_rowidx, L.rowidx.data(), sizeof(int) * std::max(nnzW, 1), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_val, L.val.data(), sizeof(double) * std::max(nnzW, 1), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_q, L.q.data(), sizeof(double) * n2, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_btype, bt.data(), n2 + m2, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_fixedmask, fixedm.data(), sizeof(uint64_t) * 64, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_ubmask, ubm.data(), sizeof(uint64_t) * 64, hipMemcpyHostToDevice));
+    c->has_template = true;
+    c->k = 0;
+    c->pos_row.clear(); c->pos_col.clear();
+    if ((rc = dvs_init(c))) return rc;
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_set_random_positions(twosd_ctx *c, int k, const int *row, const int *col, int base) {
+    if (!c || !c->has_template) return fail(TWOSD_E_STATE, "set_random_positions: no template");
+    if (k < 0 || (k > 0 && (!row || !col))) return fail(TWOSD_E_ARG, "set_random_positions: bad arguments");
+    for (auto &e : c->epis)
+        if (e.count) return fail(TWOSD_E_STATE, "set_random_positions: epigraphs already hold scenarios");
+    c->pos_row.resize(k); c->pos_col.resize(k);
+    for (int e = 0; e < k; ++e) {
+        const int rr = row[e] - base;
+        const int cc = col[e] < 0 ? -1 : col[e] - base;
+        if (rr < 0 || rr >= c->L.m) return fail(TWOSD_E_ARG, "position %d: row %d out of range", e, row[e]);
+        if (cc >= c->n1) return fail(TWOSD_E_ARG, "position %d: column %d is not a first-stage column (KeyError in delta_coefficients, subprob.jl:116)", e, col[e]);
+        c->pos_row[e] = rr; c->pos_col[e] = cc;
+    }
+    c->k = k;
+    c->prep_valid = false;
+    cut_invalidate_pk(c);
+    return TWOSD_OK;
+}
+
+// template value at position e (RHS or T entry)
+static double template_value(const twosd_ctx *c, int e) {
+    const int rr = c->pos_row[e], cc = c->pos_col[e];
+    return cc < 0 ? c->r[rr] : c->T[(size_t)rr * c->n1 + cc];
+}
+
+// b = r - T x + effect of the element deltas dv (k)
+static void rhs_at(const twosd_ctx *c, const double *x, const double *dv, std::vector<double> &b) {
+    const int m = c->L.m, n1 = c->n1;
+    b.assign(c->r.begin(), c->r.end());
+    if (x)
+        for (int i = 0; i < m; ++i) {
+            double s = 0.0;
+            for (int j = 0; j < n1; ++j) s += c->T[(size_t)i * n1 + j] * x[j];
+            b[i] -= s;
+        }
+    if (dv)
+        for (int e = 0; e < c->k; ++e) {
+            const int cc = c->pos_col[e];
+            b[c->pos_row[e]] += cc < 0 ? dv[e] : -dv[e] * (x ? x[cc] : 0.0);
+        }
+}
+
+static int install_basis(twosd_ctx *c, const std::vector<int> &head) {
+    const HostLP &L = c->L;
+    const int m = L.m, n = L.n, MP = c->MP;
+    std::vector<char> seen(n + m, 0);
+    for (int i = 0; i < m; ++i) {
+        if (head[i] < 0 || head[i] >= n + m || seen[head[i]]) return fail(TWOSD_E_ARG, "basis head[%d] = %d invalid/duplicate", i, head[i]);
+        seen[head[i]] = 1;
+    }
+    std::vector<double> B, Binv;
+    basis_matrix(L, head, B);
+    if (!dense_inverse(m, B, Binv)) return fail(TWOSD_E_ARG, "basis matrix is singular");
+    std::vector<double> pi0;
+    const double dinf = basis_dual_infeasibility(L, head, Binv, pi0);
+    if (dinf > 1e-7) return fail(TWOSD_E_ARG, "basis is not dual feasible (max dual infeasibility %g)", dinf);
+    c->head0 = head;
+    c->B0inv = Binv;
+    std::vector<double> Bp((size_t)m * MP, 0.0), BTp((size_t)m * MP, 0.0), pip(MP, 0.0);
+    for (int i = 0; i < m; ++i)
+        for (int j = 0; j < m; ++j) {
+            Bp[(size_t)i * MP + j] = Binv[(size_t)i * m + j];
+            BTp[(size_t)j * MP + i] = Binv[(size_t)i * m + j];
+        }
+    for (int i = 0; i < m; ++i) pip[i] = pi0[i];
+    std::vector<int> hb(MP, -1);
+    std::vector<uint64_t> basic(64, 0);
+    std::vector<int8_t> bt(n + m);
+    HIPCHK(hipMemcpy(bt.data(), c->d_btype, n + m, hipMemcpyDeviceToHost));
+    for (int i = 0; i < m; ++i) {
+        hb[i] = head[i] * 4 + bt[head[i]];
+        basic[head[i] & 63] |= 1ull << (head[i] >> 6);
+    }
+    int rc;
+    if ((rc = dalloc(&c->d_hb0, MP)) || (rc = dalloc(&c->d_basic0, 64)) || (rc = dalloc(&c->d_B0inv, (size_t)m * MP)) ||
+        (rc = dalloc(&c->d_B0invT, (size_t)m * MP)) || (rc = dalloc(&c->d_pi0, MP)) || (rc = dalloc(&c->d_xbase, MP)))
+        return rc;
+    HIPCHK(hipMemcpy(c->d_hb0, hb.data(), sizeof(int) * MP, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_basic0, basic.data(), sizeof(uint64_t) * 64, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_B0inv, Bp.data(), sizeof(double) * m * MP, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_B0invT, BTp.data(), sizeof(double) * m * MP, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_pi0, pip.data(), sizeof(double) * MP, hipMemcpyHostToDevice));
+    c->has_basis = true;
+    c->prep_valid = false;
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_compute_basis(twosd_ctx *c, const double *x, const double *values) {
+    if (!c || !c->has_template) return fail(TWOSD_E_STATE, "compute_basis: no template");
+    HIPCHK(hipSetDevice(c->device));
+    std::vector<double> dv(c->k, 0.0);
+    if (values)
+        for (int e = 0; e < c->k; ++e) dv[e] = values[e] - template_value(c, e);
+    std::vector<double> b;
+    rhs_at(c, x, values ? dv.data() : nullptr, b);
+    std::vector<int> head;
+    double obj = 0;
+    int iters = 0;
+    std::string err;
+    const int st = setup_solve(c->L, b, head, obj, iters, err);
+    if (st != TWOSD_LP_OPTIMAL) return fail(TWOSD_E_LP, "compute_basis: %s (status %d)", err.c_str(), st);
+    return install_basis(c, head);
+}
+
+extern "C" int twosd_set_basis(twosd_ctx *c, const int *head) {
+    if (!c || !c->has_template || !head) return fail(TWOSD_E_STATE, "set_basis: no template / NULL head");
+    HIPCHK(hipSetDevice(c->device));
+    return install_basis(c, std::vector<int>(head, head + c->L.m));
+}
+
+extern "C" int twosd_get_basis(twosd_ctx *c, int *head) {
+    if (!c || !c->has_basis || !head) return fail(TWOSD_E_STATE, "get_basis: no basis");
+    std::copy(c->head0.begin(), c->head0.end(), head);
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_epigraph_create(twosd_ctx *c, int *epi_out) {
+    if (!c || !c->has_template || !epi_out) return fail(TWOSD_E_STATE, "epigraph_create: no template");
+    c->epis.emplace_back();
+    *epi_out = (int)c->epis.size() - 1;
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_add_scenarios(twosd_ctx *c, int epi, int N, const double *values, const double *weights) {
+    if (!c || !c->has_template) return fail(TWOSD_E_STATE, "add_scenarios: no template");
+    if (epi < 0 || epi >= (int)c->epis.size()) return fail(TWOSD_E_ARG, "add_scenarios: epigraph %d does not exist", epi);
+    if (N < 0 || (N > 0 && c->k > 0 && !values)) return fail(TWOSD_E_ARG, "add_scenarios: bad arguments");
+    if (N == 0) return TWOSD_OK;
+    HIPCHK(hipSetDevice(c->device));
+    EpiDevice &E = c->epis[epi];
+    const int k = c->k;
+    std::vector<double> dv((size_t)N * k), w(N, 1.0);
+    for (int s = 0; s < N; ++s)
+        for (int e = 0; e < k; ++e) dv[(size_t)s * k + e] = values[(size_t)s * k + e] - template_value(c, e);
+    if (weights)
+        for (int s = 0; s < N; ++s) {
+            if (!(weights[s] >= 0.0) || !std::isfinite(weights[s])) return fail(TWOSD_E_ARG, "weight[%d] = %g must be finite and >= 0", s, weights[s]);
+            w[s] = weights[s];
+        }
+    int rc;
+    if ((rc = dgrow(&E.d_dv, &E.dv_cap, (size_t)(E.count + N) * k, (size_t)E.count * k, c->stream))) return rc;
+    if ((rc = dgrow(&E.d_w, &E.w_cap, (size_t)(E.count + N), (size_t)E.count, c->stream))) return rc;
+    if (k) HIPCHK(hipMemcpy(E.d_dv + (size_t)E.count * k, dv.data(), sizeof(double) * N * k, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(E.d_w + E.count, w.data(), sizeof(double) * N, hipMemcpyHostToDevice));
+    E.w_host.insert(E.w_host.end(), w.begin(), w.end());
+    for (int s = 0; s < N; ++s) E.total_weight += w[s];   // epigraph.jl:89, in insertion order
+    E.count += N;
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_epigraph_info(twosd_ctx *c, int epi, int *ns, double *tw) {
+    if (!c || epi < 0 || epi >= (int)c->epis.size()) return fail(TWOSD_E_ARG, "epigraph_info: bad epigraph");
+    if (ns) *ns = c->epis[epi].count;
+    if (tw) *tw = c->epis[epi].total_weight;
+    return TWOSD_OK;
+}
+
+// per-x shared data: xbase = B0^{-1}(r - T x), B0K[e] = coef_e * B0^{-1}[:, row_e]
+int twosd::prepare_x(twosd_ctx *c, const double *x) {
+    const int m = c->L.m, MP = c->MP, k = c->k, n1 = c->n1;
+    if (c->prep_valid && c->prep_x.size() == (size_t)n1 && (n1 == 0 || std::equal(c->prep_x.begin(), c->prep_x.end(), x)))
+        return TWOSD_OK;
+    std::vector<double> b;
+    rhs_at(c, x, nullptr, b);
+    std::vector<double> xb(MP, 0.0), bk((size_t)std::max(k, 1) * MP, 0.0);
+    for (int i = 0; i < m; ++i) {
+        const double *row = &c->B0inv[(size_t)i * m];
+        double s = 0.0;
+        for (int j = 0; j < m; ++j) s += row[j] * b[j];
+        xb[i] = s;
+    }
+    for (int e = 0; e < k; ++e) {
+        const int rr = c->pos_row[e], cc = c->pos_col[e];
+        const double coef = cc < 0 ? 1.0 : -x[cc];
+        for (int i = 0; i < m; ++i) bk[(size_t)e * MP + i] = coef * c->B0inv[(size_t)i * m + rr];
+    }
+    int rc;
+    if ((rc = dalloc(&c->d_B0K, (size_t)std::max(k, 1) * MP))) return rc;
+    HIPCHK(hipMemcpyAsync(c->d_xbase, xb.data(), sizeof(double) * MP, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_B0K, bk.data(), sizeof(double) * std::max(k, 1) * MP, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->prep_x.assign(x, x + n1);
+    c->prep_valid = true;
+    return TWOSD_OK;
+}
+
+// Launch the LP kernel over N scenarios whose deltas start at d_dv (device); results in
+// c->d_obj / d_pi / d_y / d_status / d_iters [0, N).
+int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool want_pi, bool want_y) {
+    int rc;
+    if ((rc = prepare_x(c, x))) return rc;
+    const int m = c->L.m, n = c->L.n, MP = c->MP, R = c->R;
+    if (N > c->out_cap) {
+        size_t cap = std::max<size_t>(N, 1024);
+        if ((rc = dalloc(&c->d_obj, cap)) || (rc = dalloc(&c->d_status, cap)) || (rc = dalloc(&c->d_iters, cap))) return rc;
+        dfree(c->d_pi); dfree(c->d_y);
+        c->pi_cap = c->y_cap = 0;
+        c->out_cap = (int)cap;
+    }
+    if (want_pi && (size_t)N > c->pi_cap) {
+        if ((rc = dalloc(&c->d_pi, (size_t)c->out_cap * m))) return rc;
+        c->pi_cap = c->out_cap;
+    }
+    if (want_y && (size_t)N > c->y_cap) {
+        if ((rc = dalloc(&c->d_y, (size_t)c->out_cap * n))) return rc;
+        c->y_cap = c->out_cap;
+    }
+    const int kmax = c->kmax_override > 0 ? c->kmax_override : std::min(1024, std::max(64, 2 * m + 32));
+    const int bpc = lp_max_blocks_per_cu(R, kmax);
+    const int nblocks = std::max(1, std::min((N + kWavesPerBlock - 1) / kWavesPerBlock, bpc * c->num_cus));
+    const size_t slots = (size_t)nblocks * kWavesPerBlock;
+    if (slots > c->eta_slots || kmax != c->eta_kmax) {
+        if ((rc = dalloc(&c->d_eta, slots * kmax * MP))) return rc;
+        c->eta_slots = slots;
+        c->eta_kmax = kmax;
+    }
+    if (!c->d_queue && (rc = dalloc(&c->d_queue, 4))) return rc;
+    HIPCHK(hipMemsetAsync(c->d_queue, 0, sizeof(int) * 4, c->stream));
+    LpParams P{};
+    P.m = m; P.n = n; P.MP = MP; P.k = c->k; P.N = N; P.kmax = kmax; P.C = c->C;
+    P.colptr = c->d_colptr; P.rowidx = c->d_rowidx; P.val = c->d_val; P.q = c->d_q;
+    P.hb0 = c->d_hb0; P.basic0 = c->d_basic0; P.fixedmask = c->d_fixedmask; P.ubmask = c->d_ubmask; P.btype = c->d_btype;
+    P.B0inv = c->d_B0inv; P.B0invT = c->d_B0invT; P.B0K = c->d_B0K; P.pi0 = c->d_pi0; P.xbase = c->d_xbase;
+    P.dv = d_dv; P.eta = c->d_eta; P.queue = c->d_queue;
+    P.obj = c->d_obj; P.pi = want_pi ? c->d_pi : nullptr; P.y = want_y ? c->d_y : nullptr;
+    P.status = c->d_status; P.iters = c->d_iters;
+    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    HIPCHK(launch_lp(R, P, nblocks, lp_lds_bytes(R, kmax), c->stream));
+    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
+    c->t_us[0] = 1e3 * ms;
+    c->last_lp_N = N;
+    c->last_lp_blocks = nblocks;
+    return TWOSD_OK;
+}
+
+static int copy_lp_outputs(twosd_ctx *c, int N, double *obj, double *pi, double *y, int *status) {
+    if (obj) HIPCHK(hipMemcpy(obj, c->d_obj, sizeof(double) * N, hipMemcpyDeviceToHost));
+    if (pi) HIPCHK(hipMemcpy(pi, c->d_pi, sizeof(double) * N * c->L.m, hipMemcpyDeviceToHost));
+    if (y) HIPCHK(hipMemcpy(y, c->d_y, sizeof(double) * N * c->L.n, hipMemcpyDeviceToHost));
+    std::vector<int> st(N), its(N);
+    HIPCHK(hipMemcpy(st.data(), c->d_status, sizeof(int) * N, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(its.data(), c->d_iters, sizeof(int) * N, hipMemcpyDeviceToHost));
+    int64_t sum = 0; int mx = 0, bad = 0;
+    for (int s = 0; s < N; ++s) { sum += its[s]; mx = std::max(mx, its[s]); bad += st[s] != TWOSD_LP_OPTIMAL; }
+    c->last_pivots_sum = sum; c->last_pivots_max = mx;
+    if (status) std::copy(st.begin(), st.end(), status);
+    if (bad) return fail(TWOSD_E_LP, "%d of %d scenario LPs not optimal (see status[])", bad, N);
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_solve_batch(twosd_ctx *c, int epi, const double *x, int first, int count, double *obj,
+                                 double *pi, double *y, int *status) {
+    if (!c || !c->has_template) return fail(TWOSD_E_STATE, "solve_batch: no template");
+    if (!c->has_basis) return fail(TWOSD_E_STATE, "solve_batch: no warm-start basis (twosd_compute_basis / twosd_set_basis)");
+    if (epi < 0 || epi >= (int)c->epis.size()) return fail(TWOSD_E_ARG, "solve_batch: epigraph %d does not exist", epi);
+    const EpiDevice &E = c->epis[epi];
+    if (first < 0 || count < 0 || first + count > E.count) return fail(TWOSD_E_ARG, "solve_batch: range [%d,%d) outside %d scenarios", first, first + count, E.count);
+    if (!obj || !status || (c->n1 > 0 && !x)) return fail(TWOSD_E_ARG, "solve_batch: obj/status/x required");
+    if (count == 0) return TWOSD_OK;
+    HIPCHK(hipSetDevice(c->device));
+    int rc = run_lp(c, x, E.d_dv + (size_t)first * c->k, count, pi != nullptr, y != nullptr);
+    if (rc) return rc;
+    return copy_lp_outputs(c, count, obj, pi, y, status);
+}
+
+extern "C" int twosd_solve_values(twosd_ctx *c, const double *x, int N, const double *values, double *obj, double *pi,
+                                  double *y, int *status) {
+    if (!c || !c->has_template) return fail(TWOSD_E_STATE, "solve_values: no template");
+    if (!c->has_basis) return fail(TWOSD_E_STATE, "solve_values: no warm-start basis");
+    if (N < 0 || (N > 0 && c->k > 0 && !values) || !obj || !status || (c->n1 > 0 && !x)) return fail(TWOSD_E_ARG, "solve_values: bad arguments");
+    if (N == 0) return TWOSD_OK;
+    HIPCHK(hipSetDevice(c->device));
+    const int k = c->k;
+    std::vector<double> dv((size_t)N * std::max(k, 1), 0.0);
+    for (int s = 0; s < N; ++s)
+        for (int e = 0; e < k; ++e) dv[(size_t)s * k + e] = values[(size_t)s * k + e] - template_value(c, e);
+    int rc;
+    if ((rc = dgrow(&c->d_dvtmp, &c->dvtmp_cap, (size_t)N * std::max(k, 1), 0, c->stream))) return rc;
+    HIPCHK(hipMemcpy(c->d_dvtmp, dv.data(), sizeof(double) * dv.size(), hipMemcpyHostToDevice));
+    if ((rc = run_lp(c, x, c->d_dvtmp, N, pi != nullptr, y != nullptr))) return rc;
+    return copy_lp_outputs(c, N, obj, pi, y, status);
+}
+
+extern "C" int twosd_last_timings(twosd_ctx *c, double *us4) {
+    if (!c || !us4) return fail(TWOSD_E_ARG, "last_timings: NULL");
+    for (int i = 0; i < 4; ++i) us4[i] = c->t_us[i];
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_last_lp_stats(twosd_ctx *c, int64_t *sum, int *mx) {
+    if (!c) return fail(TWOSD_E_ARG, "last_lp_stats: NULL");
+    if (sum) *sum = c->last_pivots_sum;
+    if (mx) *mx = c->last_pivots_max;
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_solve_push(twosd_ctx *c, int epi, const double *x, int first, int count, double *obj, int *status,
+                                int *new_size) {
+    if (!c || !c->has_template) return fail(TWOSD_E_STATE, "solve_push: no template");
+    if (!c->has_basis) return fail(TWOSD_E_STATE, "solve_push: no warm-start basis");
+    if (epi < 0 || epi >= (int)c->epis.size()) return fail(TWOSD_E_ARG, "solve_push: epigraph %d does not exist", epi);
+    const EpiDevice &E = c->epis[epi];
+    if (first < 0 || count < 0 || first + count > E.count) return fail(TWOSD_E_ARG, "solve_push: range outside the epigraph");
+    if (c->n1 > 0 && !x) return fail(TWOSD_E_ARG, "solve_push: x is NULL");
+    if (count == 0) { if (new_size) *new_size = c->dvs.size; return TWOSD_OK; }
+    HIPCHK(hipSetDevice(c->device));
+    int rc = run_lp(c, x, E.d_dv + (size_t)first * c->k, count, true, false);
+    if (rc) return rc;
+    rc = copy_lp_outputs(c, count, obj, nullptr, nullptr, status);
+    if (rc) return rc;   // some LP not optimal: nothing pushed
+    HIPCHK(hipEventRecord(c->ev[2], c->stream));
+    if ((rc = dvs_push_device(c, count, c->d_pi, nullptr))) return rc;
+    HIPCHK(hipEventRecord(c->ev[3], c->stream));
+    HIPCHK(hipEventSynchronize(c->ev[3]));
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->ev[2], c->ev[3]);
+    c->t_us[1] = 1e3 * ms;
+    if (new_size) *new_size = c->dvs.size;
+    return TWOSD_OK;
+}

@@ -1,0 +1,595 @@
+// cut_kernel.hip -- argmax_procedure + build_sasa_cut on gfx950 (fp64 MFMA).
+//
+// Reference: argmax_procedure (src/sd_algorithm/subprob.jl:141-169) and build_sasa_cut
+// (src/sd_algorithm/epigraph.jl:125-146).  For scenario w (element deltas dv[w,e] at
+// rows row_e; coef_e = 1 for an RHS element, -x[col_e] for a T element):
+//     score[w,v] = pi_v . (r - T x)  +  sum_e pi_v[row_e] * coef_e * dv[w,e]
+//                = base[v]          +  (DR_w . PK_v)           (an N x |V| x k GEMM)
+//     a(w)  = lowest v within tie_rel*(1+|max|) of max_v score[w,v]   (tie_rel=0: the
+//             reference's strict '>' first maximum)
+//     p_w   = weight_w / total_weight
+//     alpha = g.r + sum_{e RHS} S_e,   beta = -T' g - sum_{e T} S_e e_{col_e}
+// with g = sum_v h_v pi_v,  h_v = sum_{w: a(w)=v} p_w,  S_e = sum_w p_w PK[a(w),e] dv[w,e].
+// (Same value as the reference's per-scenario loop, re-associated.)
+//
+// Kernels:
+//   cut_pk_kernel      PK (|V| x k4 row-major) and PKT (k4 x vcap) gathers of new vertices
+//   cut_vbase_kernel   base[v] = pi_v . (r - T x)                (8|V|(m+1) bytes)
+//   cut_argmax_kernel  MFMA score tiles (16 scenarios x 16 vertices x 4 k per
+//                      v_mfma_f64_16x16x4f64), vertex chunks staged in LDS (k-major,
+//                      bank-conflict-free stride), running max/argmax per scenario in
+//                      registers; per-wave partial sums; h via uint64 fixed-point atomics
+//                      (exact and order independent -> identical on any rank count)
+//   cut_fixup_kernel   scenarios whose running argmax slid within the tolerance band are
+//                      re-decided by the exact two-pass rule (sequential fp64)
+//   cut_reduce_kernel  deterministic fixed-order sum of the partial slots
+//   cut_g_kernel(s)    g = sum_v h_v pi_v (two-level, fixed order)
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <algorithm>
+#include <vector>
+#include "twosd_ctx.h"
+
+namespace twosd {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int kVT = 32;            // vertices per LDS chunk (2 MFMA column tiles)
+constexpr int kLdsStride = 48;     // doubles per k-row in LDS (== 16 mod 32: conflict-free b64 reads)
+constexpr double kFix = 4611686018427387904.0;   // 2^62 fixed-point scale of p_w
+
+struct CutParams {
+    int N, k, k4, nv, vcap, m;
+    double tie_rel, inv_total;
+    const double *dv;      // N x k
+    const double *w;       // N
+    const double *coef;    // k4 (zero padded)
+    const double *PK;      // nv x k4
+    const double *PKT;     // k4 x vcap
+    const double *base;    // nv
+    int *arg; double *val; int *flag;   // N
+    unsigned long long *hist;           // nv (fixed point)
+    double *partial;       // slots x (k + 1): [sum p*val, S_0..S_{k-1}]
+};
+
+__global__ void cut_pk_kernel(int from, int to, int m, int k, int k4, int vcap, const int *__restrict__ rows,
+                              const double *__restrict__ V, double *__restrict__ PK, double *__restrict__ PKT) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int total = (to - from) * k4;
+    if (idx >= total) return;
+    const int v = from + idx / k4, e = idx % k4;
+    const double x = e < k ? V[(size_t)v * m + rows[e]] : 0.0;
+    PK[(size_t)v * k4 + e] = x;
+    PKT[(size_t)e * vcap + v] = x;
+}
+
+__global__ void __launch_bounds__(256) cut_vbase_kernel(int nv, int m, const double *__restrict__ V,
+                                                        const double *__restrict__ bvec, double *__restrict__ base) {
+    const int lane = threadIdx.x & 63;
+    const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int nw = (gridDim.x * blockDim.x) >> 6;
+    for (int v = gw; v < nv; v += nw) {
+        const double *p = V + (size_t)v * m;
+        double s = 0.0;
+        for (int i = lane; i < m; i += 64) s = fma(p[i], bvec[i], s);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        if (lane == 0) base[v] = s;
+    }
+}
+
+__device__ __forceinline__ double tolf(double M, double rel) { return rel * (1.0 + fabs(M)); }
+
+template <int KB>
+__global__ void __launch_bounds__(256) cut_argmax_kernel(CutParams P) {
+    __shared__ double Bs[4 * KB * kLdsStride];
+    __shared__ double bs[kVT];
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int g = lane >> 4, j = lane & 15;
+    const int ntiles = (P.N + 63) / 64;
+    const int nchunks = (P.nv + kVT - 1) / kVT;
+    // per-wave partial sums (lanes stride over elements)
+    double pv_sum = 0.0;
+    double Sacc[2] = {0.0, 0.0};
+
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int s0 = tile * 64 + wid * 16;
+        // A fragments: lane holds DR[s0 + j][4kb + g] * coef
+        double a[KB];
+        {
+            const int s = s0 + j;
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb) {
+                const int e = 4 * kb + g;
+                a[kb] = (s < P.N && e < P.k) ? P.dv[(size_t)s * P.k + e] * P.coef[e] : 0.0;
+            }
+        }
+        double M[4], SV[4];
+        int I[4], F[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { M[r] = -INFINITY; SV[r] = -INFINITY; I[r] = -1; F[r] = 0; }
+
+        for (int ch = 0; ch < nchunks; ++ch) {
+            const int v0 = ch * kVT;
+            __syncthreads();
+            // stage PKT[0..4KB)[v0..v0+VT) -> Bs[kk][v] and base
+            for (int idx = threadIdx.x; idx < 4 * KB * kVT; idx += 256) {
+                const int kk = idx / kVT, vv = idx % kVT;
+                const int v = v0 + vv;
+                Bs[kk * kLdsStride + vv] = (v < P.nv && kk < P.k4) ? P.PKT[(size_t)kk * P.vcap + v] : 0.0;
+            }
+            if (threadIdx.x < kVT) {
+                const int v = v0 + threadIdx.x;
+                bs[threadIdx.x] = v < P.nv ? P.base[v] : -INFINITY;
+            }
+            __syncthreads();
+            d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb) {
+                const double b0 = Bs[(4 * kb + g) * kLdsStride + j];
+                const double b1 = Bs[(4 * kb + g) * kLdsStride + 16 + j];
+                acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[kb], b0, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[kb], b1, acc1, 0, 0, 0);
+            }
+            // epilogue: rows i = g + 4r, columns v0 + j (tile 0) and v0 + 16 + j (tile 1)
+            const int va = v0 + j, vb = v0 + 16 + j;
+            const double ba = bs[j], bb = bs[16 + j];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double sa = va < P.nv ? ba + acc0[r] : -INFINITY;
+                const double sb = vb < P.nv ? bb + acc1[r] : -INFINITY;
+                double mt = fmax(sa, sb);
+#pragma unroll
+                for (int o = 8; o > 0; o >>= 1) mt = fmax(mt, __shfl_xor(mt, o));
+                const double tt = tolf(mt, P.tie_rel);
+                int it = 0x7fffffff;
+                double st = -INFINITY;
+                if (sb >= mt - tt) { it = vb; st = sb; }
+                if (sa >= mt - tt) { it = va; st = sa; }
+#pragma unroll
+                for (int o = 8; o > 0; o >>= 1) {
+                    const int i2 = __shfl_xor(it, o);
+                    const double s2 = __shfl_xor(st, o);
+                    if (i2 < it) { it = i2; st = s2; }
+                }
+                if (mt == -INFINITY) continue;
+                const double tM = tolf(M[r], P.tie_rel);
+                if (mt > M[r] + tM) { M[r] = mt; I[r] = it; SV[r] = st; }
+                else if (mt > M[r]) {
+                    // max slides up inside the tolerance band
+                    if (!(SV[r] >= mt - tolf(mt, P.tie_rel))) F[r] = 1;
+                    M[r] = mt;
+                }
+            }
+        }
+        // write results, accumulate partials for decided rows
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int s = s0 + g + 4 * r;
+            if (j == 0 && s < P.N) {
+                P.arg[s] = I[r];
+                P.val[s] = SV[r];
+                P.flag[s] = F[r];
+            }
+        }
+        // partial sums: loop the 16 rows of this wave (uniform)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg) {
+                const int s = s0 + gg + 4 * r;
+                const int ai = __shfl(I[r], gg * 16);
+                const int fl = __shfl(F[r], gg * 16);
+                const double vl = __shfl(SV[r], gg * 16);
+                if (s >= P.N || fl || ai < 0) continue;
+                const double p = P.w[s] * P.inv_total;
+                if (lane == 0) {
+                    pv_sum = fma(p, vl, pv_sum);
+                    atomicAdd(&P.hist[ai], (unsigned long long)__double2ull_rn(p * kFix));
+                }
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const int e = lane + 64 * t;
+                    if (e < P.k) Sacc[t] = fma(p * P.PK[(size_t)ai * P.k4 + e], P.dv[(size_t)s * P.k + e], Sacc[t]);
+                }
+            }
+        }
+    }
+    const int slot = blockIdx.x * 4 + wid;
+    double *out = P.partial + (size_t)slot * (P.k + 1);
+    if (lane == 0) out[0] = pv_sum;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int e = lane + 64 * t;
+        if (e < P.k) out[1 + e] = Sacc[t];
+    }
+}
+
+// exact two-pass rule for flagged scenarios; one wavefront per scenario
+__global__ void __launch_bounds__(256) cut_fixup_kernel(CutParams P, int slot0) {
+    const int lane = threadIdx.x & 63;
+    const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int nw = (gridDim.x * blockDim.x) >> 6;
+    double pv_sum = 0.0, Sacc[2] = {0.0, 0.0};
+    for (int s = gw; s < P.N; s += nw) {
+        if (!P.flag[s]) continue;
+        // pass 1: max over v (lanes stride vertices)
+        double mx = -INFINITY;
+        for (int v = lane; v < P.nv; v += 64) {
+            double sc = P.base[v];
+            for (int e = 0; e < P.k; ++e) sc = fma(P.PK[(size_t)v * P.k4 + e], P.dv[(size_t)s * P.k + e] * P.coef[e], sc);
+            mx = fmax(mx, sc);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+        const double tl = tolf(mx, P.tie_rel);
+        int best = 0x7fffffff;
+        double bv = -INFINITY;
+        for (int v = lane; v < P.nv; v += 64) {
+            double sc = P.base[v];
+            for (int e = 0; e < P.k; ++e) sc = fma(P.PK[(size_t)v * P.k4 + e], P.dv[(size_t)s * P.k + e] * P.coef[e], sc);
+            if (sc >= mx - tl && v < best) { best = v; bv = sc; }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const int b2 = __shfl_xor(best, o);
+            const double v2 = __shfl_xor(bv, o);
+            if (b2 < best) { best = b2; bv = v2; }
+        }
+        const double p = P.w[s] * P.inv_total;
+        if (lane == 0) {
+            P.arg[s] = best;
+            P.val[s] = bv;
+            pv_sum = fma(p, bv, pv_sum);
+            atomicAdd(&P.hist[best], (unsigned long long)__double2ull_rn(p * kFix));
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int e = lane + 64 * t;
+            if (e < P.k) Sacc[t] = fma(p * P.PK[(size_t)best * P.k4 + e], P.dv[(size_t)s * P.k + e], Sacc[t]);
+        }
+    }
+    double *out = P.partial + (size_t)(slot0 + gw) * (P.k + 1);
+    if (lane == 0) out[0] = pv_sum;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int e = lane + 64 * t;
+        if (e < P.k) out[1 + e] = Sacc[t];
+    }
+}
+
+// sums[c] = sum over slots (in slot order) of partial[slot][c], c < k+1
+__global__ void cut_reduce_kernel(int slots, int width, const double *__restrict__ partial, double *__restrict__ sums) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= width) return;
+    double s = 0.0;
+    for (int i = 0; i < slots; ++i) s += partial[(size_t)i * width + c];
+    sums[c] = s;
+}
+
+// gpart[b][i] = sum_{v in chunk b} h_v * 2^-62 * V[v][i]
+__global__ void cut_g_partial_kernel(int nv, int m, int chunk, const unsigned long long *__restrict__ hist,
+                                     const double *__restrict__ V, double *__restrict__ gpart) {
+    const int b = blockIdx.x;
+    const int v0 = b * chunk, v1 = min(nv, v0 + chunk);
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        double s = 0.0;
+        for (int v = v0; v < v1; ++v) {
+            const unsigned long long h = hist[v];
+            if (h) s = fma((double)h * (1.0 / kFix), V[(size_t)v * m + i], s);
+        }
+        gpart[(size_t)b * m + i] = s;
+    }
+}
+
+__global__ void cut_g_final_kernel(int nb, int m, const double *__restrict__ gpart, double *__restrict__ gout) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    double s = 0.0;
+    for (int b = 0; b < nb; ++b) s += gpart[(size_t)b * m + i];
+    gout[i] = s;
+}
+
+// ---------------------------------------------------------------------------------
+struct CutWs {
+    double *PK = nullptr, *PKT = nullptr;
+    int pk_count = 0, pk_vcap = 0, pk_k4 = 0;
+    size_t pk_cap = 0;
+    int *rows = nullptr;
+    double *coef = nullptr, *bvec = nullptr, *base = nullptr, *partial = nullptr, *sums = nullptr;
+    double *gpart = nullptr, *g = nullptr;
+    int *arg = nullptr, *flag = nullptr;
+    double *val = nullptr;
+    unsigned long long *hist = nullptr;
+    size_t base_cap = 0, part_cap = 0, n_cap = 0, hist_cap = 0, gpart_cap = 0;
+    int m = 0;
+};
+
+static CutWs *cws(twosd_ctx *c) {
+    if (!c->cut_ws) c->cut_ws = new CutWs();
+    return (CutWs *)c->cut_ws;
+}
+
+void cut_free(twosd_ctx *c) {
+    if (!c->cut_ws) return;
+    CutWs *w = (CutWs *)c->cut_ws;
+    hipFree(w->PK); hipFree(w->PKT); hipFree(w->rows); hipFree(w->coef); hipFree(w->bvec); hipFree(w->base);
+    hipFree(w->partial); hipFree(w->sums); hipFree(w->gpart); hipFree(w->g); hipFree(w->arg); hipFree(w->flag);
+    hipFree(w->val); hipFree(w->hist);
+    delete w;
+    c->cut_ws = nullptr;
+}
+
+void cut_invalidate_pk(twosd_ctx *c) {
+    if (!c->cut_ws) return;
+    CutWs *w = (CutWs *)c->cut_ws;
+    w->pk_count = 0;
+    if (w->rows) hipFree(w->rows);
+    w->rows = nullptr;   // forces re-upload of the element rows
+}
+
+#define HIPCHK(expr)                                                                               \
+    do {                                                                                           \
+        hipError_t _e = (expr);                                                                    \
+        if (_e != hipSuccess) return fail(TWOSD_E_DEVICE, "%s: %s", #expr, hipGetErrorString(_e)); \
+    } while (0)
+
+template <typename T>
+static int realloc_dev(T **p, size_t n) {
+    if (*p) hipFree(*p);
+    *p = nullptr;
+    hipError_t e = hipMalloc((void **)p, sizeof(T) * std::max<size_t>(n, 1));
+    if (e != hipSuccess) return fail(TWOSD_E_DEVICE, "cut workspace hipMalloc(%zu): %s", sizeof(T) * n, hipGetErrorString(e));
+    return TWOSD_OK;
+}
+
+static int kb_for(int k4) {
+    static const int KBs[] = {1, 2, 4, 6, 8, 12, 16, 24, 30, 32};
+    for (int kb : KBs)
+        if (4 * kb >= k4) return kb;
+    return -1;
+}
+
+template <int KB>
+static void launch_argmax_t(const CutParams &P, int nblocks, hipStream_t s) {
+    hipLaunchKernelGGL(cut_argmax_kernel<KB>, dim3(nblocks), dim3(256), 0, s, P);
+}
+
+static void launch_argmax(int KB, const CutParams &P, int nblocks, hipStream_t s) {
+    switch (KB) {
+        case 1: launch_argmax_t<1>(P, nblocks, s); break;
+        case 2: launch_argmax_t<2>(P, nblocks, s); break;
+        case 4: launch_argmax_t<4>(P, nblocks, s); break;
+        case 6: launch_argmax_t<6>(P, nblocks, s); break;
+        case 8: launch_argmax_t<8>(P, nblocks, s); break;
+        case 12: launch_argmax_t<12>(P, nblocks, s); break;
+        case 16: launch_argmax_t<16>(P, nblocks, s); break;
+        case 24: launch_argmax_t<24>(P, nblocks, s); break;
+        case 30: launch_argmax_t<30>(P, nblocks, s); break;
+        case 32: launch_argmax_t<32>(P, nblocks, s); break;
+    }
+}
+
+// bring PK/PKT up to date with the vertex set
+static int update_pk(twosd_ctx *c) {
+    CutWs *w = cws(c);
+    const int nv = c->dvs.size, k = c->k, k4 = (std::max(k, 1) + 3) & ~3, m = c->L.m;
+    int rc;
+    if (!w->rows || w->pk_k4 != k4 || w->m != m) {
+        if ((rc = realloc_dev(&w->rows, std::max(k, 1)))) return rc;
+        if (k) HIPCHK(hipMemcpy(w->rows, c->pos_row.data(), sizeof(int) * k, hipMemcpyHostToDevice));
+        w->pk_count = 0;
+        w->pk_k4 = k4;
+        w->m = m;
+    }
+    if (nv > w->pk_vcap) {
+        const int vcap = std::max(nv, 2 * w->pk_vcap + 256);
+        if ((rc = realloc_dev(&w->PK, (size_t)vcap * k4)) || (rc = realloc_dev(&w->PKT, (size_t)vcap * k4))) return rc;
+        w->pk_vcap = vcap;
+        w->pk_count = 0;
+    }
+    if (w->pk_count > nv) w->pk_count = 0;
+    if (w->pk_count < nv) {
+        const int total = (nv - w->pk_count) * k4;
+        hipLaunchKernelGGL(cut_pk_kernel, dim3((total + 255) / 256), dim3(256), 0, c->stream, w->pk_count, nv, m, k, k4,
+                           w->pk_vcap, w->rows, c->dvs.V, w->PK, w->PKT);
+        HIPCHK(hipGetLastError());
+        w->pk_count = nv;
+    }
+    return TWOSD_OK;
+}
+
+// argmax + partial sums over scenarios [0, N) of epigraph epi at x.  Fills w->hist (nv),
+// w->sums (k+1), w->arg / w->val.  total_weight: global total scenario weight.
+static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_rel, double total_weight,
+                            unsigned long long *d_hist, double *d_sums) {
+    CutWs *w = cws(c);
+    const EpiDevice &E = c->epis[epi];
+    const int N = E.count, k = c->k, m = c->L.m, nv = c->dvs.size, n1 = c->n1;
+    const int k4 = (std::max(k, 1) + 3) & ~3;
+    const int KB = kb_for(k4);
+    if (KB < 0) return fail(TWOSD_E_UNSUPPORTED, "k = %d random elements exceeds the cut kernel envelope (128)", k);
+    int rc;
+    if ((rc = update_pk(c))) return rc;
+    // host: bvec = r - T x, coef
+    std::vector<double> bvec(m), coef(k4, 0.0);
+    for (int i = 0; i < m; ++i) {
+        double s = 0.0;
+        for (int jj = 0; jj < n1; ++jj) s += c->T[(size_t)i * n1 + jj] * x[jj];
+        bvec[i] = c->r[i] - s;
+    }
+    for (int e = 0; e < k; ++e) coef[e] = c->pos_col[e] < 0 ? 1.0 : -x[c->pos_col[e]];
+    if (!w->coef || !w->bvec || w->m != m) {
+        if ((rc = realloc_dev(&w->coef, 256)) || (rc = realloc_dev(&w->bvec, m)) || (rc = realloc_dev(&w->g, m)) ||
+            (rc = realloc_dev(&w->sums, 256)))
+            return rc;
+    }
+    if ((size_t)nv > w->base_cap) {
+        if ((rc = realloc_dev(&w->base, nv))) return rc;
+        w->base_cap = nv;
+    }
+    if ((size_t)N > w->n_cap) {
+        if ((rc = realloc_dev(&w->arg, N)) || (rc = realloc_dev(&w->val, N)) || (rc = realloc_dev(&w->flag, N))) return rc;
+        w->n_cap = N;
+    }
+    HIPCHK(hipMemcpyAsync(w->coef, coef.data(), sizeof(double) * k4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(w->bvec, bvec.data(), sizeof(double) * m, hipMemcpyHostToDevice, c->stream));
+    const int ntiles = (N + 63) / 64;
+    const int nblocks = std::max(1, std::min(ntiles, 3 * c->num_cus));
+    const int fix_blocks = std::max(1, std::min((N + 3) / 4, c->num_cus));
+    const size_t slots = (size_t)nblocks * 4 + (size_t)fix_blocks * 4;
+    if (slots * (k + 1) > w->part_cap) {
+        if ((rc = realloc_dev(&w->partial, slots * (k + 1)))) return rc;
+        w->part_cap = slots * (k + 1);
+    }
+    HIPCHK(hipMemsetAsync(d_hist, 0, sizeof(unsigned long long) * std::max(nv, 1), c->stream));
+    hipLaunchKernelGGL(cut_vbase_kernel, dim3(std::max(1, std::min((nv + 3) / 4, 4096))), dim3(256), 0, c->stream, nv, m,
+                       c->dvs.V, w->bvec, w->base);
+    CutParams P{};
+    P.N = N; P.k = k; P.k4 = k4; P.nv = nv; P.vcap = w->pk_vcap; P.m = m;
+    P.tie_rel = tie_rel; P.inv_total = 1.0 / total_weight;
+    P.dv = E.d_dv; P.w = E.d_w; P.coef = w->coef; P.PK = w->PK; P.PKT = w->PKT; P.base = w->base;
+    P.arg = w->arg; P.val = w->val; P.flag = w->flag; P.hist = d_hist; P.partial = w->partial;
+    launch_argmax(KB, P, nblocks, c->stream);
+    hipLaunchKernelGGL(cut_fixup_kernel, dim3(fix_blocks), dim3(256), 0, c->stream, P, nblocks * 4);
+    hipLaunchKernelGGL(cut_reduce_kernel, dim3((k + 1 + 63) / 64), dim3(64), 0, c->stream, (int)slots, k + 1, w->partial,
+                       d_sums);
+    HIPCHK(hipGetLastError());
+    return TWOSD_OK;
+}
+
+// g = sum_v h_v pi_v, then alpha / beta on the host
+static int cut_finalize_impl(twosd_ctx *c, const double *x, const unsigned long long *d_hist, const double *d_sums,
+                             double *alpha, double *beta) {
+    CutWs *w = cws(c);
+    const int nv = c->dvs.size, m = c->L.m, k = c->k, n1 = c->n1;
+    (void)x;
+    const int chunk = 256;
+    const int nb = std::max(1, (nv + chunk - 1) / chunk);
+    int rc;
+    if ((size_t)nb * m > w->gpart_cap) {
+        if ((rc = realloc_dev(&w->gpart, (size_t)nb * m))) return rc;
+        w->gpart_cap = (size_t)nb * m;
+    }
+    hipLaunchKernelGGL(cut_g_partial_kernel, dim3(nb), dim3(256), 0, c->stream, nv, m, chunk, d_hist, c->dvs.V, w->gpart);
+    hipLaunchKernelGGL(cut_g_final_kernel, dim3((m + 255) / 256), dim3(256), 0, c->stream, nb, m, w->gpart, w->g);
+    HIPCHK(hipGetLastError());
+    std::vector<double> g(m), sums(k + 1);
+    HIPCHK(hipMemcpyAsync(g.data(), w->g, sizeof(double) * m, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(sums.data(), d_sums, sizeof(double) * (k + 1), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    double a = 0.0;
+    for (int i = 0; i < m; ++i) a += g[i] * c->r[i];
+    for (int jj = 0; jj < n1; ++jj) {
+        double s = 0.0;
+        for (int i = 0; i < m; ++i) s += c->T[(size_t)i * n1 + jj] * g[i];
+        beta[jj] = -s;
+    }
+    for (int e = 0; e < k; ++e) {
+        if (c->pos_col[e] < 0) a += sums[1 + e];
+        else beta[c->pos_col[e]] -= sums[1 + e];
+    }
+    *alpha = a;
+    return TWOSD_OK;
+}
+
+}  // namespace twosd
+
+using namespace twosd;
+
+static int check_cut_args(twosd_ctx *c, int epi, const double *x) {
+    if (!c || !c->has_template) return fail(TWOSD_E_STATE, "build_cut: no template");
+    if (epi < 0 || epi >= (int)c->epis.size()) return fail(TWOSD_E_ARG, "build_cut: epigraph %d does not exist", epi);
+    if (c->n1 > 0 && !x) return fail(TWOSD_E_ARG, "build_cut: x is NULL");
+    if (c->dvs.size == 0)
+        return fail(TWOSD_E_STATE, "build_cut: the dual vertex set is empty (UndefRefError in build_sasa_cut, epigraph.jl:140)");
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_build_cut(twosd_ctx *c, int epi, const double *x, double tie_rel, double *alpha, double *beta,
+                               double *weight_mark, double *max_val, int *max_arg) {
+    int rc = check_cut_args(c, epi, x);
+    if (rc) return rc;
+    if (!alpha || (c->n1 > 0 && !beta)) return fail(TWOSD_E_ARG, "build_cut: alpha/beta NULL");
+    HIPCHK(hipSetDevice(c->device));
+    const EpiDevice &E = c->epis[epi];
+    CutWs *w = cws(c);
+    const int nv = c->dvs.size;
+    if ((size_t)nv > w->hist_cap) {
+        if ((rc = realloc_dev(&w->hist, nv))) return rc;
+        w->hist_cap = nv;
+    }
+    if (E.count == 0 || E.total_weight <= 0.0) {
+        // no scenarios: the reference returns the zero cut with weight_mark = total weight
+        *alpha = 0.0;
+        for (int j = 0; j < c->n1; ++j) beta[j] = 0.0;
+        if (weight_mark) *weight_mark = E.total_weight;
+        return TWOSD_OK;
+    }
+    HIPCHK(hipEventRecord(c->ev[4], c->stream));
+    if ((rc = cut_partial_impl(c, epi, x, tie_rel, E.total_weight, w->hist, w->sums))) return rc;
+    HIPCHK(hipEventRecord(c->ev[5], c->stream));
+    if ((rc = cut_finalize_impl(c, x, w->hist, w->sums, alpha, beta))) return rc;
+    HIPCHK(hipEventRecord(c->ev[6], c->stream));
+    HIPCHK(hipEventSynchronize(c->ev[6]));
+    float ms1 = 0, ms2 = 0;
+    hipEventElapsedTime(&ms1, c->ev[4], c->ev[5]);
+    hipEventElapsedTime(&ms2, c->ev[5], c->ev[6]);
+    c->t_us[2] = 1e3 * ms1;
+    c->t_us[3] = 1e3 * ms2;
+    if (weight_mark) *weight_mark = E.total_weight;
+    if (max_val) HIPCHK(hipMemcpy(max_val, w->val, sizeof(double) * E.count, hipMemcpyDeviceToHost));
+    if (max_arg) HIPCHK(hipMemcpy(max_arg, w->arg, sizeof(int) * E.count, hipMemcpyDeviceToHost));
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_cut_partial_len(twosd_ctx *c, int64_t *n_u64, int64_t *n_f64) {
+    if (!c) return fail(TWOSD_E_ARG, "cut_partial_len: NULL");
+    if (n_u64) *n_u64 = std::max(c->dvs.size, 1);
+    if (n_f64) *n_f64 = c->k + 1;
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_cut_partial(twosd_ctx *c, int epi, const double *x, double tie_rel, double total_weight,
+                                 uint64_t *d_hist, double *d_sums, double *max_val, int *max_arg) {
+    int rc = check_cut_args(c, epi, x);
+    if (rc) return rc;
+    if (!d_hist || !d_sums) return fail(TWOSD_E_ARG, "cut_partial: device buffers NULL");
+    if (!(total_weight > 0.0)) return fail(TWOSD_E_ARG, "cut_partial: total_weight must be > 0");
+    HIPCHK(hipSetDevice(c->device));
+    const EpiDevice &E = c->epis[epi];
+    if (E.count == 0) {
+        HIPCHK(hipMemsetAsync(d_hist, 0, sizeof(uint64_t) * std::max(c->dvs.size, 1), c->stream));
+        HIPCHK(hipMemsetAsync(d_sums, 0, sizeof(double) * (c->k + 1), c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return TWOSD_OK;
+    }
+    HIPCHK(hipEventRecord(c->ev[4], c->stream));
+    if ((rc = cut_partial_impl(c, epi, x, tie_rel, total_weight, (unsigned long long *)d_hist, d_sums))) return rc;
+    HIPCHK(hipEventRecord(c->ev[5], c->stream));
+    HIPCHK(hipEventSynchronize(c->ev[5]));
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->ev[4], c->ev[5]);
+    c->t_us[2] = 1e3 * ms;
+    CutWs *w = cws(c);
+    if (max_val) HIPCHK(hipMemcpy(max_val, w->val, sizeof(double) * E.count, hipMemcpyDeviceToHost));
+    if (max_arg) HIPCHK(hipMemcpy(max_arg, w->arg, sizeof(int) * E.count, hipMemcpyDeviceToHost));
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_cut_finalize(twosd_ctx *c, const double *x, const uint64_t *d_hist, const double *d_sums,
+                                  double *alpha, double *beta) {
+    if (!c || !c->has_template || !d_hist || !d_sums || !alpha || (c->n1 > 0 && !beta))
+        return fail(TWOSD_E_ARG, "cut_finalize: bad arguments");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipEventRecord(c->ev[5], c->stream));
+    int rc = cut_finalize_impl(c, x, (const unsigned long long *)d_hist, d_sums, alpha, beta);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(c->ev[6], c->stream));
+    HIPCHK(hipEventSynchronize(c->ev[6]));
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->ev[5], c->ev[6]);
+    c->t_us[3] = 1e3 * ms;
+    return TWOSD_OK;
+}

@@ -1,0 +1,223 @@
+// host_basis.cpp -- one-time host setup of the shared warm-start basis.
+//
+// The per-scenario LPs of solve_problem! (smps_routines.jl:50-62) differ only in their
+// right-hand side, so one optimal basis B0 (computed once, here) is dual feasible for
+// every scenario and every x; the GPU kernel warm-starts every scenario from it.  This
+// file is NOT on the per-scenario path: it runs once per template (like the crash
+// basis a simplex code computes before its first solve).
+//
+// setup_solve: revised dual simplex with an explicit dense inverse updated by rank-1
+// pivots and re-inverted every kRefactor pivots (O(m^2) per pivot).  Dantzig leaving
+// row, Harris two-pass ratio test.  Requires q >= 0 so the slack basis is dual feasible.
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include "twosd_internal.h"
+
+namespace twosd {
+
+static constexpr double kTolP = 1e-9, kTolD = 1e-9, kTolPiv = 1e-9;
+static constexpr int kRefactor = 64;
+
+bool dense_inverse(int m, const std::vector<double> &A, std::vector<double> &Ainv) {
+    // Gauss-Jordan with partial pivoting on [A | I]
+    std::vector<double> M(A);
+    Ainv.assign((size_t)m * m, 0.0);
+    for (int i = 0; i < m; ++i) Ainv[(size_t)i * m + i] = 1.0;
+    for (int c = 0; c < m; ++c) {
+        int p = c;
+        double best = std::fabs(M[(size_t)c * m + c]);
+        for (int i = c + 1; i < m; ++i) {
+            double v = std::fabs(M[(size_t)i * m + c]);
+            if (v > best) { best = v; p = i; }
+        }
+        if (best < 1e-13) return false;
+        if (p != c) {
+            for (int j = 0; j < m; ++j) {
+                std::swap(M[(size_t)p * m + j], M[(size_t)c * m + j]);
+                std::swap(Ainv[(size_t)p * m + j], Ainv[(size_t)c * m + j]);
+            }
+        }
+        const double inv = 1.0 / M[(size_t)c * m + c];
+        double *mc = &M[(size_t)c * m], *ic = &Ainv[(size_t)c * m];
+        for (int j = 0; j < m; ++j) { mc[j] *= inv; ic[j] *= inv; }
+        for (int i = 0; i < m; ++i) {
+            if (i == c) continue;
+            const double f = M[(size_t)i * m + c];
+            if (f == 0.0) continue;
+            double *mi = &M[(size_t)i * m], *ii = &Ainv[(size_t)i * m];
+            for (int j = 0; j < m; ++j) { mi[j] -= f * mc[j]; ii[j] -= f * ic[j]; }
+        }
+    }
+    return true;
+}
+
+void basis_matrix(const HostLP &L, const std::vector<int> &head, std::vector<double> &B) {
+    const int m = L.m;
+    B.assign((size_t)m * m, 0.0);
+    for (int c = 0; c < m; ++c) {
+        const int j = head[c];
+        if (j >= L.n) B[(size_t)(j - L.n) * m + c] = 1.0;
+        else
+            for (int p = L.colptr[j]; p < L.colptr[j + 1]; ++p) B[(size_t)L.rowidx[p] * m + c] = L.val[p];
+    }
+}
+
+static inline int btype_of(const HostLP &L, int j) {
+    if (j < L.n) return BT_Y;
+    char s = L.sense[j - L.n];
+    return s == 'G' ? BT_G : (s == 'L' ? BT_L : BT_E);
+}
+
+static inline double col_dot(const HostLP &L, int j, const double *v) {
+    if (j >= L.n) return v[j - L.n];
+    double s = 0.0;
+    for (int p = L.colptr[j]; p < L.colptr[j + 1]; ++p) s += v[L.rowidx[p]] * L.val[p];
+    return s;
+}
+
+double basis_dual_infeasibility(const HostLP &L, const std::vector<int> &head,
+                                const std::vector<double> &Binv, std::vector<double> &pi0) {
+    const int m = L.m, n = L.n;
+    pi0.assign(m, 0.0);
+    for (int i = 0; i < m; ++i) {
+        const int j = head[i];
+        const double c = j < n ? L.q[j] : 0.0;
+        if (c == 0.0) continue;
+        const double *row = &Binv[(size_t)i * m];
+        for (int t = 0; t < m; ++t) pi0[t] += c * row[t];
+    }
+    std::vector<char> isb(n + m, 0);
+    for (int i = 0; i < m; ++i) isb[head[i]] = 1;
+    double worst = 0.0;
+    for (int j = 0; j < n + m; ++j) {
+        if (isb[j]) continue;
+        const int bt = btype_of(L, j);
+        if (bt == BT_E) continue;
+        const double d = (j < n ? L.q[j] : 0.0) - col_dot(L, j, pi0.data());
+        const double inf = (bt == BT_G) ? d : -d;   // G slack sits at its upper bound
+        if (inf > worst) worst = inf;
+    }
+    return worst;
+}
+
+int setup_solve(const HostLP &L, const std::vector<double> &b, std::vector<int> &head, double &obj,
+                int &iters, std::string &err) {
+    const int m = L.m, n = L.n;
+    for (int j = 0; j < n; ++j)
+        if (L.q[j] < 0) { err = "setup_solve: negative stage-2 cost; install a dual-feasible basis with twosd_set_basis"; return TWOSD_LP_NUMERIC; }
+    head.resize(m);
+    for (int i = 0; i < m; ++i) head[i] = n + i;
+    std::vector<char> isb(n + m, 0);
+    for (int i = 0; i < m; ++i) isb[n + i] = 1;
+    std::vector<double> Binv, B, xB(m), pi(m), rho(m), col(m);
+    auto reinvert = [&]() -> bool {
+        basis_matrix(L, head, B);
+        if (!dense_inverse(m, B, Binv)) return false;
+        for (int i = 0; i < m; ++i) {
+            const double *row = &Binv[(size_t)i * m];
+            double s = 0.0;
+            for (int t = 0; t < m; ++t) s += row[t] * b[t];
+            xB[i] = s;
+        }
+        std::fill(pi.begin(), pi.end(), 0.0);
+        for (int i = 0; i < m; ++i) {
+            const int j = head[i];
+            const double c = j < n ? L.q[j] : 0.0;
+            if (c == 0.0) continue;
+            const double *row = &Binv[(size_t)i * m];
+            for (int t = 0; t < m; ++t) pi[t] += c * row[t];
+        }
+        return true;
+    };
+    if (!reinvert()) { err = "setup_solve: singular slack basis"; return TWOSD_LP_NUMERIC; }
+    iters = 0;
+    const int max_iter = 50 * (m + n) + 1000;
+    for (;;) {
+        // leaving row: largest primal infeasibility (lowest index on ties)
+        int r = -1;
+        double best = 0.0, delta = 0.0;
+        for (int i = 0; i < m; ++i) {
+            const int bt = btype_of(L, head[i]);
+            const double x = xB[i];
+            double d = 0.0;
+            if ((bt == BT_Y || bt == BT_L) && x < -kTolP) d = x;
+            else if (bt == BT_G && x > kTolP) d = x;
+            else if (bt == BT_E && std::fabs(x) > kTolP) d = x;
+            else continue;
+            if (std::fabs(d) > best) { best = std::fabs(d); r = i; delta = d; }
+        }
+        if (r < 0) break;
+        if (iters >= max_iter) { err = "setup_solve: iteration limit"; return TWOSD_LP_ITER_LIMIT; }
+        std::memcpy(rho.data(), &Binv[(size_t)r * m], sizeof(double) * m);
+        const double s = delta > 0 ? 1.0 : -1.0;
+        double thmax = std::numeric_limits<double>::infinity();
+        // pass 1
+        for (int j = 0; j < n + m; ++j) {
+            if (isb[j]) continue;
+            const int bt = btype_of(L, j);
+            if (bt == BT_E) continue;
+            const double a = s * col_dot(L, j, rho.data());
+            const bool atlb = bt != BT_G;
+            if (atlb ? a > kTolPiv : a < -kTolPiv) {
+                const double d = (j < n ? L.q[j] : 0.0) - col_dot(L, j, pi.data());
+                const double ratio = (atlb ? d + kTolD : d - kTolD) / a;
+                if (ratio < thmax) thmax = ratio;
+            }
+        }
+        if (thmax == std::numeric_limits<double>::infinity()) { err = "setup_solve: primal infeasible"; return TWOSD_LP_INFEASIBLE; }
+        int q = -1;
+        double amax = 0.0, dq = 0.0, aqs = 0.0;
+        for (int j = 0; j < n + m; ++j) {
+            if (isb[j]) continue;
+            const int bt = btype_of(L, j);
+            if (bt == BT_E) continue;
+            const double a = s * col_dot(L, j, rho.data());
+            const bool atlb = bt != BT_G;
+            if (atlb ? a > kTolPiv : a < -kTolPiv) {
+                const double d = (j < n ? L.q[j] : 0.0) - col_dot(L, j, pi.data());
+                if (d / a <= thmax && std::fabs(a) > amax) { amax = std::fabs(a); q = j; dq = d; aqs = a; }
+            }
+        }
+        if (q < 0) { err = "setup_solve: ratio test failed"; return TWOSD_LP_NUMERIC; }
+        const double thetaD = dq / aqs;
+        // entering column
+        std::fill(col.begin(), col.end(), 0.0);
+        if (q >= n) {
+            for (int i = 0; i < m; ++i) col[i] = Binv[(size_t)i * m + (q - n)];
+        } else {
+            for (int p = L.colptr[q]; p < L.colptr[q + 1]; ++p) {
+                const int rr = L.rowidx[p];
+                const double a = L.val[p];
+                for (int i = 0; i < m; ++i) col[i] += a * Binv[(size_t)i * m + rr];
+            }
+        }
+        const double arq = col[r];
+        if (std::fabs(arq) < 1e-12) { err = "setup_solve: tiny pivot"; return TWOSD_LP_NUMERIC; }
+        for (int i = 0; i < m; ++i) pi[i] += s * thetaD * rho[i];
+        const double thetaP = delta / arq;
+        for (int i = 0; i < m; ++i) xB[i] -= thetaP * col[i];
+        xB[r] = thetaP;
+        // explicit inverse update
+        double *rr = &Binv[(size_t)r * m];
+        for (int t = 0; t < m; ++t) rr[t] /= arq;
+        for (int i = 0; i < m; ++i) {
+            if (i == r || col[i] == 0.0) continue;
+            const double f = col[i];
+            double *ri = &Binv[(size_t)i * m];
+            for (int t = 0; t < m; ++t) ri[t] -= f * rr[t];
+        }
+        isb[head[r]] = 0;
+        isb[q] = 1;
+        head[r] = q;
+        ++iters;
+        if (iters % kRefactor == 0 && !reinvert()) { err = "setup_solve: singular basis"; return TWOSD_LP_NUMERIC; }
+    }
+    if (!reinvert()) { err = "setup_solve: singular final basis"; return TWOSD_LP_NUMERIC; }
+    obj = 0.0;
+    for (int i = 0; i < m; ++i)
+        if (head[i] < n) obj += L.q[head[i]] * xB[i];
+    return TWOSD_LP_OPTIMAL;
+}
+
+}  // namespace twosd

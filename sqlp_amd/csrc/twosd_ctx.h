@@ -1,0 +1,82 @@
+// twosd_ctx.h -- the opaque twosd_ctx behind the C ABI (library-internal).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <vector>
+#include "twosd_internal.h"
+
+namespace twosd {
+
+struct EpiDevice {
+    double *d_dv = nullptr;       // count x k scenario deltas (value - template value)
+    double *d_w = nullptr;        // count weights
+    size_t dv_cap = 0, w_cap = 0;
+    int count = 0;
+    double total_weight = 0.0;    // epigraph.jl:89, accumulated in insertion order
+    std::vector<double> w_host;
+};
+
+}  // namespace twosd
+
+struct twosd_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[8] = {};
+    int num_cus = 256;
+    int kmax_override = 0;
+    double t_us[4] = {0, 0, 0, 0};
+    // template
+    bool has_template = false, has_basis = false;
+    twosd::HostLP L;              // W CSC, q, sense (host)
+    int n1 = 0, R = 0, MP = 0, C = 0, k = 0;
+    std::vector<double> r, T;     // r (m2), dense T (m2 x n1, row-major)
+    std::vector<int> pos_row, pos_col;
+    int *d_colptr = nullptr, *d_rowidx = nullptr;
+    double *d_val = nullptr, *d_q = nullptr;
+    int8_t *d_btype = nullptr;
+    uint64_t *d_fixedmask = nullptr, *d_ubmask = nullptr;
+    // basis
+    std::vector<int> head0;
+    std::vector<double> B0inv;    // m x m host copy
+    int *d_hb0 = nullptr;
+    uint64_t *d_basic0 = nullptr;
+    double *d_B0inv = nullptr, *d_B0invT = nullptr, *d_pi0 = nullptr, *d_xbase = nullptr, *d_B0K = nullptr;
+    bool prep_valid = false;
+    std::vector<double> prep_x;
+    // LP workspace + outputs
+    double *d_eta = nullptr;
+    size_t eta_slots = 0;
+    int eta_kmax = 0;
+    int *d_queue = nullptr;
+    double *d_obj = nullptr, *d_pi = nullptr, *d_y = nullptr;
+    int *d_status = nullptr, *d_iters = nullptr;
+    int out_cap = 0;
+    size_t pi_cap = 0, y_cap = 0;
+    double *d_dvtmp = nullptr;
+    size_t dvtmp_cap = 0;
+    int last_lp_N = 0, last_lp_blocks = 0;
+    int64_t last_pivots_sum = 0;
+    int last_pivots_max = 0;
+    // epigraphs
+    std::vector<twosd::EpiDevice> epis;
+    // dual vertex set
+    twosd::DvsDevice dvs;
+    void *dvs_ws = nullptr;       // dvs scratch (dvs_kernel.hip)
+    // cut workspace (cut_kernel.hip)
+    void *cut_ws = nullptr;
+};
+
+namespace twosd {
+int fail(int code, const char *fmt, ...);
+template <typename T>
+int dgrow(T **p, size_t *cap, size_t count, size_t keep, hipStream_t s);
+int prepare_x(twosd_ctx *c, const double *x);
+int run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool want_pi, bool want_y);
+// dual vertex set (dvs_kernel.hip)
+int dvs_init(twosd_ctx *c);
+void dvs_free(twosd_ctx *c);
+int dvs_push_device(twosd_ctx *c, int count, const double *d_pis, int *d_out_index);
+// cut (cut_kernel.hip)
+void cut_free(twosd_ctx *c);
+void cut_invalidate_pk(twosd_ctx *c);
+}  // namespace twosd

@@ -1,0 +1,86 @@
+// twosd_internal.h -- shared declarations of libtwosd_hip.so (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <vector>
+#include "twosd_hip.h"
+
+namespace twosd {
+
+// ---- LP kernel envelope ----------------------------------------------------------
+// One wavefront solves one scenario.  Row i of the basis lives in lane (i % 64),
+// register slot (i / 64); R = ceil(m / 64) slots (template parameter).  Columns
+// j (structural y then slacks) are strided over lanes, C = ceil((n + m) / 64) <= 64.
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr int kMaxColsPerLane = 64;
+
+// variable bound types (all nonbasic variables sit at 0)
+enum : int { BT_Y = 0, BT_G = 1, BT_L = 2, BT_E = 3 };
+
+struct LpParams {
+    int m, n, MP;          // rows, structural columns, padded rows (= 64 * R)
+    int k;                 // random elements per scenario
+    int N;                 // scenarios in this launch
+    int kmax;              // eta capacity per wavefront
+    int C;                 // column slots per lane
+    // template
+    const int *colptr, *rowidx; const double *val;   // W CSC (0-based, int32)
+    const double *q;                                 // n
+    const int *hb0;        // MP: head0 * 4 + bound type, -1 for padded rows
+    const uint64_t *basic0;    // 64: per-lane bit c set <=> column 64c+lane basic in B0
+    const uint64_t *fixedmask; // 64: E slacks and padding columns (never enter)
+    const uint64_t *ubmask;    // 64: G slacks (nonbasic at upper bound 0)
+    const int8_t *btype;       // n + m: bound type of every column
+    // shared basis data (L2 / MALL resident)
+    const double *B0inv;   // m rows x MP (row-major, zero-padded)
+    const double *B0invT;  // m rows x MP: row i = column i of B0inv
+    const double *B0K;     // k rows x MP: coef_e * column row_e of B0inv
+    const double *pi0;     // MP
+    const double *xbase;   // MP: B0inv (r - T x)
+    // scenarios
+    const double *dv;      // N x k deltas (value - template)
+    // workspace
+    double *eta;           // nslots x kmax x MP
+    int *queue;            // [0] work counter
+    // outputs
+    double *obj, *pi, *y;  // N, N x m (nullable), N x n (nullable)
+    int *status, *iters;   // N, N
+};
+
+int lp_rows_per_lane(int m);   // supported R for m, or -1
+hipError_t launch_lp(int R, const LpParams &p, int nblocks, size_t lds_bytes, hipStream_t s);
+size_t lp_lds_bytes(int R, int kmax);
+int lp_max_blocks_per_cu(int R, int kmax);
+
+// ---- host-side setup (host_basis.cpp) --------------------------------------------
+struct HostLP {
+    int m = 0, n = 0;
+    std::vector<int> colptr, rowidx;   // W CSC, 0-based
+    std::vector<double> val, q;
+    std::vector<char> sense;           // 'G','L','E'
+};
+// dense inverse (row-major m x m), partial pivoting; false if singular
+bool dense_inverse(int m, const std::vector<double> &A, std::vector<double> &Ainv);
+void basis_matrix(const HostLP &L, const std::vector<int> &head, std::vector<double> &B);
+// setup solve from the slack basis (explicit-inverse revised dual simplex with periodic
+// re-inversion); returns LP status, fills head (optimal basis) and obj
+int setup_solve(const HostLP &L, const std::vector<double> &b, std::vector<int> &head, double &obj,
+                int &iters, std::string &err);
+// max dual infeasibility of basis head (0 = dual feasible); pi0 = c_B' B^{-1}
+double basis_dual_infeasibility(const HostLP &L, const std::vector<int> &head,
+                                const std::vector<double> &Binv, std::vector<double> &pi0);
+
+// ---- dual vertex set kernels (dvs_kernel.hip) ------------------------------------
+struct DvsDevice {
+    int m = 0, cap = 0, size = 0;
+    double *V = nullptr;          // cap x m
+    uint64_t *hash = nullptr;     // cap: reference hash (bits of round16(L1 norm))
+    uint64_t *fp = nullptr;       // cap: fingerprint of (hash, rounded components)
+    int *table = nullptr;         // tcap slots: vertex id or -1
+    int tcap = 0;                 // power of two
+};
+
+// ---- cut kernels (cut_kernel.hip) --------------------------------------------------
+}  // namespace twosd

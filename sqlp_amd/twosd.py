@@ -1,0 +1,336 @@
+"""Host-side mirror of the reference's TwoSD hot-path API, backed by libtwosd_hip.so.
+
+Reference (module TwoSD, yhz0/SQLP) -> here:
+  sdDualVertexSet / push!         dual_set.jl:69-127      -> sdDualVertexSet / push / .push
+  sdEpigraph(prob, w, lb)         epigraph.jl:52-61       -> sdEpigraph(ctx, w, lb)
+  add_scenario!(epi, w, weight)   epigraph.jl:81-96       -> add_scenario / add_scenarios
+  solve_problem!(sp, x, w)        smps_routines.jl:50-62  -> solve_problem / solve_batch
+  evaluate(sp1, sp2, sto, x; N)   smps_routines.jl:67-82  -> evaluate
+  argmax_procedure(...)           subprob.jl:141-169      -> argmax_procedure
+  build_sasa_cut(epi, x, V)       epigraph.jl:125-146     -> build_sasa_cut -> sdCut
+  sd_iteration! (hot segment)     algorithm.jl:45-55,79-85 -> sd_iteration_hot_path
+All arithmetic runs on the GPU through the C ABI; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, ptr
+from .smps import spStageProblem, spSmpsPosition, scenario_positions
+
+MIN_SENSE = "MIN_SENSE"
+DEFAULT_TIE_REL = 1e-12
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+@dataclass
+class sdCut:
+    """eta >= alpha + beta'x (epigraph.jl:5-12); never scaled."""
+    alpha: float
+    beta: np.ndarray
+    weight_mark: float
+
+
+class SDContext:
+    """Device-resident hot-path state of one cell on one GPU: the stage-2 template
+    (extract_coefficients, subprob.jl:15-69), the random-element layout, the shared
+    warm-start basis, and the dual vertex set (cell.dual_vertices, cell.jl:25)."""
+
+    def __init__(self, sp2: spStageProblem, sto=None, positions=None, device: int = 0):
+        self.lib = _lib.load()
+        h = C.c_void_p()
+        check(self.lib.twosd_create(device, C.byref(h)))
+        self.h = h
+        self.sp2 = sp2
+        self.m, self.n1, self.n2 = sp2.shape
+        Tcp, Trv, Tnz = sp2.T
+        Wcp, Wrv, Wnz = sp2.W
+        self._keep = [np.ascontiguousarray(a) for a in (Tcp, Trv, Tnz, Wcp, Wrv, Wnz)]
+        sense = np.frombuffer("".join(sp2.sense).encode(), dtype=np.int8).copy()
+        self._keep += [sense]
+        check(self.lib.twosd_set_template(
+            self.h, self.m, self.n1, self.n2,
+            ptr(self._keep[0]), ptr(self._keep[1]), ptr(self._keep[2]),
+            ptr(self._keep[3]), ptr(self._keep[4]), ptr(self._keep[5]),
+            ptr(_f64(sp2.q)), ptr(_f64(sp2.r)), ptr(sense), ptr(_f64(sp2.ylb)), ptr(_f64(sp2.yub)), 0))
+        self.row_lookup = {n: i for i, n in enumerate(sp2.stage_constraints)}
+        self.col_lookup = {n: j for j, n in enumerate(sp2.last_stage_vars)}
+        if sto is not None and positions is None:
+            positions = list(sto.indep.keys())
+        self.set_positions(positions or [])
+        self.has_basis = False
+
+    def set_positions(self, positions):
+        """Random-element layout; KeyError for an unknown row/column like
+        delta_coefficients (subprob.jl:112,116)."""
+        self.positions = [spSmpsPosition(*p) for p in positions]
+        self.pos_index = {p: e for e, p in enumerate(self.positions)}
+        rows = np.array([self.row_lookup[p.row_name] for p in self.positions], dtype=np.int32)
+        cols = np.array([-1 if p.col_name in ("RHS", "rhs") else self.col_lookup[p.col_name]
+                         for p in self.positions], dtype=np.int32)
+        self.k = len(self.positions)
+        self.rows, self.cols = rows, cols
+        check(self.lib.twosd_set_random_positions(self.h, self.k, ptr(rows), ptr(cols), 0))
+        # template value of every element (for scenario -> values conversion)
+        T = self.sp2.dense_T()
+        self.template_values = np.array(
+            [self.sp2.r[r] if c < 0 else T[r, c] for r, c in zip(rows, cols)], dtype=np.float64)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.twosd_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- warm-start basis -------------------------------------------------------
+    def compute_basis(self, x, values=None):
+        """Optimal basis of the scenario `values` (default: template) at x, installed as the
+        shared warm start of every scenario solve."""
+        x = _f64(x)
+        v = None if values is None else _f64(values)
+        check(self.lib.twosd_compute_basis(self.h, ptr(x), ptr(v)))
+        self.has_basis = True
+
+    def set_basis(self, head):
+        head = np.ascontiguousarray(head, dtype=np.int32)
+        check(self.lib.twosd_set_basis(self.h, ptr(head)))
+        self.has_basis = True
+
+    def get_basis(self):
+        head = np.zeros(self.m, dtype=np.int32)
+        check(self.lib.twosd_get_basis(self.h, ptr(head)))
+        return head
+
+    def scenario_values(self, scenario) -> np.ndarray:
+        """spSmpsScenario (list of position => value) -> value vector in layout order.
+        Elements a scenario omits keep their template value (delta 0)."""
+        v = self.template_values.copy()
+        for pos, val in scenario:
+            pos = spSmpsPosition(*pos)
+            if pos not in self.pos_index:
+                # unknown position: KeyError on its row / column like subprob.jl:112,116
+                self.row_lookup[pos.row_name]
+                if pos.col_name not in ("RHS", "rhs"):
+                    self.col_lookup[pos.col_name]
+                raise KeyError(f"{pos} is not a random element of this context")
+            v[self.pos_index[pos]] = val
+        return v
+
+    def timings_us(self):
+        t = np.zeros(4)
+        check(self.lib.twosd_last_timings(self.h, ptr(t)))
+        return t
+
+    def lp_stats(self):
+        s = C.c_int64()
+        mx = C.c_int()
+        check(self.lib.twosd_last_lp_stats(self.h, C.byref(s), C.byref(mx)))
+        return s.value, mx.value
+
+    # -- solve_problem! / evaluate ----------------------------------------------
+    def solve_values(self, x, values, want_pi=True, want_y=False, raise_on_status=True):
+        values = _f64(np.atleast_2d(values))
+        N = values.shape[0]
+        obj = np.zeros(N)
+        st = np.zeros(N, dtype=np.int32)
+        pi = np.zeros((N, self.m)) if want_pi else None
+        y = np.zeros((N, self.n2)) if want_y else None
+        rc = self.lib.twosd_solve_values(self.h, ptr(_f64(x)), N, ptr(values), ptr(obj), ptr(pi), ptr(y), ptr(st))
+        if rc != 0 and not (rc == -4 and not raise_on_status):
+            check(rc)
+        return obj, y, pi, st
+
+
+class sdDualVertexSet:
+    """Device-resident dual vertex set of an SDContext (dual_set.jl:69-127).  There is one
+    set per context (the cell's shared set)."""
+
+    def __init__(self, ctx: SDContext, data=None):
+        self.ctx = ctx
+        if data is not None:
+            self.push_batch(np.atleast_2d(np.asarray(data, dtype=np.float64)))
+
+    def push(self, vec):
+        """push!(dvs, vec): appends iff no equal vertex exists; returns self (dual_set.jl:84-94)."""
+        self.push_batch(np.asarray(vec, dtype=np.float64)[None, :])
+        return self
+
+    def push_batch(self, pis) -> np.ndarray:
+        """Sequential push! of every row; returns the vertex index of each row."""
+        pis = _f64(np.atleast_2d(pis))
+        if pis.shape[1] != self.ctx.m:
+            raise ValueError(f"dual vector length {pis.shape[1]} != {self.ctx.m}")
+        out = np.zeros(pis.shape[0], dtype=np.int32)
+        ns = C.c_int()
+        check(self.ctx.lib.twosd_dvs_push(self.ctx.h, pis.shape[0], ptr(pis), ptr(out), C.byref(ns)))
+        return out
+
+    def __len__(self):
+        s = C.c_int()
+        check(self.ctx.lib.twosd_dvs_size(self.ctx.h, C.byref(s)))
+        return s.value
+
+    def matrix(self, first=0, count=None) -> np.ndarray:
+        n = len(self)
+        count = n - first if count is None else count
+        out = np.zeros((count, self.ctx.m))
+        check(self.ctx.lib.twosd_dvs_get(self.ctx.h, first, count, ptr(out)))
+        return out
+
+    def __iter__(self):
+        return iter(list(self.matrix()))
+
+    def clear(self):
+        check(self.ctx.lib.twosd_dvs_clear(self.ctx.h))
+
+    def truncate(self, size):
+        check(self.ctx.lib.twosd_dvs_truncate(self.ctx.h, int(size)))
+
+
+def push(dvs: sdDualVertexSet, vec):
+    return dvs.push(vec)
+
+
+class sdEpigraph:
+    """sdEpigraph (epigraph.jl:17-61): scenario pool + weights on the device, cuts on the host."""
+
+    def __init__(self, ctx: SDContext, objective_weight: float, lower_bound: float):
+        self.ctx = ctx
+        self.objective_weight = float(objective_weight)
+        self.lower_bound = float(lower_bound)
+        e = C.c_int()
+        check(ctx.lib.twosd_epigraph_create(ctx.h, C.byref(e)))
+        self.index = e.value
+        self.scenario_weight: list = []
+        self.cuts: list = []
+        self.incumbent_cut = None
+
+    @property
+    def total_scenario_weight(self) -> float:
+        tw = C.c_double()
+        check(self.ctx.lib.twosd_epigraph_info(self.ctx.h, self.index, None, C.byref(tw)))
+        return tw.value
+
+    @property
+    def num_scenarios(self) -> int:
+        n = C.c_int()
+        check(self.ctx.lib.twosd_epigraph_info(self.ctx.h, self.index, C.byref(n), None))
+        return n.value
+
+
+def add_scenario(epi: sdEpigraph, scenario, weight: float = 1.0):
+    """add_scenario!(epi, scenario, weight) (epigraph.jl:81-96)."""
+    add_scenarios(epi, epi.ctx.scenario_values(scenario)[None, :], np.array([weight]))
+
+
+def add_scenarios(epi: sdEpigraph, values, weights=None):
+    """Batched add_scenario!: values N x k (layout order), weights N (default 1.0)."""
+    values = _f64(np.atleast_2d(values))
+    N = values.shape[0]
+    w = None if weights is None else _f64(weights)
+    check(epi.ctx.lib.twosd_add_scenarios(epi.ctx.h, epi.index, N, ptr(values), ptr(w)))
+    epi.scenario_weight.extend([1.0] * N if w is None else list(w))
+
+
+def solve_batch(epi: sdEpigraph, x, first=0, count=None, want_pi=True, want_y=False):
+    """solve_problem! over scenarios [first, first+count) of epi at x -> (obj, y, pi, status)."""
+    ctx = epi.ctx
+    count = epi.num_scenarios - first if count is None else count
+    obj = np.zeros(count)
+    st = np.zeros(count, dtype=np.int32)
+    pi = np.zeros((count, ctx.m)) if want_pi else None
+    y = np.zeros((count, ctx.n2)) if want_y else None
+    check(ctx.lib.twosd_solve_batch(ctx.h, epi.index, ptr(_f64(x)), first, count, ptr(obj), ptr(pi), ptr(y), ptr(st)))
+    return obj, y, pi, st
+
+
+def solve_problem(ctx: SDContext, x, scenario):
+    """solve_problem!(sp, x, scenario) -> (obj, y_opt, dual_opt) (smps_routines.jl:50-62).
+    A non-optimal LP raises (the reference logs @error and returns junk duals)."""
+    obj, y, pi, st = ctx.solve_values(x, ctx.scenario_values(scenario)[None, :], want_pi=True, want_y=True)
+    return float(obj[0]), y[0], pi[0]
+
+
+def evaluate(ctx: SDContext, first_stage_cost, x, values):
+    """evaluate(sp1, sp2, sto, x; N) (smps_routines.jl:67-82) on given sampled values:
+    c'x + (1/N) sum_w obj_w.  first_stage_cost: the stage-1 objective vector."""
+    obj, _, _, _ = ctx.solve_values(x, values, want_pi=False)
+    N = obj.shape[0]
+    s2 = 0.0
+    for o in obj:                      # s2_cost += 1/N*obj, in sample order (:79)
+        s2 += 1.0 / N * o
+    return float(np.dot(first_stage_cost, x)) + s2
+
+
+def argmax_procedure(epi: sdEpigraph, x, dual_vertices: sdDualVertexSet, tie_rel=DEFAULT_TIE_REL):
+    """(max_val, max_arg) over every scenario of epi (subprob.jl:141-169); max_arg holds
+    0-based vertex indices into dual_vertices (the reference returns Refs to vectors)."""
+    cut, mv, ma = _build_cut(epi, x, tie_rel, want_argmax=True)
+    return mv, ma
+
+
+def build_sasa_cut(epi: sdEpigraph, x, dual_vertices: sdDualVertexSet, tie_rel=DEFAULT_TIE_REL) -> sdCut:
+    """build_sasa_cut(epi, x, V) (epigraph.jl:125-146)."""
+    cut, _, _ = _build_cut(epi, x, tie_rel, want_argmax=False)
+    return cut
+
+
+def _build_cut(epi, x, tie_rel, want_argmax):
+    ctx = epi.ctx
+    a = C.c_double()
+    wm = C.c_double()
+    beta = np.zeros(ctx.n1)
+    N = epi.num_scenarios
+    mv = np.zeros(N) if want_argmax else None
+    ma = np.zeros(N, dtype=np.int32) if want_argmax else None
+    check(ctx.lib.twosd_build_cut(ctx.h, epi.index, ptr(_f64(x)), float(tie_rel), C.byref(a), ptr(beta),
+                                  C.byref(wm), ptr(mv), ptr(ma)))
+    return sdCut(a.value, beta, wm.value), mv, ma
+
+
+def solve_push(epi: sdEpigraph, x, first, count):
+    """Device-side solve_problem! + push! of the duals (no host round trip)."""
+    ctx = epi.ctx
+    obj = np.zeros(count)
+    st = np.zeros(count, dtype=np.int32)
+    ns = C.c_int()
+    check(ctx.lib.twosd_solve_push(ctx.h, epi.index, ptr(_f64(x)), first, count, ptr(obj), ptr(st), C.byref(ns)))
+    return obj, st, ns.value
+
+
+def sd_iteration_hot_path(epis, scenario_values, x_candidate, x_incumbent, V: sdDualVertexSet,
+                          update_incumbent_cut=True, tie_rel=DEFAULT_TIE_REL):
+    """The data-parallel part of sd_iteration! (algorithm.jl:45-55 and :79-85):
+    for every epigraph i: add_scenario!(epi_i, w_i, 1.0); solve at x_candidate and at
+    x_incumbent, push! both duals (in the reference's order: epi 1 cand, epi 1 inc,
+    epi 2 cand, ...); then build_sasa_cut at x_candidate (appended to epi.cuts) and, if
+    update_incumbent_cut, at x_incumbent (epi.incumbent_cut).  scenario_values[i] is a
+    (N_i x k) block of new scenarios for epigraph i."""
+    pis = []
+    for epi, vals in zip(epis, scenario_values):
+        vals = np.atleast_2d(vals)
+        first = epi.num_scenarios
+        add_scenarios(epi, vals, np.ones(vals.shape[0]))
+        _, _, pc, _ = solve_batch(epi, x_candidate, first, vals.shape[0])
+        _, _, pinc, _ = solve_batch(epi, x_incumbent, first, vals.shape[0])
+        inter = np.empty((2 * vals.shape[0], pc.shape[1]))
+        inter[0::2] = pc
+        inter[1::2] = pinc
+        pis.append(inter)
+    V.push_batch(np.vstack(pis))
+    for epi in epis:
+        epi.cuts.append(build_sasa_cut(epi, x_candidate, V, tie_rel))
+        if update_incumbent_cut:
+            epi.incumbent_cut = build_sasa_cut(epi, x_incumbent, V, tie_rel)

@@ -1,0 +1,76 @@
+"""GPU parity of the batched stage-2 LP (solve_problem!, smps_routines.jl:50-62)
+against the oracle (C dual simplex + HiGHS), through the C ABI."""
+import numpy as np
+import pytest
+
+from tests import instances as I
+
+pytestmark = pytest.mark.gpu
+
+CASES = [("lands", 512), ("newsvendor", 256), ("transship", 512), ("ssn", 512), ("storm", 512)]
+
+
+def _ctx(name):
+    from sqlp_amd import twosd
+    inst = I.load(name)
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    x = I.x_ev(name)
+    from sqlp_amd import smps
+    ctx.compute_basis(x, smps.mean_values(inst["sto"]))
+    return ctx, x
+
+
+def _dual_feasible(sp, pi, tol=1e-7):
+    # W' pi <= q (reduced costs of y >= 0), sign of pi by row sense
+    scale = 1.0 + np.abs(sp.q).max()
+    d = sp.q - sp.W.T @ pi
+    ok = d.min() >= -tol * scale
+    for i, s in enumerate(sp.senses):
+        if s == 'G':
+            ok &= pi[i] >= -tol * scale
+        elif s == 'L':
+            ok &= pi[i] <= tol * scale
+    return ok
+
+
+@pytest.mark.parametrize("name,N", CASES)
+def test_lp_batch_matches_oracle(name, N):
+    from oracle import cpu, lp_highs
+    ctx, x = _ctx(name)
+    vals = I.sample(name, N, seed=7)
+    obj, y, pi, st = ctx.solve_values(x, vals, want_pi=True, want_y=True)
+    assert (st == 0).all(), np.bincount(st)
+    inst = I.load(name)
+    sp = inst["osp2"]
+    b = I.rhs_of(name, x, vals)
+    # oracle C dual simplex from the same basis
+    lp = cpu.CpuLP(sp.W, sp.q, sp.senses)
+    lp.set_basis(ctx.get_basis())
+    pos, rows, cols = __import__("sqlp_amd").smps.scenario_positions(inst["sp2"], inst["sto"])
+    o_obj, o_pi, _, o_st, _ = lp.solve_batch(rows, sp.r - sp.T @ x, vals - sp.r[rows], nthreads=4)
+    assert (o_st == 0).all()
+    np.testing.assert_allclose(obj, o_obj, rtol=1e-9, atol=1e-9)
+    # strong duality + dual feasibility of every GPU dual (obj = pi . b)
+    for s in range(N):
+        assert abs(pi[s] @ b[s] - obj[s]) <= 1e-9 * (1 + abs(obj[s]))
+        assert _dual_feasible(sp, pi[s])
+    # primal feasibility of y
+    W = sp.W
+    for s in range(0, N, max(1, N // 64)):
+        r = W @ y[s] - b[s]
+        for i, sn in enumerate(sp.senses):
+            if sn == 'G':
+                assert r[i] >= -1e-7 * (1 + abs(b[s][i]))
+            elif sn == 'L':
+                assert r[i] <= 1e-7 * (1 + abs(b[s][i]))
+            else:
+                assert abs(r[i]) <= 1e-7 * (1 + abs(b[s][i]))
+        assert (y[s] >= -1e-9).all()
+    # HiGHS objective on a subset (unique optimum)
+    for s in range(0, N, max(1, N // 16)):
+        hst, hobj, _, _ = lp_highs.solve_rhs(sp, b[s])
+        assert hst == 0
+        assert abs(hobj - obj[s]) <= 1e-8 * (1 + abs(hobj))
+    # same pivot rules -> same vertex as the oracle on (almost) every scenario
+    same = np.mean([np.allclose(pi[s], o_pi[s], rtol=1e-9, atol=1e-9) for s in range(N)])
+    assert same >= 0.95, same
