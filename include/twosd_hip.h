@@ -157,6 +157,11 @@ int twosd_last_timings(twosd_ctx *ctx, double *us4);
 /* Statistics of the last LP batch: sum of simplex pivots, max pivots. */
 int twosd_last_lp_stats(twosd_ctx *ctx, int64_t *pivots_sum, int *pivots_max);
 
+/* Executed fp64 row operations of the last LP batch: each is one fused multiply-add over
+ * a padded basis row of *row_width (= 64 * ceil(m2/64)) doubles, i.e. 2 * row_width flops
+ * (used for the counted-FLOP roofline of the LP kernel). */
+int twosd_last_lp_ops(twosd_ctx *ctx, int64_t *row_ops, int *row_width);
+
 #ifdef __cplusplus
 }
 #endif

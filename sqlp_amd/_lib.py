@@ -48,6 +48,7 @@ SIGNATURES = [
     ("twosd_cut_finalize", I, [P, P, P, P, P, P]),
     ("twosd_last_timings", I, [P, P]),
     ("twosd_last_lp_stats", I, [P, P, P]),
+    ("twosd_last_lp_ops", I, [P, P, P]),
 ]
 
 _lib = None

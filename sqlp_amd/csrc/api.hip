@@ -99,7 +99,8 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_fixedmask); dfree(c->d_ubmask);
     dfree(c->d_hb0); dfree(c->d_basic0); dfree(c->d_B0inv); dfree(c->d_B0invT); dfree(c->d_pi0);
     dfree(c->d_xbase); dfree(c->d_B0K); dfree(c->d_eta); dfree(c->d_queue);
-    dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_dvtmp);
+    dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_ops);
+    dfree(c->d_dvtmp);
     for (auto &e : c->epis) { dfree(e.d_dv); dfree(e.d_w); }
     c->epis.clear();
     c->out_cap = 0; c->eta_slots = 0; c->dvtmp_cap = 0;
@@ -391,7 +392,9 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
     const int m = c->L.m, n = c->L.n, MP = c->MP, R = c->R;
     if (N > c->out_cap) {
         size_t cap = std::max<size_t>(N, 1024);
-        if ((rc = dalloc(&c->d_obj, cap)) || (rc = dalloc(&c->d_status, cap)) || (rc = dalloc(&c->d_iters, cap))) return rc;
+        if ((rc = dalloc(&c->d_obj, cap)) || (rc = dalloc(&c->d_status, cap)) || (rc = dalloc(&c->d_iters, cap)) ||
+            (rc = dalloc(&c->d_ops, cap)))
+            return rc;
         dfree(c->d_pi); dfree(c->d_y);
         c->pi_cap = c->y_cap = 0;
         c->out_cap = (int)cap;
@@ -422,7 +425,7 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
     P.B0inv = c->d_B0inv; P.B0invT = c->d_B0invT; P.B0K = c->d_B0K; P.pi0 = c->d_pi0; P.xbase = c->d_xbase;
     P.dv = d_dv; P.eta = c->d_eta; P.queue = c->d_queue;
     P.obj = c->d_obj; P.pi = want_pi ? c->d_pi : nullptr; P.y = want_y ? c->d_y : nullptr;
-    P.status = c->d_status; P.iters = c->d_iters;
+    P.status = c->d_status; P.iters = c->d_iters; P.ops = c->d_ops;
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
     HIPCHK(launch_lp(R, P, nblocks, lp_lds_bytes(R, kmax), c->stream));
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
@@ -442,9 +445,11 @@ static int copy_lp_outputs(twosd_ctx *c, int N, double *obj, double *pi, double 
     std::vector<int> st(N), its(N);
     HIPCHK(hipMemcpy(st.data(), c->d_status, sizeof(int) * N, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(its.data(), c->d_iters, sizeof(int) * N, hipMemcpyDeviceToHost));
-    int64_t sum = 0; int mx = 0, bad = 0;
-    for (int s = 0; s < N; ++s) { sum += its[s]; mx = std::max(mx, its[s]); bad += st[s] != TWOSD_LP_OPTIMAL; }
-    c->last_pivots_sum = sum; c->last_pivots_max = mx;
+    std::vector<long long> ops(N);
+    HIPCHK(hipMemcpy(ops.data(), c->d_ops, sizeof(long long) * N, hipMemcpyDeviceToHost));
+    int64_t sum = 0, osum = 0; int mx = 0, bad = 0;
+    for (int s = 0; s < N; ++s) { sum += its[s]; osum += ops[s]; mx = std::max(mx, its[s]); bad += st[s] != TWOSD_LP_OPTIMAL; }
+    c->last_pivots_sum = sum; c->last_pivots_max = mx; c->last_ops_sum = osum;
     if (status) std::copy(st.begin(), st.end(), status);
     if (bad) return fail(TWOSD_E_LP, "%d of %d scenario LPs not optimal (see status[])", bad, N);
     return TWOSD_OK;
@@ -493,6 +498,13 @@ extern "C" int twosd_last_lp_stats(twosd_ctx *c, int64_t *sum, int *mx) {
     if (!c) return fail(TWOSD_E_ARG, "last_lp_stats: NULL");
     if (sum) *sum = c->last_pivots_sum;
     if (mx) *mx = c->last_pivots_max;
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_last_lp_ops(twosd_ctx *c, int64_t *row_ops, int *row_width) {
+    if (!c) return fail(TWOSD_E_ARG, "last_lp_ops: NULL");
+    if (row_ops) *row_ops = c->last_ops_sum;
+    if (row_width) *row_width = c->MP;
     return TWOSD_OK;
 }
 

@@ -154,8 +154,7 @@ __global__ void __launch_bounds__(256) cut_argmax_kernel(CutParams P) {
                     if (i2 < it) { it = i2; st = s2; }
                 }
                 if (mt == -INFINITY) continue;
-                const double tM = tolf(M[r], P.tie_rel);
-                if (mt > M[r] + tM) { M[r] = mt; I[r] = it; SV[r] = st; }
+                if (M[r] == -INFINITY || mt > M[r] + tolf(M[r], P.tie_rel)) { M[r] = mt; I[r] = it; SV[r] = st; }
                 else if (mt > M[r]) {
                     // max slides up inside the tolerance band
                     if (!(SV[r] >= mt - tolf(mt, P.tie_rel))) F[r] = 1;
@@ -302,8 +301,9 @@ struct CutWs {
     int *arg = nullptr, *flag = nullptr;
     double *val = nullptr;
     unsigned long long *hist = nullptr;
-    size_t base_cap = 0, part_cap = 0, n_cap = 0, hist_cap = 0, gpart_cap = 0;
-    int m = 0;
+    size_t base_cap = 0, part_cap = 0, n_cap = 0, hist_cap = 0, gpart_cap = 0, sums_cap = 0;
+    int m = 0, vec_m = 0;
+    std::vector<double> h_coef, h_bvec;   // pinned-lifetime host staging for async uploads
 };
 
 static CutWs *cws(twosd_ctx *c) {
@@ -413,17 +413,18 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     int rc;
     if ((rc = update_pk(c))) return rc;
     // host: bvec = r - T x, coef
-    std::vector<double> bvec(m), coef(k4, 0.0);
+    std::vector<double> &bvec = w->h_bvec, &coef = w->h_coef;
+    bvec.assign(m, 0.0);
+    coef.assign(k4, 0.0);
     for (int i = 0; i < m; ++i) {
         double s = 0.0;
         for (int jj = 0; jj < n1; ++jj) s += c->T[(size_t)i * n1 + jj] * x[jj];
         bvec[i] = c->r[i] - s;
     }
     for (int e = 0; e < k; ++e) coef[e] = c->pos_col[e] < 0 ? 1.0 : -x[c->pos_col[e]];
-    if (!w->coef || !w->bvec || w->m != m) {
-        if ((rc = realloc_dev(&w->coef, 256)) || (rc = realloc_dev(&w->bvec, m)) || (rc = realloc_dev(&w->g, m)) ||
-            (rc = realloc_dev(&w->sums, 256)))
-            return rc;
+    if (!w->coef || !w->bvec || !w->g || w->vec_m != m) {
+        if ((rc = realloc_dev(&w->coef, 256)) || (rc = realloc_dev(&w->bvec, m)) || (rc = realloc_dev(&w->g, m))) return rc;
+        w->vec_m = m;
     }
     if ((size_t)nv > w->base_cap) {
         if ((rc = realloc_dev(&w->base, nv))) return rc;
@@ -519,6 +520,10 @@ extern "C" int twosd_build_cut(twosd_ctx *c, int epi, const double *x, double ti
     if ((size_t)nv > w->hist_cap) {
         if ((rc = realloc_dev(&w->hist, nv))) return rc;
         w->hist_cap = nv;
+    }
+    if ((size_t)(c->k + 1) > w->sums_cap) {
+        if ((rc = realloc_dev(&w->sums, c->k + 1))) return rc;
+        w->sums_cap = c->k + 1;
     }
     if (E.count == 0 || E.total_weight <= 0.0) {
         // no scenarios: the reference returns the zero cut with weight_mark = total weight

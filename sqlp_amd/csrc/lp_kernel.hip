@@ -142,6 +142,7 @@ __global__ void __launch_bounds__(256) lp_dual_simplex_kernel(LpParams P) {
         }
         uint64_t bmask = P.basic0[lane];
         int K = 0, it = 0, status = TWOSD_LP_OPTIMAL;
+        long long nops = k;   // x_B warm start: k rows
         wave_sync();
 
         for (;;) {
@@ -193,8 +194,10 @@ __global__ void __launch_bounds__(256) lp_dual_simplex_kernel(LpParams P) {
 #pragma unroll
                     for (int t = 0; t < R; ++t) rh[t] = fma(up, row[64 * t + lane], rh[t]);
                     set_row<R, double>(u, p, 0.0, lane);
+                    ++nops;
                 }
             }
+            nops += K;
 #pragma unroll
             for (int t = 0; t < R; ++t) rho_l[64 * t + lane] = rh[t];
             wave_sync();
@@ -297,6 +300,7 @@ __global__ void __launch_bounds__(256) lp_dual_simplex_kernel(LpParams P) {
                     }
                 }
             }
+            nops += K + (q >= n ? 1 : (P.colptr[q + 1] - P.colptr[q])) + 4;
             const double arq = get_row<R>(col, r);
             if (fabs(arq) < 1e-12) { status = TWOSD_LP_NUMERIC; break; }
 
@@ -379,6 +383,7 @@ __global__ void __launch_bounds__(256) lp_dual_simplex_kernel(LpParams P) {
                 if (hb[t] >= 0 && j < n) ob = fma(P.q[j], xB[t], ob);
             }
             objv = wave_sum(ob);
+            nops += K + m;
             if (P.pi) {
                 double *po = P.pi + (size_t)s * m;
 #pragma unroll
@@ -406,6 +411,7 @@ __global__ void __launch_bounds__(256) lp_dual_simplex_kernel(LpParams P) {
             P.obj[s] = objv;
             P.status[s] = status;
             P.iters[s] = it;
+            if (P.ops) P.ops[s] = nops;
         }
         wave_sync();
     }

@@ -50,6 +50,8 @@ struct twosd_ctx {
     int *d_queue = nullptr;
     double *d_obj = nullptr, *d_pi = nullptr, *d_y = nullptr;
     int *d_status = nullptr, *d_iters = nullptr;
+    long long *d_ops = nullptr;
+    int64_t last_ops_sum = 0;
     int out_cap = 0;
     size_t pi_cap = 0, y_cap = 0;
     double *d_dvtmp = nullptr;

@@ -47,6 +47,7 @@ struct LpParams {
     // outputs
     double *obj, *pi, *y;  // N, N x m (nullable), N x n (nullable)
     int *status, *iters;   // N, N
+    long long *ops;        // N (nullable): executed 64R-wide fp64 row operations (FMA rows)
 };
 
 int lp_rows_per_lane(int m);   // supported R for m, or -1

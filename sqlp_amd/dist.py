@@ -1,0 +1,87 @@
+"""Scenario data-parallelism across GPUs (one process per GPU, torch.distributed).
+
+The reference is single-process (no MPI/NCCL; the comments at
+algorithm.jl:7,10-11 and cell.jl:25 only anticipate per-epigraph parallelism).  Here the
+hot path shards naturally by scenario:
+  * LP solves and argmax are per scenario against a replicated template / vertex set;
+    rank g owns the contiguous range shard_range(N, g, G).
+  * build_sasa_cut needs ONE exchange: the vertex-weight histogram (uint64 fixed point,
+    summed exactly, so every rank count gives bit-identical h) and k+1 fp64 sums,
+    all-reduced over RCCL (backend "nccl") -- a few KB per cut.
+  * vertex-set growth: every rank dedups its new duals locally, then the locally-new rows
+    are all-gathered and pushed in (rank, local index) order, so every rank holds the same
+    ordered set (the order decides argmax ties).
+The collectives are plain torch.distributed calls on tensors, so the same code runs on
+CPU tensors with gloo (tests) and on HIP tensors with RCCL (bench).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def shard_range(N: int, rank: int, world_size: int):
+    """Contiguous scenario range [lo, hi) of `rank`."""
+    return (N * rank) // world_size, (N * (rank + 1)) // world_size
+
+
+def allreduce_cut_partials(hist: torch.Tensor, sums: torch.Tensor):
+    """Sum the per-rank cut partials in place: hist (int64 fixed point, exact) and sums
+    (fp64).  No-op on a single rank."""
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(hist, op=dist.ReduceOp.SUM)
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+    return hist, sums
+
+
+def allgather_rows_ordered(rows: torch.Tensor) -> torch.Tensor:
+    """Concatenate every rank's (n_r x m) rows in rank order (variable n_r)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return rows
+    G = dist.get_world_size()
+    n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=rows.device)
+    counts = [torch.zeros_like(n) for _ in range(G)]
+    dist.all_gather(counts, n)
+    counts = [int(c.item()) for c in counts]
+    mx = max(counts)
+    pad = torch.zeros((mx, rows.shape[1]), dtype=rows.dtype, device=rows.device)
+    pad[: rows.shape[0]] = rows
+    bufs = [torch.zeros_like(pad) for _ in range(G)]
+    dist.all_gather(bufs, pad)
+    return torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
+
+
+def build_cut_sharded(ctx, epi, x, total_weight, tie_rel, device):
+    """build_sasa_cut over the scenarios of every rank: local partial on this GPU,
+    all-reduce over RCCL, identical finalize on every rank.  Returns (alpha, beta)."""
+    n_u64, n_f64 = ctx.cut_partial_len()
+    hist = torch.zeros(n_u64, dtype=torch.int64, device=device)
+    sums = torch.zeros(n_f64, dtype=torch.float64, device=device)
+    torch.cuda.synchronize(device)
+    ctx.cut_partial(epi, x, tie_rel, total_weight, hist.data_ptr(), sums.data_ptr())
+    allreduce_cut_partials(hist, sums)
+    torch.cuda.synchronize(device)
+    return ctx.cut_finalize(x, hist.data_ptr(), sums.data_ptr())
+
+
+def finalize_from_partials(hist: np.ndarray, sums: np.ndarray, V: np.ndarray, r: np.ndarray, T: np.ndarray,
+                           cols: np.ndarray):
+    """Host restatement of twosd_cut_finalize (used by the gloo tests): g = sum_v h_v pi_v,
+    alpha = g.r + sum_{e RHS} S_e, beta = -T'g - sum_{e T} S_e e_col."""
+    h = hist.astype(np.float64) * 2.0 ** -62
+    g = h @ V
+    alpha = float(g @ r)
+    beta = -(T.T @ g)
+    for e, c in enumerate(cols):
+        if c < 0:
+            alpha += sums[1 + e]
+        else:
+            beta[c] -= sums[1 + e]
+    return alpha, beta

@@ -139,6 +139,31 @@ class SDContext:
         check(self.lib.twosd_last_lp_stats(self.h, C.byref(s), C.byref(mx)))
         return s.value, mx.value
 
+    def lp_flops(self):
+        """Counted fp64 FLOPs of the last LP batch (2 * row width per executed row op)."""
+        ops = C.c_int64()
+        w = C.c_int()
+        check(self.lib.twosd_last_lp_ops(self.h, C.byref(ops), C.byref(w)))
+        return 2.0 * w.value * ops.value
+
+    # -- multi-GPU split of build_sasa_cut (device buffers from the caller) --------
+    def cut_partial_len(self):
+        a = C.c_int64()
+        b = C.c_int64()
+        check(self.lib.twosd_cut_partial_len(self.h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def cut_partial(self, epi, x, tie_rel, total_weight, d_hist_ptr, d_sums_ptr):
+        check(self.lib.twosd_cut_partial(self.h, epi.index, ptr(_f64(x)), float(tie_rel), float(total_weight),
+                                         C.c_void_p(d_hist_ptr), C.c_void_p(d_sums_ptr), None, None))
+
+    def cut_finalize(self, x, d_hist_ptr, d_sums_ptr):
+        a = C.c_double()
+        beta = np.zeros(self.n1)
+        check(self.lib.twosd_cut_finalize(self.h, ptr(_f64(x)), C.c_void_p(d_hist_ptr), C.c_void_p(d_sums_ptr),
+                                          C.byref(a), ptr(beta)))
+        return a.value, beta
+
     # -- solve_problem! / evaluate ----------------------------------------------
     def solve_values(self, x, values, want_pi=True, want_y=False, raise_on_status=True):
         values = _f64(np.atleast_2d(values))
