@@ -162,6 +162,10 @@ int twosd_last_lp_stats(twosd_ctx *ctx, int64_t *pivots_sum, int *pivots_max);
  * (used for the counted-FLOP roofline of the LP kernel). */
 int twosd_last_lp_ops(twosd_ctx *ctx, int64_t *row_ops, int *row_width);
 
+/* Diagnostic: per-phase cycle totals of the hypersparse LP kernel, summed over waves
+ * (non-zero only in the TWOSD_STAMPS build libtwosd_hip_stamps.so).  reset != 0 clears. */
+int twosd_debug_stamps(twosd_ctx *ctx, uint64_t *out10, int reset);
+
 #ifdef __cplusplus
 }
 #endif

@@ -10,7 +10,10 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtwosd_hip.so")
+# TWOSD_LIB=<variant> selects libtwosd_hip_<variant>.so (e.g. "stamps": the phase-stamp
+# diagnostic build, never used for timing claims; tuning variants during development)
+LIB_PATH = os.path.join(_HERE, f"libtwosd_hip_{os.environ['TWOSD_LIB']}.so" if os.environ.get("TWOSD_LIB")
+                        else "libtwosd_hip.so")
 
 TWOSD_OK = 0
 ERRORS = {-1: "TWOSD_E_ARG", -2: "TWOSD_E_DEVICE", -3: "TWOSD_E_STATE", -4: "TWOSD_E_LP",
@@ -49,6 +52,7 @@ SIGNATURES = [
     ("twosd_last_timings", I, [P, P]),
     ("twosd_last_lp_stats", I, [P, P, P]),
     ("twosd_last_lp_ops", I, [P, P, P]),
+    ("twosd_debug_stamps", I, [P, P, I]),
 ]
 
 _lib = None

@@ -94,6 +94,39 @@ extern "C" int twosd_create(int device, twosd_ctx **out) {
     return TWOSD_OK;
 }
 
+// Sliced ELL of S*64 columns: column j = 64*s + l gives (row, value) entries via colf.
+// Slot s has width E_s = max entries over its 64 columns; entry e of lane l is stored at
+// [(slot[s] + e) * 64 + l], padding (row 0, value 0).
+template <typename F>
+static void build_ell(int S, F colf, std::vector<int> &slot, std::vector<int> &ix, std::vector<double> &v) {
+    slot.assign(S + 1, 0);
+    std::vector<std::vector<std::pair<int, double>>> cols(64);
+    ix.clear(); v.clear();
+    for (int s = 0; s < S; ++s) {
+        int width = 0;
+        for (int l = 0; l < 64; ++l) {
+            cols[l].clear();
+            colf(64 * s + l, cols[l]);
+            width = std::max(width, (int)cols[l].size());
+        }
+        for (int e = 0; e < width; ++e)
+            for (int l = 0; l < 64; ++l) {
+                const bool has = e < (int)cols[l].size();
+                ix.push_back(has ? cols[l][e].first : 0);
+                v.push_back(has ? cols[l][e].second : 0.0);
+            }
+        slot[s + 1] = slot[s] + width;
+    }
+}
+
+template <typename T>
+static int upload(T **d, const std::vector<T> &h) {
+    int rc = dalloc(d, std::max<size_t>(h.size(), 1));
+    if (rc) return rc;
+    if (!h.empty()) HIPCHK(hipMemcpy(*d, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice));
+    return TWOSD_OK;
+}
+
 static void free_template(twosd_ctx *c) {
     dfree(c->d_colptr); dfree(c->d_rowidx); dfree(c->d_val); dfree(c->d_q); dfree(c->d_btype);
     dfree(c->d_fixedmask); dfree(c->d_ubmask);
@@ -101,6 +134,11 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_xbase); dfree(c->d_B0K); dfree(c->d_eta); dfree(c->d_queue);
     dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_ops);
     dfree(c->d_dvtmp);
+    dfree(c->d_bcolptr); dfree(c->d_browidx); dfree(c->d_bval); dfree(c->d_kptr); dfree(c->d_kidx); dfree(c->d_kval);
+    dfree(c->d_d0); dfree(c->d_eidx); dfree(c->d_evals); dfree(c->d_stamps);
+    dfree(c->d_wslot); dfree(c->d_wix); dfree(c->d_wv); dfree(c->d_bslot); dfree(c->d_bix); dfree(c->d_bv);
+    dfree(c->d_brptr); dfree(c->d_brcol); dfree(c->d_brval); dfree(c->d_wrow4); dfree(c->d_wval4);
+    c->earena_slots = 0; c->earena_cap = 0;
     for (auto &e : c->epis) { dfree(e.d_dv); dfree(e.d_w); }
     c->epis.clear();
     c->out_cap = 0; c->eta_slots = 0; c->dvtmp_cap = 0;
@@ -161,11 +199,14 @@ extern "C" int twosd_set_template(twosd_ctx *c, int m2, int n1, int n2, const in
             if (i < 0 || i >= m2) return fail(TWOSD_E_ARG, "T row index out of range");
             c->T[(size_t)i * n1 + j] = Tnz[p];
         }
-    const int R = lp_rows_per_lane(m2);
+    const int R = hyper_rows_per_lane(m2);
     if (R < 0) return fail(TWOSD_E_UNSUPPORTED, "m2 = %d exceeds the LP kernel envelope (%d rows)", m2, 64 * 16);
     const int C = (n2 + m2 + 63) / 64;
     if (C > kMaxColsPerLane) return fail(TWOSD_E_UNSUPPORTED, "n2 + m2 = %d exceeds %d columns", n2 + m2, 64 * kMaxColsPerLane);
     c->R = R; c->MP = 64 * R; c->C = C;
+    c->CH = hyper_cols_per_lane(n2 + m2);
+    const char *kern = getenv("TWOSD_LP_KERNEL");
+    c->use_hyper = c->CH > 0 && !(kern && std::string(kern) == "dense");
     // device template
     int rc;
     if ((rc = dalloc(&c->d_colptr, n2 + 1)) || (rc = dalloc(&c->d_rowidx, nnzW)) || (rc = dalloc(&c->d_val, nnzW)) ||
@@ -179,7 +220,7 @@ extern "C" int twosd_set_template(twosd_ctx *c, int m2, int n1, int n2, const in
         if (j >= n2) { char s = L.sense[j - n2]; b = s == 'G' ? BT_G : (s == 'L' ? BT_L : BT_E); }
         bt[j] = (int8_t)b;
     }
-    for (int j = 0; j < 64 * C; ++j) {
+    for (int j = 0; j < 64 * 64; ++j) {
         const int lane = j & 63, cs = j >> 6;
         if (j >= n2 + m2 || bt[j] == BT_E) fixedm[lane] |= 1ull << cs;
         else if (bt[j] == BT_G) ubm[lane] |= 1ull << cs;
@@ -191,6 +232,44 @@ extern "C" int twosd_set_template(twosd_ctx *c, int m2, int n1, int n2, const in
     HIPCHK(hipMemcpy(c->d_btype, bt.data(), n2 + m2, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d_fixedmask, fixedm.data(), sizeof(uint64_t) * 64, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d_ubmask, ubm.data(), sizeof(uint64_t) * 64, hipMemcpyHostToDevice));
+    if (c->CH > 0) {   // sliced ELL of the columns of [W I] for the hypersparse kernel
+        std::vector<int> ws, wi;
+        std::vector<double> wvv;
+        build_ell(c->CH, [&](int j, std::vector<std::pair<int, double>> &out) {
+            if (j < n2)
+                for (int p = L.colptr[j]; p < L.colptr[j + 1]; ++p) out.push_back({L.rowidx[p], L.val[p]});
+            else if (j < n2 + m2)
+                out.push_back({j - n2, 1.0});
+        }, ws, wi, wvv);
+        if ((rc = upload(&c->d_wslot, ws)) || (rc = upload(&c->d_wix, wi)) || (rc = upload(&c->d_wv, wvv))) return rc;
+        // packed-4 pricing layout when every column has <= 4 entries and m2 < 0xFFFF
+        int maxnnz = 1;
+        for (int j = 0; j < n2; ++j) maxnnz = std::max(maxnnz, L.colptr[j + 1] - L.colptr[j]);
+        // opt-in (TWOSD_PACK4=1): measured slower than sliced ELL on storm (divergent branches)
+        c->has_pack4 = maxnnz <= 4 && m2 < 0xFFFF && getenv("TWOSD_PACK4") && std::string(getenv("TWOSD_PACK4")) == "1";
+        if (c->has_pack4) {
+            const int S = c->CH;
+            std::vector<unsigned long long> pk((size_t)S * 64, ~0ull);
+            std::vector<double> pv((size_t)S * 256, 0.0);
+            for (int j = 0; j < 64 * S && j < n2 + m2; ++j) {
+                const int s = j >> 6, l = j & 63;
+                unsigned long long word = ~0ull;
+                int e = 0;
+                auto put = [&](int row, double v) {
+                    word &= ~(0xFFFFull << (16 * e));
+                    word |= (unsigned long long)row << (16 * e);
+                    pv[((size_t)s * 4 + e) * 64 + l] = v;
+                    ++e;
+                };
+                if (j < n2)
+                    for (int p = L.colptr[j]; p < L.colptr[j + 1]; ++p) put(L.rowidx[p], L.val[p]);
+                else
+                    put(j - n2, 1.0);
+                pk[(size_t)s * 64 + l] = word;
+            }
+            if ((rc = upload(&c->d_wrow4, pk)) || (rc = upload(&c->d_wval4, pv))) return rc;
+        }
+    }
     c->has_template = true;
     c->k = 0;
     c->pos_row.clear(); c->pos_col.clear();
@@ -280,6 +359,59 @@ static int install_basis(twosd_ctx *c, const std::vector<int> &head) {
     HIPCHK(hipMemcpy(c->d_B0inv, Bp.data(), sizeof(double) * m * MP, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d_B0invT, BTp.data(), sizeof(double) * m * MP, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d_pi0, pip.data(), sizeof(double) * MP, hipMemcpyHostToDevice));
+    // hypersparse form: B0^{-1} CSC over MP (padded) columns, reduced costs d0 in lane-slot order
+    if (c->CH > 0) {
+        double amax = 0.0;
+        for (double v : Binv) amax = std::max(amax, std::fabs(v));
+        const double drop = 1e-14 * amax;
+        std::vector<int> cp(MP + 1, 0), ri;
+        std::vector<double> vv;
+        for (int cc = 0; cc < MP; ++cc) {
+            if (cc < m)
+                for (int i = 0; i < m; ++i) {
+                    const double v = Binv[(size_t)i * m + cc];
+                    if (std::fabs(v) > drop) { ri.push_back(i); vv.push_back(v); }
+                }
+            cp[cc + 1] = (int)ri.size();
+        }
+        std::vector<double> d0((size_t)64 * c->CH, 0.0);
+        for (int j = 0; j < n + m; ++j) {
+            if (seen[j]) continue;   // basic
+            double s = 0.0;
+            if (j >= n) s = pi0[j - n];
+            else
+                for (int p = L.colptr[j]; p < L.colptr[j + 1]; ++p) s += pi0[L.rowidx[p]] * L.val[p];
+            d0[j] = (j < n ? L.q[j] : 0.0) - s;
+        }
+        std::vector<int> bs, bi;
+        std::vector<double> bvv;
+        build_ell(c->R, [&](int cc, std::vector<std::pair<int, double>> &out) {
+            for (int p = cp[cc]; p < cp[cc + 1]; ++p) out.push_back({ri[p], vv[p]});
+        }, bs, bi, bvv);
+        if ((rc = upload(&c->d_bslot, bs)) || (rc = upload(&c->d_bix, bi)) || (rc = upload(&c->d_bv, bvv))) return rc;
+        // CSR of B0^{-1} over MP rows (row scatter of rho)
+        std::vector<int> rp(MP + 1, 0), rcix;
+        std::vector<double> rvv;
+        for (int i = 0; i < MP; ++i) {
+            if (i < m)
+                for (int cc = 0; cc < m; ++cc) {
+                    const double v = Binv[(size_t)i * m + cc];
+                    if (std::fabs(v) > drop) { rcix.push_back(cc); rvv.push_back(v); }
+                }
+            rp[i + 1] = (int)rcix.size();
+        }
+        if ((rc = upload(&c->d_brptr, rp)) || (rc = upload(&c->d_brcol, rcix)) || (rc = upload(&c->d_brval, rvv))) return rc;
+        if ((rc = dalloc(&c->d_bcolptr, MP + 1)) || (rc = dalloc(&c->d_browidx, ri.size())) ||
+            (rc = dalloc(&c->d_bval, vv.size())) || (rc = dalloc(&c->d_d0, d0.size())))
+            return rc;
+        HIPCHK(hipMemcpy(c->d_bcolptr, cp.data(), sizeof(int) * (MP + 1), hipMemcpyHostToDevice));
+        if (!ri.empty()) {
+            HIPCHK(hipMemcpy(c->d_browidx, ri.data(), sizeof(int) * ri.size(), hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(c->d_bval, vv.data(), sizeof(double) * vv.size(), hipMemcpyHostToDevice));
+        }
+        HIPCHK(hipMemcpy(c->d_d0, d0.data(), sizeof(double) * d0.size(), hipMemcpyHostToDevice));
+        c->b0_nnz = (int64_t)ri.size();
+    }
     c->has_basis = true;
     c->prep_valid = false;
     return TWOSD_OK;
@@ -378,6 +510,29 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
     if ((rc = dalloc(&c->d_B0K, (size_t)std::max(k, 1) * MP))) return rc;
     HIPCHK(hipMemcpyAsync(c->d_xbase, xb.data(), sizeof(double) * MP, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->d_B0K, bk.data(), sizeof(double) * std::max(k, 1) * MP, hipMemcpyHostToDevice, c->stream));
+    // hypersparse kernel: the same B0K as CSR by row (row i: (e, coef_e B0^{-1}[i][row_e]))
+    std::vector<int> kp(MP + 1, 0), ki;
+    std::vector<double> kv;
+    if (c->CH > 0) {
+        double amax = 0.0;
+        for (double v : c->B0inv) amax = std::max(amax, std::fabs(v));
+        const double drop = 1e-14 * amax;
+        for (int i = 0; i < MP; ++i) {
+            if (i < m)
+                for (int e = 0; e < k; ++e) {
+                    const double v = bk[(size_t)e * MP + i];
+                    if (std::fabs(c->B0inv[(size_t)i * m + c->pos_row[e]]) > drop && v != 0.0) { ki.push_back(e); kv.push_back(v); }
+                }
+            kp[i + 1] = (int)ki.size();
+        }
+        if ((rc = dalloc(&c->d_kptr, MP + 1)) || (rc = dalloc(&c->d_kidx, ki.size())) || (rc = dalloc(&c->d_kval, kv.size())))
+            return rc;
+        HIPCHK(hipMemcpyAsync(c->d_kptr, kp.data(), sizeof(int) * (MP + 1), hipMemcpyHostToDevice, c->stream));
+        if (!ki.empty()) {
+            HIPCHK(hipMemcpyAsync(c->d_kidx, ki.data(), sizeof(int) * ki.size(), hipMemcpyHostToDevice, c->stream));
+            HIPCHK(hipMemcpyAsync(c->d_kval, kv.data(), sizeof(double) * kv.size(), hipMemcpyHostToDevice, c->stream));
+        }
+    }
     HIPCHK(hipStreamSynchronize(c->stream));
     c->prep_x.assign(x, x + n1);
     c->prep_valid = true;
@@ -407,6 +562,53 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
         if ((rc = dalloc(&c->d_y, (size_t)c->out_cap * n))) return rc;
         c->y_cap = c->out_cap;
     }
+    if (!c->d_queue && (rc = dalloc(&c->d_queue, 4))) return rc;
+    if (c->use_hyper) {
+        const int kmax = c->kmax_override > 0 ? c->kmax_override : std::min(512, std::max(64, 2 * m + 32));
+        const int ecap = std::max(4096, 32 * MP);
+        const int CH = c->CH;
+        const int bpc = hyper_max_blocks_per_cu(R, CH, kmax);
+        const int nblocks = std::max(1, std::min((N + kWavesPerBlock - 1) / kWavesPerBlock, bpc * c->num_cus));
+        const size_t slots = (size_t)nblocks * kWavesPerBlock;
+        if (slots > c->earena_slots || ecap != c->earena_cap) {
+            if ((rc = dalloc(&c->d_eidx, slots * ecap)) || (rc = dalloc(&c->d_evals, slots * ecap))) return rc;
+            c->earena_slots = slots;
+            c->earena_cap = ecap;
+        }
+        HIPCHK(hipMemsetAsync(c->d_queue, 0, sizeof(int) * 4, c->stream));
+        HyperParams H{};
+        H.m = m; H.n = n; H.k = c->k; H.N = N; H.kmax = kmax; H.ecap = ecap;
+        H.colptr = c->d_colptr; H.rowidx = c->d_rowidx; H.val = c->d_val; H.q = c->d_q; H.btype = c->d_btype;
+        H.bcolptr = c->d_bcolptr; H.browidx = c->d_browidx; H.bval = c->d_bval;
+        H.wslot = c->d_wslot; H.wix = c->d_wix; H.wv = c->d_wv;
+        H.bslot = c->d_bslot; H.bix = c->d_bix; H.bv = c->d_bv;
+        H.brptr = c->d_brptr; H.brcol = c->d_brcol; H.brval = c->d_brval;
+        H.wrow4 = c->has_pack4 ? c->d_wrow4 : nullptr;
+        H.wval4 = c->has_pack4 ? c->d_wval4 : nullptr;
+        H.kptr = c->d_kptr; H.kidx = c->d_kidx; H.kval = c->d_kval;
+        H.xbase = c->d_xbase; H.d0 = c->d_d0; H.hb0 = c->d_hb0;
+        H.basic0 = c->d_basic0; H.fixedmask = c->d_fixedmask; H.ubmask = c->d_ubmask;
+        H.dv = d_dv; H.eidx = c->d_eidx; H.evals = c->d_evals; H.queue = c->d_queue;
+        H.obj = c->d_obj; H.pi = want_pi ? c->d_pi : nullptr; H.y = want_y ? c->d_y : nullptr;
+        H.status = c->d_status; H.iters = c->d_iters; H.ops = c->d_ops;
+        if (!c->d_stamps) {
+            if ((rc = dalloc(&c->d_stamps, 16))) return rc;
+            HIPCHK(hipMemset(c->d_stamps, 0, sizeof(unsigned long long) * 16));
+        }
+        H.stamps = c->d_stamps;
+        HIPCHK(hipEventRecord(c->ev[0], c->stream));
+        HIPCHK(launch_hyper(R, CH, H, nblocks, hyper_lds_bytes(R, kmax), c->stream));
+        HIPCHK(hipEventRecord(c->ev[1], c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        float ms = 0;
+        hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
+        c->t_us[0] = 1e3 * ms;
+        c->last_lp_N = N;
+        c->last_lp_blocks = nblocks;
+        c->last_ops_width = 1;
+        return TWOSD_OK;
+    }
+    c->last_ops_width = MP;
     const int kmax = c->kmax_override > 0 ? c->kmax_override : std::min(1024, std::max(64, 2 * m + 32));
     const int bpc = lp_max_blocks_per_cu(R, kmax);
     const int nblocks = std::max(1, std::min((N + kWavesPerBlock - 1) / kWavesPerBlock, bpc * c->num_cus));
@@ -501,10 +703,19 @@ extern "C" int twosd_last_lp_stats(twosd_ctx *c, int64_t *sum, int *mx) {
     return TWOSD_OK;
 }
 
+extern "C" int twosd_debug_stamps(twosd_ctx *c, uint64_t *out10, int reset) {
+    if (!c || !out10) return fail(TWOSD_E_ARG, "debug_stamps: NULL");
+    for (int i = 0; i < 10; ++i) out10[i] = 0;
+    if (!c->d_stamps) return TWOSD_OK;
+    HIPCHK(hipMemcpy(out10, c->d_stamps, sizeof(uint64_t) * 10, hipMemcpyDeviceToHost));
+    if (reset) HIPCHK(hipMemset(c->d_stamps, 0, sizeof(uint64_t) * 16));
+    return TWOSD_OK;
+}
+
 extern "C" int twosd_last_lp_ops(twosd_ctx *c, int64_t *row_ops, int *row_width) {
     if (!c) return fail(TWOSD_E_ARG, "last_lp_ops: NULL");
     if (row_ops) *row_ops = c->last_ops_sum;
-    if (row_width) *row_width = c->MP;
+    if (row_width) *row_width = c->last_ops_width;
     return TWOSD_OK;
 }
 

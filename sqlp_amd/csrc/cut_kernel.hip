@@ -258,12 +258,31 @@ __global__ void __launch_bounds__(256) cut_fixup_kernel(CutParams P, int slot0) 
     }
 }
 
-// sums[c] = sum over slots (in slot order) of partial[slot][c], c < k+1
-__global__ void cut_reduce_kernel(int slots, int width, const double *__restrict__ partial, double *__restrict__ sums) {
+// sums[c] = sum over slots of partial[slot][c], c < k+1, in a fixed order: block b sums
+// the slot range [b*per, (b+1)*per) with a fixed-shape in-block tree, then the last level
+// adds the block results in block order (deterministic, independent of timing).
+constexpr int kReduceBlocks = 64;
+__global__ void __launch_bounds__(256) cut_reduce1_kernel(int slots, int width, const double *__restrict__ partial,
+                                                          double *__restrict__ part2) {
+    __shared__ double sh[256];
+    const int b = blockIdx.x, c = blockIdx.y;
+    const int per = (slots + kReduceBlocks - 1) / kReduceBlocks;
+    const int s0 = b * per, s1 = min(slots, s0 + per);
+    double s = 0.0;
+    for (int i = s0 + threadIdx.x; i < s1; i += 256) s += partial[(size_t)i * width + c];
+    sh[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part2[(size_t)c * kReduceBlocks + b] = sh[0];
+}
+__global__ void cut_reduce2_kernel(int width, const double *__restrict__ part2, double *__restrict__ sums) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= width) return;
     double s = 0.0;
-    for (int i = 0; i < slots; ++i) s += partial[(size_t)i * width + c];
+    for (int b = 0; b < kReduceBlocks; ++b) s += part2[(size_t)c * kReduceBlocks + b];
     sums[c] = s;
 }
 
@@ -301,7 +320,8 @@ struct CutWs {
     int *arg = nullptr, *flag = nullptr;
     double *val = nullptr;
     unsigned long long *hist = nullptr;
-    size_t base_cap = 0, part_cap = 0, n_cap = 0, hist_cap = 0, gpart_cap = 0, sums_cap = 0;
+    double *part2 = nullptr;
+    size_t base_cap = 0, part_cap = 0, n_cap = 0, hist_cap = 0, gpart_cap = 0, sums_cap = 0, part2_cap = 0;
     int m = 0, vec_m = 0;
     std::vector<double> h_coef, h_bvec;   // pinned-lifetime host staging for async uploads
 };
@@ -316,7 +336,7 @@ void cut_free(twosd_ctx *c) {
     CutWs *w = (CutWs *)c->cut_ws;
     hipFree(w->PK); hipFree(w->PKT); hipFree(w->rows); hipFree(w->coef); hipFree(w->bvec); hipFree(w->base);
     hipFree(w->partial); hipFree(w->sums); hipFree(w->gpart); hipFree(w->g); hipFree(w->arg); hipFree(w->flag);
-    hipFree(w->val); hipFree(w->hist);
+    hipFree(w->val); hipFree(w->hist); hipFree(w->part2);
     delete w;
     c->cut_ws = nullptr;
 }
@@ -454,8 +474,13 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     P.arg = w->arg; P.val = w->val; P.flag = w->flag; P.hist = d_hist; P.partial = w->partial;
     launch_argmax(KB, P, nblocks, c->stream);
     hipLaunchKernelGGL(cut_fixup_kernel, dim3(fix_blocks), dim3(256), 0, c->stream, P, nblocks * 4);
-    hipLaunchKernelGGL(cut_reduce_kernel, dim3((k + 1 + 63) / 64), dim3(64), 0, c->stream, (int)slots, k + 1, w->partial,
-                       d_sums);
+    if ((size_t)(k + 1) * kReduceBlocks > w->part2_cap) {
+        if ((rc = realloc_dev(&w->part2, (size_t)(k + 1) * kReduceBlocks))) return rc;
+        w->part2_cap = (size_t)(k + 1) * kReduceBlocks;
+    }
+    hipLaunchKernelGGL(cut_reduce1_kernel, dim3(kReduceBlocks, k + 1), dim3(256), 0, c->stream, (int)slots, k + 1,
+                       w->partial, w->part2);
+    hipLaunchKernelGGL(cut_reduce2_kernel, dim3((k + 1 + 63) / 64), dim3(64), 0, c->stream, k + 1, w->part2, d_sums);
     HIPCHK(hipGetLastError());
     return TWOSD_OK;
 }

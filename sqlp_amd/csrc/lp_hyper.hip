@@ -1,0 +1,604 @@
+// lp_hyper.hip -- hypersparse batched dual simplex for the stage-2 LPs (gfx950).
+//
+// Same problem, pivot rules and outputs as lp_kernel.hip (solve_problem!,
+// src/smps/smps_routines.jl:50-62), restructured for what the SMPS recourse matrices
+// look like: B0^{-1} of storm is 1.2 % dense (about 6 nonzeros per row/column) and
+// the FTRAN columns B^{-1} a_q about 1 %, so every 64R-wide dense row operation of the
+// dense kernel is ~99 % zeros.  Here:
+//   * B0^{-1} is stored CSC (column c -> (row i, B0^{-1}[i][c])), shared by all waves;
+//   * the eta file of a wave is a sparse arena (row index, value) in HBM (L1/L2 hits in
+//     practice), its pivot rows and offsets in the wave's LDS slice;
+//   * BTRAN: u = e_r' E_K..E_1 with u dense in LDS, each eta a lane-parallel sparse dot;
+//     rho_c = sum_i u_i B0^{-1}[i][c] as lane-parallel gathers over B0^{-1} columns;
+//   * reduced costs d_j live in registers of the lane that owns column j (j = 64c+lane,
+//     C slots, template parameter) and are updated in place (no dual vector, no pi);
+//   * FTRAN: scatter of the sparse B0^{-1} columns of a_q, then the sparse etas;
+//   * x_B and dual Devex weights stay in registers (row i: lane i%64, slot i/64).
+// The leaving-row choice, Harris two-pass ratio test and tie breaks are those of
+// lp_kernel.hip, so both kernels follow the same pivot path up to rounding.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include "twosd_internal.h"
+#include "wave_ops.h"
+
+namespace twosd {
+
+#define HTOL_P 1e-9
+#define HTOL_D 1e-9
+#define HTOL_PIV 1e-9
+#define HPI_ZERO 1e-12
+
+// Diagnostic build (-DTWOSD_STAMPS, libtwosd_hip_stamps.so): per-phase s_memtime cycle
+// totals summed over waves.  Never used for timing claims (stamps perturb the schedule).
+#ifdef TWOSD_STAMPS
+#define STAMP_DECL unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
+    unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#define STAMP(i)                                                      \
+    {                                                                 \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();   \
+        st_acc[i] += t_ - st_last;                                    \
+        st_last = t_;                                                 \
+    }
+#define STAMP_FLUSH                                                                         \
+    if (lane == 0 && P.stamps)                                                              \
+        for (int i_ = 0; i_ < 10; ++i_) atomicAdd(&P.stamps[i_], st_acc[i_]);
+#else
+#define STAMP_DECL
+#define STAMP(i)
+#define STAMP_FLUSH
+#endif
+
+__device__ __forceinline__ double h_wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ double h_wave_min(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ void h_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ double h_infeas(double x, int bt) {
+    if (bt == BT_Y || bt == BT_L) return x < -HTOL_P ? x : 0.0;
+    if (bt == BT_G) return x > HTOL_P ? x : 0.0;
+    return fabs(x) > HTOL_P ? x : 0.0;
+}
+
+template <int R>
+__device__ __forceinline__ int h_get_row_i(const int (&a)[R], int p) {
+    const int slot = p >> 6;
+    int v = a[0];
+#pragma unroll
+    for (int t = 1; t < R; ++t)
+        if (t == slot) v = a[t];
+    return __builtin_amdgcn_readlane(v, p & 63);
+}
+
+size_t hyper_lds_bytes(int R, int kmax) {
+    const int kmaxp = (kmax + 3) & ~3;
+    return (size_t)kWavesPerBlock * (16 * 64 * R + 2 * kmaxp + 4 * (kmaxp + 4));
+}
+
+// min waves per SIMD (VGPR budget 256 / 168): measured on MI355X, storm (R=9) is fastest
+// at 2 waves/SIMD, ssn (R=4) at 3 (tools/lp_speed.py)
+#ifndef TWOSD_HYPER_WPE
+#define TWOSD_HYPER_WPE(R) ((R) >= 9 ? 2 : 3)
+#endif
+template <int R, int C>
+__global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(HyperParams P) {
+    extern __shared__ double lds_raw[];
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    constexpr int MP = 64 * R;
+    const int kmaxp = (P.kmax + 3) & ~3;
+    char *slice = reinterpret_cast<char *>(lds_raw) + (size_t)wid * (16 * MP + 2 * kmaxp + 4 * (kmaxp + 4));
+    double *ut = reinterpret_cast<double *>(slice);        // dense scratch vector (u, then alpha_q)
+    double *rho = ut + MP;                                  // pivot row of B^{-1}
+    unsigned short *etap = reinterpret_cast<unsigned short *>(rho + MP);
+    int *etaoff = reinterpret_cast<int *>(etap + kmaxp);
+
+    const int m = P.m, n = P.n;
+    const int slot_id = blockIdx.x * kWavesPerBlock + wid;
+    int *eidx = P.eidx + (size_t)slot_id * P.ecap;
+    double *evals = P.evals + (size_t)slot_id * P.ecap;
+    const uint64_t fixedm = P.fixedmask[lane];
+    const uint64_t ubm = P.ubmask[lane];
+
+#pragma unroll
+    for (int t = 0; t < R; ++t) { ut[64 * t + lane] = 0.0; rho[64 * t + lane] = 0.0; }
+    h_wave_sync();
+    STAMP_DECL
+
+    for (;;) {
+        int s = 0;
+        if (lane == 0) s = atomicAdd(P.queue, 1);
+        s = __builtin_amdgcn_readfirstlane(__shfl(s, 0));
+        if (s >= P.N) break;
+
+        const double *dvs = P.dv + (size_t)s * P.k;
+        double xB[R];
+        float w[R];
+        int hb[R];
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+            const int i = 64 * t + lane;
+            double x = P.xbase[i];
+            const int p0 = P.kptr[i], p1 = P.kptr[i + 1];
+            for (int p = p0; p < p1; ++p) x = fma(P.kval[p], dvs[P.kidx[p]], x);
+            xB[t] = x;
+            hb[t] = P.hb0[i];
+            w[t] = 1.0f;
+        }
+        double d[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) d[c] = P.d0[64 * c + lane];
+        uint64_t bmask = P.basic0[lane];
+        int K = 0, it = 0, status = TWOSD_LP_OPTIMAL;
+        int eoff = 0;
+        long long nops = P.kptr[MP];
+        if (lane == 0) etaoff[0] = 0;
+        h_wave_sync();
+        STAMP(0)
+
+        for (;;) {
+            // ---- 1. leaving row (same rule as lp_kernel.hip)
+            double best = 0.0, bdel = 0.0;
+            int br = 0x7fffffff;
+#pragma unroll
+            for (int t = 0; t < R; ++t) {
+                if (hb[t] < 0) continue;
+                const double dl = h_infeas(xB[t], hb[t] & 3);
+                if (dl != 0.0) {
+                    const double sc = dl * dl / (double)w[t];
+                    if (sc > best) { best = sc; br = 64 * t + lane; bdel = dl; }
+                }
+            }
+            const ArgBest lr = warg_max(best, br, bdel, 0.0);
+            const int r = lr.idx;
+            STAMP(1)
+            if (lr.key == 0.0) break;
+            if (K >= P.kmax) { status = TWOSD_LP_ITER_LIMIT; break; }
+            const double delta = lr.p0;
+
+            // ---- 2. BTRAN: u = e_r' E_K..E_1 (u dense in LDS), rho = u' B0^{-1}
+            if (lane == (r & 63)) ut[r] = 1.0;
+            h_wave_sync();
+            // etas in groups of 4: the group's entries (first 64 of each) are loaded together,
+            // so one memory round trip serves four sequential steps
+            for (int tg = K - 1; tg >= 0; tg -= 4) {
+                int gi[4], gn[4], go[4];
+                double gv[4];
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int tt = tg - g;
+                    gi[g] = 0; gv[g] = 0.0; gn[g] = 0; go[g] = 0;
+                    if (tt >= 0) {
+                        go[g] = etaoff[tt];
+                        gn[g] = etaoff[tt + 1] - go[g];
+                        if (lane < gn[g]) { gi[g] = eidx[go[g] + lane]; gv[g] = evals[go[g] + lane]; }
+                    }
+                }
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int tt = tg - g;
+                    if (tt < 0) break;
+                    double acc = gv[g] != 0.0 ? ut[gi[g]] * gv[g] : 0.0;
+                    for (int e = 64 + lane; e < gn[g]; e += 64) acc = fma(ut[eidx[go[g] + e]], evals[go[g] + e], acc);
+                    acc = wsum(acc);
+                    nops += gn[g];
+                    if (lane == 0) ut[etap[tt]] = acc;
+                    h_wave_sync();
+                }
+            }
+            STAMP(2)
+            // rho = u' B0^{-1} as a row scatter over the nonzeros of u, which sit at r and at
+            // the eta pivot rows; each row is consumed once (then zeroed), in the fixed order
+            // r, etap[K-1], ..., etap[0], so the accumulation order is deterministic.
+            for (int tg = K; tg >= 0; tg -= 4) {
+                int gi[4], gn[4], gp[4], go[4];
+                double gv[4];
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int tt = tg - g;
+                    gi[g] = 0; gv[g] = 0.0; gn[g] = 0; go[g] = 0; gp[g] = 0;
+                    if (tt >= 0) {
+                        gp[g] = (tt == K) ? r : (int)etap[tt];
+                        go[g] = P.brptr[gp[g]];
+                        gn[g] = P.brptr[gp[g] + 1] - go[g];
+                        if (lane < gn[g]) { gi[g] = P.brcol[go[g] + lane]; gv[g] = P.brval[go[g] + lane]; }
+                    }
+                }
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int tt = tg - g;
+                    if (tt < 0) break;
+                    const double up = ut[gp[g]];
+                    if (up != 0.0) {
+                        if (lane < gn[g]) rho[gi[g]] = fma(up, gv[g], rho[gi[g]]);
+                        for (int e = 64 + lane; e < gn[g]; e += 64)
+                            rho[P.brcol[go[g] + e]] = fma(up, P.brval[go[g] + e], rho[P.brcol[go[g] + e]]);
+                        nops += gn[g];
+                        h_wave_sync();
+                        if (lane == 0) ut[gp[g]] = 0.0;
+                    }
+                    h_wave_sync();
+                }
+            }
+            STAMP(3)
+
+            // ---- 3. Harris ratio test over nonbasic columns.  d lives in registers; the pivot
+            // row alpha~ is recomputed (same gathers, same order -> same bits) in passes 2/3
+            // only for the few columns pass 1 found nonzero / eligible (rho is ~2-5 % dense).
+            auto alpha_col = [&](int c) -> double {
+                const int e0 = P.wslot[c], e1 = P.wslot[c + 1];
+                double a = 0.0;
+#pragma unroll 1
+                for (int e = e0; e < e1; ++e) {
+                    const double v = P.wv[e * 64 + lane];
+                    a = fma(rho[P.wix[e * 64 + lane]], v, a);
+                }
+                return a;
+            };
+            const double sg = delta > 0 ? 1.0 : -1.0;
+            double thmax = INFINITY;
+            uint64_t nzm = 0, elm = 0;
+            // per-lane register list of the first kLCap nonzero alpha~ (slot, value, d)
+            constexpr int kLCap = 6;
+            double lv[kLCap], ld[kLCap];
+            int ls[kLCap];
+            int lcnt = 0;
+#pragma unroll
+            for (int i = 0; i < kLCap; ++i) { lv[i] = 0.0; ld[i] = 0.0; ls[i] = -1; }
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const uint64_t bit = 1ull << c;
+                if ((bmask | fixedm) & bit) continue;
+                const double a = sg * alpha_col(c);
+                if (a != 0.0) {
+                    nzm |= bit;
+#pragma unroll
+                    for (int i = 0; i < kLCap; ++i)
+                        if (i == lcnt) { lv[i] = a; ld[i] = d[c]; ls[i] = c; }
+                    ++lcnt;
+                }
+                const bool atlb = !(ubm & bit);
+                if (atlb ? a > HTOL_PIV : a < -HTOL_PIV) {
+                    elm |= bit;
+                    thmax = fmin(thmax, ((atlb ? d[c] + HTOL_D : d[c] - HTOL_D)) / a);
+                }
+            }
+            thmax = wmin(thmax);
+            STAMP(4)
+            if (thmax == INFINITY) {
+                status = TWOSD_LP_INFEASIBLE;
+                h_wave_sync();
+#pragma unroll
+                for (int t = 0; t < R; ++t) rho[64 * t + lane] = 0.0;
+                break;
+            }
+            double bA = 0.0, bD = 0.0, bAs = 0.0;
+            int bq = 0x7fffffff;
+            // eligible columns held in the list (slot order, so the scan order is unchanged)
+#pragma unroll
+            for (int i = 0; i < kLCap; ++i) {
+                if (ls[i] < 0 || !((elm >> ls[i]) & 1ull)) continue;
+                const double a = lv[i];
+                if (ld[i] / a <= thmax && fabs(a) > bA) { bA = fabs(a); bq = 64 * ls[i] + lane; bD = ld[i]; bAs = a; }
+            }
+            if (lcnt > kLCap) {   // rare overflow: slots past the list are recomputed
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    if (!(elm & (1ull << c)) || c <= ls[kLCap - 1]) continue;
+                    const double a = sg * alpha_col(c);
+                    if (d[c] / a <= thmax && fabs(a) > bA) { bA = fabs(a); bq = 64 * c + lane; bD = d[c]; bAs = a; }
+                }
+            }
+            const ArgBest eq = warg_max(bA, bq, bD, bAs);
+            const int q = eq.idx;
+            STAMP(5)
+            if (eq.key == 0.0) {
+                status = TWOSD_LP_NUMERIC;
+                h_wave_sync();
+#pragma unroll
+                for (int t = 0; t < R; ++t) rho[64 * t + lane] = 0.0;
+                break;
+            }
+            const double thetaD = eq.p0 / eq.p1;
+            // pass 3: d_j -= thetaD * alpha~_j for every nonbasic column with alpha_j != 0
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                if (!(nzm & (1ull << c))) continue;
+                double a = 0.0;
+                bool inlist = false;
+#pragma unroll
+                for (int i = 0; i < kLCap; ++i)
+                    if (ls[i] == c) { a = lv[i]; inlist = true; }
+                if (!inlist) a = sg * alpha_col(c);
+                d[c] = fma(-thetaD, a, d[c]);
+            }
+            h_wave_sync();
+#pragma unroll
+            for (int t = 0; t < R; ++t) rho[64 * t + lane] = 0.0;   // rho is rebuilt by scatter next pivot
+            nops += P.wslot[C] * 64;
+            STAMP(6)
+
+            // ---- 4. FTRAN: ut = E_K..E_1 B0^{-1} a_q (ut is all zeros here).  Column cc of
+            // B0^{-1} is ELL slot cc/64, lane cc%64: its entry e sits at (bslot + e)*64 + cc%64.
+            {
+                const int np0 = q >= n ? 0 : P.colptr[q], np1 = q >= n ? 1 : P.colptr[q + 1];
+                for (int pw = np0; pw < np1; ++pw) {
+                    const int cc = q >= n ? q - n : P.rowidx[pw];
+                    const double aw = q >= n ? 1.0 : P.val[pw];
+                    const int ts = cc >> 6, cl = cc & 63;
+                    const int e0 = P.bslot[ts], e1 = P.bslot[ts + 1];
+                    for (int e = e0 + lane; e < e1; e += 64) {
+                        const double v = P.bv[e * 64 + cl];
+                        if (v != 0.0) {
+                            const int i = P.bix[e * 64 + cl];
+                            ut[i] = fma(aw, v, ut[i]);
+                        }
+                    }
+                    nops += e1 - e0;
+                    h_wave_sync();
+                }
+            }
+            for (int tg = 0; tg < K; tg += 4) {
+                int gi[4], gn[4], go[4];
+                double gv[4];
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int tt = tg + g;
+                    gi[g] = 0; gv[g] = 0.0; gn[g] = 0; go[g] = 0;
+                    if (tt < K) {
+                        go[g] = etaoff[tt];
+                        gn[g] = etaoff[tt + 1] - go[g];
+                        if (lane < gn[g]) { gi[g] = eidx[go[g] + lane]; gv[g] = evals[go[g] + lane]; }
+                    }
+                }
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int tt = tg + g;
+                    if (tt >= K) break;
+                    const int p = etap[tt];
+                    const double vp = ut[p];
+                    if (vp != 0.0) {
+                        if (lane < gn[g]) ut[gi[g]] = (gi[g] == p) ? gv[g] * vp : fma(gv[g], vp, ut[gi[g]]);
+                        for (int e = 64 + lane; e < gn[g]; e += 64) {
+                            const int i = eidx[go[g] + e];
+                            const double ev = evals[go[g] + e];
+                            ut[i] = (i == p) ? ev * vp : fma(ev, vp, ut[i]);
+                        }
+                        nops += gn[g];
+                    }
+                    h_wave_sync();
+                }
+            }
+            const double arq = ut[r];
+            double col[R];
+#pragma unroll
+            for (int t = 0; t < R; ++t) col[t] = ut[64 * t + lane];
+            h_wave_sync();
+#pragma unroll
+            for (int t = 0; t < R; ++t) ut[64 * t + lane] = 0.0;
+            STAMP(7)
+            if (fabs(arq) < 1e-12) { status = TWOSD_LP_NUMERIC; h_wave_sync(); break; }
+
+            // ---- 5. updates: primal, Devex, sparse eta, basis, reduced costs of q / leaving
+            const double thetaP = delta / arq;
+            const double inv_arq = 1.0 / arq;
+            float wrr = 0.0f;
+            {
+                const int slot = r >> 6;
+                float v = w[0];
+#pragma unroll
+                for (int t = 1; t < R; ++t)
+                    if (t == slot) v = w[t];
+                wrr = __shfl(v, r & 63);
+            }
+            int cnt = 0;
+#pragma unroll
+            for (int t = 0; t < R; ++t) cnt += __popcll(__ballot(col[t] != 0.0));
+            if (eoff + cnt > P.ecap) { status = TWOSD_LP_ITER_LIMIT; h_wave_sync(); break; }
+            int base = eoff;
+#pragma unroll
+            for (int t = 0; t < R; ++t) {
+                const int i = 64 * t + lane;
+                const bool nz = col[t] != 0.0;
+                const uint64_t bal = __ballot(nz);
+                if (nz) {
+                    const int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
+                    const double ratio = col[t] * inv_arq;
+                    eidx[pos] = i;
+                    evals[pos] = (i == r) ? inv_arq : -ratio;
+                    if (i == r) {
+                        xB[t] = thetaP;
+                        const float nw = (float)((double)wrr * inv_arq * inv_arq);
+                        w[t] = nw > 1.0f ? nw : 1.0f;
+                    } else {
+                        xB[t] = fma(-thetaP, col[t], xB[t]);
+                        const float cand = (float)(ratio * ratio * (double)wrr);
+                        w[t] = cand > w[t] ? cand : w[t];
+                    }
+                }
+                base += __popcll(bal);
+            }
+            eoff += cnt;
+            if (lane == 0) {
+                etap[K] = (unsigned short)r;
+                etaoff[K + 1] = eoff;
+            }
+            ++K;
+            const int leaving = h_get_row_i<R>(hb, r) >> 2;
+            // reduced cost of the leaving variable: -sg * thetaD; of q: 0
+            if (lane == (leaving & 63)) {
+                const int ls = leaving >> 6;
+                bmask &= ~(1ull << ls);
+#pragma unroll
+                for (int c = 0; c < C; ++c)
+                    if (c == ls) d[c] = -sg * thetaD;
+            }
+            if (lane == (q & 63)) {
+                const int qs = q >> 6;
+                bmask |= 1ull << qs;
+#pragma unroll
+                for (int c = 0; c < C; ++c)
+                    if (c == qs) d[c] = 0.0;
+            }
+            if (lane == (r & 63)) {
+                const int rs = r >> 6;
+#pragma unroll
+                for (int t = 0; t < R; ++t)
+                    if (t == rs) hb[t] = q * 4 + (int)P.btype[q];
+            }
+            ++it;
+            h_wave_sync();
+            STAMP(8)
+        }
+
+        // ---- vertex recovery: pi = c_B' B^{-1}
+        double objv = NAN;
+        if (status == TWOSD_LP_OPTIMAL) {
+#pragma unroll
+            for (int t = 0; t < R; ++t) {
+                const int j = hb[t] >> 2;
+                ut[64 * t + lane] = (hb[t] >= 0 && j < n) ? P.q[j] : 0.0;
+            }
+            h_wave_sync();
+            for (int tt = K - 1; tt >= 0; --tt) {
+                const int off = etaoff[tt], nnz = etaoff[tt + 1] - off;
+                double acc = 0.0;
+                for (int e = lane; e < nnz; e += 64) acc = fma(ut[eidx[off + e]], evals[off + e], acc);
+                acc = wsum(acc);
+                nops += nnz;
+                if (lane == 0) ut[etap[tt]] = acc;
+                h_wave_sync();
+            }
+            double pv[R];
+            double pmax = 0.0;
+#pragma unroll
+            for (int t = 0; t < R; ++t) {
+                const int e0 = P.bslot[t], e1 = P.bslot[t + 1];
+                double a = 0.0;
+#pragma unroll 1
+                for (int e = e0; e < e1; ++e) {
+                    const double v = P.bv[e * 64 + lane];
+                    a = fma(ut[P.bix[e * 64 + lane]], v, a);
+                }
+                pv[t] = a;
+                pmax = fmax(pmax, fabs(a));
+            }
+            nops += P.bcolptr[MP];
+            pmax = wmax(pmax);
+            const double zt = HPI_ZERO * (1.0 + pmax);
+            double ob = 0.0;
+#pragma unroll
+            for (int t = 0; t < R; ++t) {
+                if (fabs(pv[t]) <= zt) pv[t] = 0.0;
+                const int j = hb[t] >> 2;
+                if (hb[t] >= 0 && j < n) ob = fma(P.q[j], xB[t], ob);
+            }
+            objv = wsum(ob);
+            h_wave_sync();
+#pragma unroll
+            for (int t = 0; t < R; ++t) ut[64 * t + lane] = 0.0;
+            if (P.pi) {
+                double *po = P.pi + (size_t)s * m;
+#pragma unroll
+                for (int t = 0; t < R; ++t)
+                    if (64 * t + lane < m) po[64 * t + lane] = pv[t];
+            }
+            if (P.y) {
+                double *yo = P.y + (size_t)s * n;
+                for (int j = lane; j < n; j += 64) yo[j] = 0.0;
+                __builtin_amdgcn_s_waitcnt(0);
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int t = 0; t < R; ++t) {
+                    const int j = hb[t] >> 2;
+                    if (hb[t] >= 0 && j < n) yo[j] = xB[t];
+                }
+            }
+        } else if (P.pi) {
+            double *po = P.pi + (size_t)s * m;
+#pragma unroll
+            for (int t = 0; t < R; ++t)
+                if (64 * t + lane < m) po[64 * t + lane] = NAN;
+        }
+        if (lane == 0) {
+            P.obj[s] = objv;
+            P.status[s] = status;
+            P.iters[s] = it;
+            if (P.ops) P.ops[s] = nops;
+        }
+        h_wave_sync();
+        STAMP(9)
+    }
+    STAMP_FLUSH
+}
+
+// ---- dispatch: R in {1,2,4,9,16}, C in {2,4,8,16,32,64}
+static const int kHR[] = {1, 2, 4, 9, 16};
+static const int kHC[] = {2, 4, 8, 16, 32, 64};
+
+int hyper_rows_per_lane(int m) {
+    for (int R : kHR)
+        if (m <= 64 * R) return R;
+    return -1;
+}
+int hyper_cols_per_lane(int ncols) {
+    for (int C : kHC)
+        if (ncols <= 64 * C) return C;
+    return -1;
+}
+
+template <int R, int C>
+static hipError_t hl(const HyperParams &p, int nb, size_t lds, hipStream_t s) {
+    hipLaunchKernelGGL((lp_hyper_kernel<R, C>), dim3(nb), dim3(256), lds, s, p);
+    return hipGetLastError();
+}
+template <int R, int C>
+static int ho(size_t lds) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lp_hyper_kernel<R, C>, 256, lds) != hipSuccess) return 1;
+    return nb > 0 ? nb : 1;
+}
+
+#define HYPER_C_SWITCH(R, FN, ...)                  \
+    switch (C) {                                    \
+        case 2: return FN<R, 2>(__VA_ARGS__);       \
+        case 4: return FN<R, 4>(__VA_ARGS__);       \
+        case 8: return FN<R, 8>(__VA_ARGS__);       \
+        case 16: return FN<R, 16>(__VA_ARGS__);     \
+        case 32: return FN<R, 32>(__VA_ARGS__);     \
+        case 64: return FN<R, 64>(__VA_ARGS__);     \
+    }
+
+hipError_t launch_hyper(int R, int C, const HyperParams &p, int nblocks, size_t lds, hipStream_t s) {
+    switch (R) {
+        case 1: HYPER_C_SWITCH(1, hl, p, nblocks, lds, s); break;
+        case 2: HYPER_C_SWITCH(2, hl, p, nblocks, lds, s); break;
+        case 4: HYPER_C_SWITCH(4, hl, p, nblocks, lds, s); break;
+        case 9: HYPER_C_SWITCH(9, hl, p, nblocks, lds, s); break;
+        case 16: HYPER_C_SWITCH(16, hl, p, nblocks, lds, s); break;
+    }
+    return hipErrorInvalidValue;
+}
+
+int hyper_max_blocks_per_cu(int R, int C, int kmax) {
+    const size_t lds = hyper_lds_bytes(R, kmax);
+    switch (R) {
+        case 1: HYPER_C_SWITCH(1, ho, lds); break;
+        case 2: HYPER_C_SWITCH(2, ho, lds); break;
+        case 4: HYPER_C_SWITCH(4, ho, lds); break;
+        case 9: HYPER_C_SWITCH(9, ho, lds); break;
+        case 16: HYPER_C_SWITCH(16, ho, lds); break;
+    }
+    return 1;
+}
+
+}  // namespace twosd

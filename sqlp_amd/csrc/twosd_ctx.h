@@ -43,6 +43,26 @@ struct twosd_ctx {
     double *d_B0inv = nullptr, *d_B0invT = nullptr, *d_pi0 = nullptr, *d_xbase = nullptr, *d_B0K = nullptr;
     bool prep_valid = false;
     std::vector<double> prep_x;
+    // hypersparse kernel data
+    int CH = 0;                   // column slots per lane of the hypersparse kernel
+    bool use_hyper = true;
+    int *d_bcolptr = nullptr, *d_browidx = nullptr, *d_kptr = nullptr, *d_kidx = nullptr;
+    double *d_bval = nullptr, *d_kval = nullptr, *d_d0 = nullptr;
+    int *d_wslot = nullptr, *d_wix = nullptr, *d_bslot = nullptr, *d_bix = nullptr;
+    double *d_wv = nullptr, *d_bv = nullptr;
+    int *d_brptr = nullptr, *d_brcol = nullptr;
+    double *d_brval = nullptr;
+    bool has_pack4 = false;
+    unsigned long long *d_wrow4 = nullptr;
+    double *d_wval4 = nullptr;
+    int *d_eidx = nullptr;
+    double *d_evals = nullptr;
+    size_t earena_slots = 0;
+    int earena_cap = 0;
+    int64_t last_iterlimit = 0;
+    int64_t b0_nnz = 0;
+    unsigned long long *d_stamps = nullptr;
+    int last_ops_width = 1;
     // LP workspace + outputs
     double *d_eta = nullptr;
     size_t eta_slots = 0;

@@ -50,6 +50,38 @@ struct LpParams {
     long long *ops;        // N (nullable): executed 64R-wide fp64 row operations (FMA rows)
 };
 
+// hypersparse kernel (lp_hyper.hip)
+struct HyperParams {
+    int m, n, k, N, kmax, ecap;
+    const int *colptr, *rowidx; const double *val;      // W CSC
+    const double *q; const int8_t *btype;
+    const int *bcolptr, *browidx; const double *bval;   // B0^{-1} CSC, MP columns (padded empty)
+    // sliced-ELL copies (entry e of slot s for lane l at [(slot_off[s] + e) * 64 + l]; padding: idx 0, val 0):
+    const int *wslot, *wix; const double *wv;           // columns of [W I], C slots (j = 64c + lane)
+    const int *bslot, *bix; const double *bv;           // columns of B0^{-1}, R slots (c = 64t + lane)
+    const int *brptr, *brcol; const double *brval;      // B0^{-1} CSR (MP rows)
+    // packed pricing (all columns of [W I] with <= 4 entries): rows of column 64c+l as four
+    // 16-bit fields of wrow4[c*64+l] (0xFFFF = none), values at wval4[(c*4+e)*64+l]; null if unused
+    const unsigned long long *wrow4; const double *wval4;
+    const int *kptr, *kidx; const double *kval;         // B0K CSR by row (MP rows): (e, coef_e B0^{-1}[i][row_e])
+    const double *xbase;                                // MP
+    const double *d0;                                   // 64*C reduced costs at B0 (lane-slot order j = 64c+lane)
+    const int *hb0;                                     // MP
+    const uint64_t *basic0, *fixedmask, *ubmask;        // 64
+    const double *dv;                                   // N x k
+    int *eidx; double *evals;                           // nslots x ecap sparse eta arena
+    int *queue;
+    double *obj, *pi, *y;
+    int *status, *iters;
+    long long *ops;                                     // executed FMAs
+    unsigned long long *stamps;                         // [10] phase cycles (TWOSD_STAMPS builds only)
+};
+size_t hyper_lds_bytes(int R, int kmax);
+int hyper_rows_per_lane(int m);
+int hyper_cols_per_lane(int ncols);
+hipError_t launch_hyper(int R, int C, const HyperParams &p, int nblocks, size_t lds, hipStream_t s);
+int hyper_max_blocks_per_cu(int R, int C, int kmax);
+
 int lp_rows_per_lane(int m);   // supported R for m, or -1
 hipError_t launch_lp(int R, const LpParams &p, int nblocks, size_t lds_bytes, hipStream_t s);
 size_t lp_lds_bytes(int R, int kmax);

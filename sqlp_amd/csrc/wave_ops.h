@@ -1,0 +1,97 @@
+// wave_ops.h -- wavefront-64 reductions for gfx950 without LDS round trips.
+//
+// __shfl_xor lowers to ds_bpermute (an LDS-path round trip per 32-bit half); a double
+// reduction over 64 lanes then costs ~12 of them.  Here each 16-lane row is reduced with
+// DPP lane moves (quad_perm xor1, quad_perm xor2, row_half_mirror, row_mirror: every lane
+// of a row ends with the row result), then the four row results are combined in a fixed
+// order through v_readlane (lanes 0, 16, 32, 48).  The combine order is fixed, so the
+// result is bit-identical on every lane and every run.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace twosd {
+
+// DPP controls (GFX9 encoding)
+constexpr int kDppXor1 = 0xB1;        // quad_perm(1,0,3,2)
+constexpr int kDppXor2 = 0x4E;        // quad_perm(2,3,0,1)
+constexpr int kDppHalfMirror = 0x141; // row_half_mirror
+constexpr int kDppMirror = 0x140;     // row_mirror
+
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const int lo = dpp_i<CTRL>((int)(uint32_t)u);
+    const int hi = dpp_i<CTRL>((int)(uint32_t)(u >> 32));
+    return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+__device__ __forceinline__ double readlane_dbl(double v, int lane) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), lane);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// sum over the 64 lanes; every lane returns the same bits (uniform)
+__device__ __forceinline__ double wsum(double v) {
+    v += dpp_d<kDppXor1>(v);
+    v += dpp_d<kDppXor2>(v);
+    v += dpp_d<kDppHalfMirror>(v);
+    v += dpp_d<kDppMirror>(v);
+    return (readlane_dbl(v, 0) + readlane_dbl(v, 16)) + (readlane_dbl(v, 32) + readlane_dbl(v, 48));
+}
+
+__device__ __forceinline__ double wmin(double v) {
+    v = fmin(v, dpp_d<kDppXor1>(v));
+    v = fmin(v, dpp_d<kDppXor2>(v));
+    v = fmin(v, dpp_d<kDppHalfMirror>(v));
+    v = fmin(v, dpp_d<kDppMirror>(v));
+    return fmin(fmin(readlane_dbl(v, 0), readlane_dbl(v, 16)), fmin(readlane_dbl(v, 32), readlane_dbl(v, 48)));
+}
+
+__device__ __forceinline__ double wmax(double v) {
+    v = fmax(v, dpp_d<kDppXor1>(v));
+    v = fmax(v, dpp_d<kDppXor2>(v));
+    v = fmax(v, dpp_d<kDppHalfMirror>(v));
+    v = fmax(v, dpp_d<kDppMirror>(v));
+    return fmax(fmax(readlane_dbl(v, 0), readlane_dbl(v, 16)), fmax(readlane_dbl(v, 32), readlane_dbl(v, 48)));
+}
+
+// arg-reduction: the lane with the largest key (ties: smallest idx); returns the winning
+// idx (uniform) and the payload values of that lane.  Lanes without a candidate pass
+// key = -inf / idx = INT_MAX.
+struct ArgBest {
+    double key;
+    int idx;
+    double p0, p1;
+};
+template <int CTRL>
+__device__ __forceinline__ void arg_step(double &key, int &idx, double &p0, double &p1) {
+    const double k2 = dpp_d<CTRL>(key);
+    const int i2 = dpp_i<CTRL>(idx);
+    const double a2 = dpp_d<CTRL>(p0);
+    const double b2 = dpp_d<CTRL>(p1);
+    if (k2 > key || (k2 == key && i2 < idx)) { key = k2; idx = i2; p0 = a2; p1 = b2; }
+}
+__device__ __forceinline__ ArgBest warg_max(double key, int idx, double p0, double p1) {
+    arg_step<kDppXor1>(key, idx, p0, p1);
+    arg_step<kDppXor2>(key, idx, p0, p1);
+    arg_step<kDppHalfMirror>(key, idx, p0, p1);
+    arg_step<kDppMirror>(key, idx, p0, p1);
+    ArgBest b{readlane_dbl(key, 0), __builtin_amdgcn_readlane(idx, 0), readlane_dbl(p0, 0), readlane_dbl(p1, 0)};
+#pragma unroll
+    for (int l = 16; l < 64; l += 16) {
+        const double k2 = readlane_dbl(key, l);
+        const int i2 = __builtin_amdgcn_readlane(idx, l);
+        if (k2 > b.key || (k2 == b.key && i2 < b.idx)) {
+            b.key = k2; b.idx = i2; b.p0 = readlane_dbl(p0, l); b.p1 = readlane_dbl(p1, l);
+        }
+    }
+    return b;
+}
+
+}  // namespace twosd

@@ -1,0 +1,41 @@
+"""Development timing of the LP batch alone: python tools/lp_speed.py <instance> <N> [reps].
+Prints LP kernel ms (HIP events), scenarios/s and pivots; honours TWOSD_LIB / TWOSD_LP_KERNEL."""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    from sqlp_amd import smps, twosd
+    name = sys.argv[1] if len(sys.argv) > 1 else "storm"
+    N = int(sys.argv[2]) if len(sys.argv) > 2 else 100000
+    reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    d = os.path.join(ROOT, "data", "smps", name)
+    cor, tim, sto = smps.load_smps(d, name)
+    sp2 = smps.get_smps_stage_template(cor, tim, 2)
+    with open(os.path.join(ROOT, "tests", "golden", "ev_x.json")) as f:
+        x = np.array(json.load(f)[name]["x"])
+    ctx = twosd.SDContext(sp2, sto)
+    ctx.compute_basis(x, smps.mean_values(sto))
+    vals = smps.sample_values(sto, N, np.random.default_rng(1))
+    epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(epi, vals)
+    twosd.solve_batch(epi, x, 0, min(N, 4096), want_pi=False)
+    ts = []
+    for _ in range(reps):
+        obj, _, _, st = twosd.solve_batch(epi, x, 0, N, want_pi=False)
+        ts.append(ctx.timings_us()[0] / 1e3)
+    piv, pmax = ctx.lp_stats()
+    t = min(ts)
+    print(f"{os.environ.get('TWOSD_LIB', 'default')} {name} N={N} lp_ms={t:.2f} ({' '.join(f'{v:.1f}' for v in ts)}) "
+          f"scen/s={N / t * 1e3:.0f} pivots/scen={piv / N:.2f} max={pmax} status_ok={(st == 0).mean():.4f} "
+          f"objsum={obj.sum():.6e}")
+
+
+if __name__ == "__main__":
+    main()
