@@ -27,7 +27,7 @@ def round16(x: float) -> float:
     an exact power of two, round half-to-even, scale back.  Returns x itself when the
     scale overflows (Julia's _round_digits non-finite guard)."""
     x = float(x)
-    if x == 0.0:
+    if x == 0.0 or not math.isfinite(x):     # Base.round: `isfinite(x) || return x`
         return x
     m, e2 = math.frexp(x)           # x = m * 2**e2, 0.5 <= |m| < 1  -> exponent(x) = e2-1
     digits = SIGNIFICANT_DIGITS - e2

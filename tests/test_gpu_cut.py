@@ -1,0 +1,149 @@
+"""GPU argmax_procedure + build_sasa_cut (subprob.jl:141-169, epigraph.jl:125-146) vs the
+oracle: reference-order C port on the same V / scenarios / weights, the golden fixtures,
+multi-epigraph importance weights (config C5) and the sharded partial/finalize API."""
+import os
+
+import numpy as np
+import pytest
+
+from tests import instances as I
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _setup(name, nv_src=512, seed=3):
+    from sqlp_amd import smps, twosd
+    inst = I.load(name)
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    x = I.x_ev(name)
+    ctx.compute_basis(x, smps.mean_values(inst["sto"]))
+    V = twosd.sdDualVertexSet(ctx)
+    _, _, pis, st = ctx.solve_values(x, I.sample(name, nv_src, seed), want_pi=True)
+    V.push_batch(pis[st == 0])
+    return ctx, x, V
+
+
+@pytest.mark.parametrize("name,N", [("lands", 300), ("newsvendor", 200), ("transship", 700), ("ssn", 1500),
+                                    ("storm", 1000)])
+@pytest.mark.parametrize("tie_rel", [0.0, 1e-12])
+def test_cut_matches_oracle(name, N, tie_rel):
+    from oracle import cpu
+    from sqlp_amd import twosd
+    ctx, x, V = _setup(name)
+    vals = I.sample(name, N, seed=17)
+    w = np.random.default_rng(5).uniform(0.5, 1.5, size=N)
+    epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(epi, vals, w)
+    cut, mv, ma = twosd._build_cut(epi, x, tie_rel, want_argmax=True)
+    sp = I.load(name)["osp2"]
+    Vm = V.matrix()
+    a, b, omv, oma = cpu.build_cut(sp.r, sp.T, x, Vm, ctx.rows, vals - sp.r[ctx.rows], w, tie_rel=tie_rel, nthreads=4)
+    assert cut.weight_mark == pytest.approx(w.sum(), rel=1e-15)
+    np.testing.assert_allclose(mv, omv, rtol=1e-10, atol=1e-9)
+    scores = (Vm @ (sp.r - sp.T @ x))[None, :] + (vals - sp.r[ctx.rows]) @ Vm[:, ctx.rows].T
+    top2 = np.sort(scores, axis=1)[:, -2:] if Vm.shape[0] > 1 else np.hstack([scores, scores - 1])
+    clear = (top2[:, 1] - top2[:, 0]) > 1e-9 * (1 + np.abs(top2[:, 1]))
+    # argmax: identical index wherever the maximum is unambiguous; a valid argmax elsewhere
+    assert (ma[clear] == oma[clear]).all()
+    best = scores.max(1)
+    assert (scores[np.arange(N), ma] >= best - 1e-9 * (1 + np.abs(best))).all()
+    if tie_rel > 0 or clear.all():
+        assert cut.alpha == pytest.approx(a, rel=1e-8, abs=1e-8)        # north star: 1e-8 rel
+        np.testing.assert_allclose(cut.beta, b, rtol=1e-8, atol=1e-8 * (1 + np.abs(b).max()))
+    if tie_rel > 0:
+        assert (ma == oma).mean() > 0.999
+    # the cut equals the reference formula (epigraph.jl:134-143) over the GPU's own choices
+    p = w / w.sum()
+    ra = np.tile(sp.r, (N, 1))
+    ra[:, ctx.rows] = vals
+    a_ref = float(np.sum(p * np.einsum("ij,ij->i", Vm[ma], ra)))
+    b_ref = -(sp.T.T @ (p @ Vm[ma]))
+    assert cut.alpha == pytest.approx(a_ref, rel=1e-9, abs=1e-9)
+    np.testing.assert_allclose(cut.beta, b_ref, rtol=1e-9, atol=1e-9 * (1 + np.abs(b_ref).max()))
+
+
+@pytest.mark.parametrize("name", ["lands", "transship", "ssn", "storm"])
+def test_cut_golden_fixture(name):
+    from sqlp_amd import twosd
+    z = np.load(os.path.join(G, f"cut_{name}.npz"))
+    inst = I.load(name)
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    V = twosd.sdDualVertexSet(ctx)
+    idx = V.push_batch(z["V"])
+    assert idx.tolist() == list(range(len(z["V"])))
+    epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(epi, z["values"], z["w"])
+    cut, mv, ma = twosd._build_cut(epi, z["x"], 0.0, want_argmax=True)
+    assert (ma == z["max_arg"]).all()
+    assert cut.alpha == pytest.approx(float(z["alpha"]), rel=1e-8)
+    np.testing.assert_allclose(cut.beta, z["beta"], rtol=1e-8, atol=1e-8)
+    np.testing.assert_allclose(mv, z["max_val"], rtol=1e-10, atol=1e-9)
+
+
+def test_multi_epigraph_importance_weights():
+    """Config C5 shape: transship, 4 epigraphs (objective weight 0.25), scenarios drawn from
+    N(mu, (1.5 sigma)^2) with likelihood-ratio weights, a shared vertex set."""
+    from oracle import cpu
+    from sqlp_amd import twosd
+    ctx, x, V = _setup("transship", 2048)
+    sto = I.load("transship")["sto"]
+    mu = np.array([d[1] for d in sto.indep.values()])
+    sd = np.sqrt([d[2] for d in sto.indep.values()])
+    rng = np.random.default_rng(8)
+    sp = I.load("transship")["osp2"]
+    Vm = V.matrix()
+    for e in range(4):
+        epi = twosd.sdEpigraph(ctx, 0.25, 0.0)
+        vals = rng.normal(mu, 1.5 * sd, size=(600, len(mu)))
+        logw = (-0.5 * ((vals - mu) / sd) ** 2).sum(1) - (-0.5 * ((vals - mu) / (1.5 * sd)) ** 2).sum(1) + len(mu) * np.log(1.5)
+        w = np.exp(logw)
+        twosd.add_scenarios(epi, vals, w)
+        cut = twosd.build_sasa_cut(epi, x, V, tie_rel=1e-12)
+        a, b, _, _ = cpu.build_cut(sp.r, sp.T, x, Vm, ctx.rows, vals - sp.r[ctx.rows], w, tie_rel=1e-12)
+        assert cut.alpha == pytest.approx(a, rel=1e-8)
+        np.testing.assert_allclose(cut.beta, b, rtol=1e-8, atol=1e-8)
+        assert epi.total_scenario_weight == pytest.approx(w.sum(), rel=1e-14)
+
+
+def test_sharded_partials_equal_single_cut():
+    """twosd_cut_partial on two scenario shards + host sum (the all-reduce) + finalize ==
+    twosd_build_cut over all scenarios; the uint64 vertex histogram is bit-identical."""
+    import torch
+    from sqlp_amd import twosd
+    ctx, x, V = _setup("ssn", 1024)
+    vals = I.sample("ssn", 2000, seed=21)
+    w = np.random.default_rng(1).uniform(0.5, 1.5, size=2000)
+    full = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(full, vals, w)
+    ref = twosd.build_sasa_cut(full, x, V, tie_rel=1e-12)
+    halves = [twosd.sdEpigraph(ctx, 1.0, 0.0) for _ in range(2)]
+    twosd.add_scenarios(halves[0], vals[:900], w[:900])
+    twosd.add_scenarios(halves[1], vals[900:], w[900:])
+    nu, nf = ctx.cut_partial_len()
+    dev = torch.device("cuda", 0)
+    H = [torch.zeros(nu, dtype=torch.int64, device=dev) for _ in range(2)]
+    S = [torch.zeros(nf, dtype=torch.float64, device=dev) for _ in range(2)]
+    hist1 = torch.zeros(nu, dtype=torch.int64, device=dev)
+    sums1 = torch.zeros(nf, dtype=torch.float64, device=dev)
+    ctx.cut_partial(full, x, 1e-12, w.sum(), hist1.data_ptr(), sums1.data_ptr())
+    for e in range(2):
+        ctx.cut_partial(halves[e], x, 1e-12, w.sum(), H[e].data_ptr(), S[e].data_ptr())
+    torch.cuda.synchronize()
+    hist = H[0] + H[1]
+    sums = S[0] + S[1]
+    assert torch.equal(hist, hist1)
+    a, b = ctx.cut_finalize(x, hist.data_ptr(), sums.data_ptr())
+    assert a == pytest.approx(ref.alpha, rel=1e-12)
+    np.testing.assert_allclose(b, ref.beta, rtol=1e-12, atol=1e-12)
+
+
+def test_empty_vertex_set_raises():
+    from sqlp_amd import twosd
+    from sqlp_amd._lib import TwoSDError
+    inst = I.load("lands")
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(epi, I.sample("lands", 4, 1))
+    with pytest.raises(TwoSDError):            # UndefRefError in build_sasa_cut (epigraph.jl:140)
+        twosd.build_sasa_cut(epi, I.x_ev("lands"), twosd.sdDualVertexSet(ctx))
