@@ -86,6 +86,21 @@ int twosd_compute_basis(twosd_ctx *ctx, const double *x, const double *values);
 int twosd_set_basis(twosd_ctx *ctx, const int *head);
 int twosd_get_basis(twosd_ctx *ctx, int *head);
 
+/* Warm-start basis pool (no reference counterpart: the reference warm-starts each
+ * solve from the solver's previous basis, smps_routines.jl:50-62).  With only the
+ * RHS random, every optimal basis of one scenario is dual feasible for all of them;
+ * the LP kernel starts each scenario from the pool basis with the least primal
+ * infeasibility.  Results are the same optimal vertices (same tie rules) -- only
+ * the pivot count changes.  set_basis / compute_basis reset the pool to one basis.
+ *   pool_add_basis: append a (dual-feasible) basis; *added = 0 if already present.
+ *   pool_build: solve training scenarios [first, first+count) of epigraph epi at x
+ *     and add their optimal bases, most frequent first, up to max_pool bases. */
+int twosd_pool_add_basis(twosd_ctx *ctx, const int *head, int *added);
+int twosd_pool_build(twosd_ctx *ctx, int epi, const double *x, int first, int count, int max_pool,
+                     int *pool_size);
+int twosd_pool_size(twosd_ctx *ctx, int *size);
+int twosd_pool_get(twosd_ctx *ctx, int p, int *head);
+
 /* Epigraphs (sdEpigraph, epigraph.jl:17-61): per-epigraph scenario pool + weights. */
 int twosd_epigraph_create(twosd_ctx *ctx, int *epi_out);
 /* add_scenario!(epi, w, weight) batched (epigraph.jl:81-96): values[N*k] are the

@@ -34,6 +34,10 @@ SIGNATURES = [
     ("twosd_compute_basis", I, [P, P, P]),
     ("twosd_set_basis", I, [P, P]),
     ("twosd_get_basis", I, [P, P]),
+    ("twosd_pool_add_basis", I, [P, P, P]),
+    ("twosd_pool_build", I, [P, I, P, I, I, I, P]),
+    ("twosd_pool_size", I, [P, P]),
+    ("twosd_pool_get", I, [P, I, P]),
     ("twosd_epigraph_create", I, [P, P]),
     ("twosd_add_scenarios", I, [P, I, I, P, P]),
     ("twosd_epigraph_info", I, [P, I, P, P]),

@@ -13,6 +13,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <map>
 #include "twosd_internal.h"
 #include "twosd_ctx.h"
 
@@ -134,7 +135,9 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_xbase); dfree(c->d_B0K); dfree(c->d_eta); dfree(c->d_queue);
     dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_ops);
     dfree(c->d_dvtmp);
-    dfree(c->d_bcolptr); dfree(c->d_browidx); dfree(c->d_bval); dfree(c->d_kptr); dfree(c->d_kidx); dfree(c->d_kval);
+    dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ax); dfree(c->d_sel_qv); dfree(c->d_sel_aptr); dfree(c->d_sel_abt);
+    dfree(c->d_sel_qptr); dfree(c->d_sel_qe); dfree(c->d_head_out); dfree(c->d_pool_pick); c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
+    dfree(c->d_kslot); dfree(c->d_kix); dfree(c->d_kv);
     dfree(c->d_d0); dfree(c->d_eidx); dfree(c->d_evals); dfree(c->d_stamps);
     dfree(c->d_wslot); dfree(c->d_wix); dfree(c->d_wv); dfree(c->d_bslot); dfree(c->d_bix); dfree(c->d_bv);
     dfree(c->d_brptr); dfree(c->d_brcol); dfree(c->d_brval); dfree(c->d_wrow4); dfree(c->d_wval4);
@@ -319,102 +322,142 @@ static void rhs_at(const twosd_ctx *c, const double *x, const double *dv, std::v
         }
 }
 
-static int install_basis(twosd_ctx *c, const std::vector<int> &head) {
+// validate a basis head: valid distinct columns, nonsingular, dual feasible for q
+static int make_pool_basis(twosd_ctx *c, const std::vector<int> &head, PoolBasis &pb) {
     const HostLP &L = c->L;
-    const int m = L.m, n = L.n, MP = c->MP;
+    const int m = L.m, n = L.n;
     std::vector<char> seen(n + m, 0);
     for (int i = 0; i < m; ++i) {
         if (head[i] < 0 || head[i] >= n + m || seen[head[i]]) return fail(TWOSD_E_ARG, "basis head[%d] = %d invalid/duplicate", i, head[i]);
         seen[head[i]] = 1;
     }
-    std::vector<double> B, Binv;
+    std::vector<double> B;
     basis_matrix(L, head, B);
-    if (!dense_inverse(m, B, Binv)) return fail(TWOSD_E_ARG, "basis matrix is singular");
-    std::vector<double> pi0;
-    const double dinf = basis_dual_infeasibility(L, head, Binv, pi0);
+    if (!dense_inverse(m, B, pb.Binv)) return fail(TWOSD_E_ARG, "basis matrix is singular");
+    const double dinf = basis_dual_infeasibility(L, head, pb.Binv, pb.pi0);
     if (dinf > 1e-7) return fail(TWOSD_E_ARG, "basis is not dual feasible (max dual infeasibility %g)", dinf);
-    c->head0 = head;
-    c->B0inv = Binv;
-    std::vector<double> Bp((size_t)m * MP, 0.0), BTp((size_t)m * MP, 0.0), pip(MP, 0.0);
-    for (int i = 0; i < m; ++i)
-        for (int j = 0; j < m; ++j) {
-            Bp[(size_t)i * MP + j] = Binv[(size_t)i * m + j];
-            BTp[(size_t)j * MP + i] = Binv[(size_t)i * m + j];
-        }
-    for (int i = 0; i < m; ++i) pip[i] = pi0[i];
-    std::vector<int> hb(MP, -1);
-    std::vector<uint64_t> basic(64, 0);
+    pb.head = head;
+    return TWOSD_OK;
+}
+
+// Upload the hypersparse-kernel form of every pool basis, pool-strided (pool[0] first, so
+// the leading MP / 64 / 64C entries are the primary basis): hb0 (MP), basic0 (64),
+// d0 (64C), B^{-1} columns as sliced ELL (bslot absolute into the concatenated bix/bv),
+// B^{-1} rows as CSR (brptr absolute into the concatenated brcol/brval).
+static int upload_pool(twosd_ctx *c) {
+    const HostLP &L = c->L;
+    const int m = L.m, n = L.n, MP = c->MP, P = (int)c->pool.size();
     std::vector<int8_t> bt(n + m);
     HIPCHK(hipMemcpy(bt.data(), c->d_btype, n + m, hipMemcpyDeviceToHost));
-    for (int i = 0; i < m; ++i) {
-        hb[i] = head[i] * 4 + bt[head[i]];
-        basic[head[i] & 63] |= 1ull << (head[i] >> 6);
-    }
-    int rc;
-    if ((rc = dalloc(&c->d_hb0, MP)) || (rc = dalloc(&c->d_basic0, 64)) || (rc = dalloc(&c->d_B0inv, (size_t)m * MP)) ||
-        (rc = dalloc(&c->d_B0invT, (size_t)m * MP)) || (rc = dalloc(&c->d_pi0, MP)) || (rc = dalloc(&c->d_xbase, MP)))
-        return rc;
-    HIPCHK(hipMemcpy(c->d_hb0, hb.data(), sizeof(int) * MP, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->d_basic0, basic.data(), sizeof(uint64_t) * 64, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->d_B0inv, Bp.data(), sizeof(double) * m * MP, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->d_B0invT, BTp.data(), sizeof(double) * m * MP, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->d_pi0, pip.data(), sizeof(double) * MP, hipMemcpyHostToDevice));
-    // hypersparse form: B0^{-1} CSC over MP (padded) columns, reduced costs d0 in lane-slot order
-    if (c->CH > 0) {
-        double amax = 0.0;
-        for (double v : Binv) amax = std::max(amax, std::fabs(v));
-        const double drop = 1e-14 * amax;
-        std::vector<int> cp(MP + 1, 0), ri;
-        std::vector<double> vv;
-        for (int cc = 0; cc < MP; ++cc) {
-            if (cc < m)
-                for (int i = 0; i < m; ++i) {
-                    const double v = Binv[(size_t)i * m + cc];
-                    if (std::fabs(v) > drop) { ri.push_back(i); vv.push_back(v); }
-                }
-            cp[cc + 1] = (int)ri.size();
+    std::vector<int> hb((size_t)P * MP, -1), bnnz(P, 0);
+    std::vector<uint64_t> basic((size_t)P * 64, 0);
+    std::vector<int> bs_all, bi_all, rp_all, rc_all;
+    std::vector<double> bv_all, rv_all, d0_all;
+    for (int p = 0; p < P; ++p) {
+        const PoolBasis &B = c->pool[p];
+        std::vector<char> isb(n + m, 0);
+        for (int i = 0; i < m; ++i) {
+            hb[(size_t)p * MP + i] = B.head[i] * 4 + bt[B.head[i]];
+            basic[(size_t)p * 64 + (B.head[i] & 63)] |= 1ull << (B.head[i] >> 6);
+            isb[B.head[i]] = 1;
         }
+        if (c->CH <= 0) continue;
+        double amax = 0.0;
+        for (double v : B.Binv) amax = std::max(amax, std::fabs(v));
+        const double drop = 1e-14 * amax;
         std::vector<double> d0((size_t)64 * c->CH, 0.0);
         for (int j = 0; j < n + m; ++j) {
-            if (seen[j]) continue;   // basic
+            if (isb[j]) continue;
             double s = 0.0;
-            if (j >= n) s = pi0[j - n];
+            if (j >= n) s = B.pi0[j - n];
             else
-                for (int p = L.colptr[j]; p < L.colptr[j + 1]; ++p) s += pi0[L.rowidx[p]] * L.val[p];
+                for (int q = L.colptr[j]; q < L.colptr[j + 1]; ++q) s += B.pi0[L.rowidx[q]] * L.val[q];
             d0[j] = (j < n ? L.q[j] : 0.0) - s;
         }
+        d0_all.insert(d0_all.end(), d0.begin(), d0.end());
         std::vector<int> bs, bi;
         std::vector<double> bvv;
+        int nnz = 0;
         build_ell(c->R, [&](int cc, std::vector<std::pair<int, double>> &out) {
-            for (int p = cp[cc]; p < cp[cc + 1]; ++p) out.push_back({ri[p], vv[p]});
+            if (cc < m)
+                for (int i = 0; i < m; ++i) {
+                    const double v = B.Binv[(size_t)i * m + cc];
+                    if (std::fabs(v) > drop) { out.push_back({i, v}); ++nnz; }
+                }
         }, bs, bi, bvv);
-        if ((rc = upload(&c->d_bslot, bs)) || (rc = upload(&c->d_bix, bi)) || (rc = upload(&c->d_bv, bvv))) return rc;
-        // CSR of B0^{-1} over MP rows (row scatter of rho)
-        std::vector<int> rp(MP + 1, 0), rcix;
-        std::vector<double> rvv;
+        bnnz[p] = nnz;
+        const int eoff = (int)(bi_all.size() / 64);
+        for (int v : bs) bs_all.push_back(v + eoff);
+        bi_all.insert(bi_all.end(), bi.begin(), bi.end());
+        bv_all.insert(bv_all.end(), bvv.begin(), bvv.end());
+        const int roff = (int)rc_all.size();
+        rp_all.push_back(roff);
         for (int i = 0; i < MP; ++i) {
             if (i < m)
                 for (int cc = 0; cc < m; ++cc) {
-                    const double v = Binv[(size_t)i * m + cc];
-                    if (std::fabs(v) > drop) { rcix.push_back(cc); rvv.push_back(v); }
+                    const double v = B.Binv[(size_t)i * m + cc];
+                    if (std::fabs(v) > drop) { rc_all.push_back(cc); rv_all.push_back(v); }
                 }
-            rp[i + 1] = (int)rcix.size();
+            rp_all.push_back((int)rc_all.size());
         }
-        if ((rc = upload(&c->d_brptr, rp)) || (rc = upload(&c->d_brcol, rcix)) || (rc = upload(&c->d_brval, rvv))) return rc;
-        if ((rc = dalloc(&c->d_bcolptr, MP + 1)) || (rc = dalloc(&c->d_browidx, ri.size())) ||
-            (rc = dalloc(&c->d_bval, vv.size())) || (rc = dalloc(&c->d_d0, d0.size())))
-            return rc;
-        HIPCHK(hipMemcpy(c->d_bcolptr, cp.data(), sizeof(int) * (MP + 1), hipMemcpyHostToDevice));
-        if (!ri.empty()) {
-            HIPCHK(hipMemcpy(c->d_browidx, ri.data(), sizeof(int) * ri.size(), hipMemcpyHostToDevice));
-            HIPCHK(hipMemcpy(c->d_bval, vv.data(), sizeof(double) * vv.size(), hipMemcpyHostToDevice));
-        }
-        HIPCHK(hipMemcpy(c->d_d0, d0.data(), sizeof(double) * d0.size(), hipMemcpyHostToDevice));
-        c->b0_nnz = (int64_t)ri.size();
     }
-    c->has_basis = true;
+    int rc;
+    if ((rc = upload(&c->d_hb0, hb)) || (rc = upload(&c->d_basic0, basic)) || (rc = upload(&c->d_bnnz, bnnz))) return rc;
+    if (c->CH > 0) {
+        if ((rc = upload(&c->d_bslot, bs_all)) || (rc = upload(&c->d_bix, bi_all)) || (rc = upload(&c->d_bv, bv_all)) ||
+            (rc = upload(&c->d_brptr, rp_all)) || (rc = upload(&c->d_brcol, rc_all)) || (rc = upload(&c->d_brval, rv_all)) ||
+            (rc = upload(&c->d_d0, d0_all)))
+            return rc;
+        c->b0_nnz = bnnz[0];
+    }
     c->prep_valid = false;
     return TWOSD_OK;
+}
+
+static int install_basis(twosd_ctx *c, const std::vector<int> &head) {
+    const int m = c->L.m, MP = c->MP;
+    PoolBasis pb;
+    int rc = make_pool_basis(c, head, pb);
+    if (rc) return rc;
+    c->head0 = head;
+    c->B0inv = pb.Binv;
+    // dense-kernel form of the primary basis
+    std::vector<double> Bp((size_t)m * MP, 0.0), BTp((size_t)m * MP, 0.0), pip(MP, 0.0);
+    for (int i = 0; i < m; ++i)
+        for (int j = 0; j < m; ++j) {
+            Bp[(size_t)i * MP + j] = pb.Binv[(size_t)i * m + j];
+            BTp[(size_t)j * MP + i] = pb.Binv[(size_t)i * m + j];
+        }
+    for (int i = 0; i < m; ++i) pip[i] = pb.pi0[i];
+    if ((rc = dalloc(&c->d_B0inv, (size_t)m * MP)) || (rc = dalloc(&c->d_B0invT, (size_t)m * MP)) || (rc = dalloc(&c->d_pi0, MP)))
+        return rc;
+    HIPCHK(hipMemcpy(c->d_B0inv, Bp.data(), sizeof(double) * m * MP, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_B0invT, BTp.data(), sizeof(double) * m * MP, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_pi0, pip.data(), sizeof(double) * MP, hipMemcpyHostToDevice));
+    c->pool.clear();
+    c->pool.push_back(std::move(pb));
+    if ((rc = upload_pool(c))) return rc;
+    c->has_basis = true;
+    return TWOSD_OK;
+}
+
+static bool same_basis(const std::vector<int> &a, const std::vector<int> &b) {
+    std::vector<int> sa(a), sb(b);
+    std::sort(sa.begin(), sa.end());
+    std::sort(sb.begin(), sb.end());
+    return sa == sb;
+}
+
+// append a basis to the pool; returns 1 if added, 0 if already present, < 0 on error
+static int pool_add(twosd_ctx *c, const std::vector<int> &head, bool upload_now) {
+    for (const PoolBasis &B : c->pool)
+        if (same_basis(B.head, head)) return 0;
+    PoolBasis pb;
+    int rc = make_pool_basis(c, head, pb);
+    if (rc) return rc;
+    c->pool.push_back(std::move(pb));
+    if (upload_now && (rc = upload_pool(c))) return rc;
+    return 1;
 }
 
 extern "C" int twosd_compute_basis(twosd_ctx *c, const double *x, const double *values) {
@@ -443,6 +486,105 @@ extern "C" int twosd_set_basis(twosd_ctx *c, const int *head) {
 extern "C" int twosd_get_basis(twosd_ctx *c, int *head) {
     if (!c || !c->has_basis || !head) return fail(TWOSD_E_STATE, "get_basis: no basis");
     std::copy(c->head0.begin(), c->head0.end(), head);
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_pool_add_basis(twosd_ctx *c, const int *head, int *added) {
+    if (!c || !c->has_basis || !head) return fail(TWOSD_E_STATE, "pool_add_basis: no primary basis / NULL head");
+    HIPCHK(hipSetDevice(c->device));
+    const int rc = pool_add(c, std::vector<int>(head, head + c->L.m), true);
+    if (rc < 0) return rc;
+    if (added) *added = rc;
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_pool_size(twosd_ctx *c, int *size) {
+    if (!c || !size) return fail(TWOSD_E_ARG, "pool_size: NULL argument");
+    *size = (int)c->pool.size();
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_pool_get(twosd_ctx *c, int p, int *head) {
+    if (!c || !head || p < 0 || p >= (int)c->pool.size()) return fail(TWOSD_E_ARG, "pool_get: basis %d of %zu", p, c ? c->pool.size() : 0);
+    std::copy(c->pool[p].head.begin(), c->pool[p].head.end(), head);
+    return TWOSD_OK;
+}
+
+static int64_t pivots_of_last_lp(twosd_ctx *c, int N) {
+    std::vector<int> its(N);
+    if (hipMemcpy(its.data(), c->d_iters, sizeof(int) * N, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    int64_t sum = 0;
+    for (int v : its) sum += v;
+    return sum;
+}
+
+// Grow the pool from training scenarios [first, first + count) of epigraph epi at x.  The
+// first half harvests: solved from the current pool, its optimal bases are added in order
+// of decreasing frequency (ties: first occurrence) up to max_pool bases.  The second half
+// validates: the grown pool is kept only if it solves those scenarios in fewer pivots.
+extern "C" int twosd_pool_build(twosd_ctx *c, int epi, const double *x, int first, int count, int max_pool,
+                                int *pool_size) {
+    if (!c || !c->has_basis) return fail(TWOSD_E_STATE, "pool_build: no primary basis");
+    if (epi < 0 || epi >= (int)c->epis.size()) return fail(TWOSD_E_ARG, "pool_build: epigraph %d does not exist", epi);
+    const EpiDevice &E = c->epis[epi];
+    if (first < 0 || count < 0 || first + count > E.count || max_pool < 1 || (c->n1 > 0 && !x))
+        return fail(TWOSD_E_ARG, "pool_build: bad arguments");
+    if (!c->use_hyper) return fail(TWOSD_E_UNSUPPORTED, "pool_build: basis pool needs the hypersparse LP kernel");
+    if (pool_select_lds_bytes(c->k) > 160 * 1024) return fail(TWOSD_E_UNSUPPORTED, "pool_build: k = %d random elements too many for pool selection", c->k);
+    HIPCHK(hipSetDevice(c->device));
+    const int m = c->L.m;
+    const int nh = count / 2, nv = count - nh;
+    if (nh > 0 && (int)c->pool.size() < max_pool) {
+        const double *dh = E.d_dv + (size_t)first * c->k, *dval = dh + (size_t)nh * c->k;
+        int rc;
+        if ((rc = run_lp(c, x, dval, nv, false, false))) return rc;
+        const int64_t piv0 = pivots_of_last_lp(c, nv);
+        c->want_head = true;
+        rc = run_lp(c, x, dh, nh, false, false);
+        c->want_head = false;
+        if (rc) return rc;
+        std::vector<int> heads((size_t)nh * m), st(nh);
+        HIPCHK(hipMemcpy(heads.data(), c->d_head_out, sizeof(int) * heads.size(), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(st.data(), c->d_status, sizeof(int) * nh, hipMemcpyDeviceToHost));
+        std::map<std::vector<int>, std::pair<int, int>> freq;   // sorted head -> (count, first scenario)
+        for (const PoolBasis &B : c->pool) {
+            std::vector<int> key(B.head);
+            std::sort(key.begin(), key.end());
+            freq[key] = {0, -1};                                 // already in the pool
+        }
+        for (int s = 0; s < nh; ++s) {
+            if (st[s] != TWOSD_LP_OPTIMAL) continue;
+            std::vector<int> key(heads.begin() + (size_t)s * m, heads.begin() + (size_t)(s + 1) * m);
+            std::sort(key.begin(), key.end());
+            auto it = freq.find(key);
+            if (it == freq.end()) freq.emplace(std::move(key), std::make_pair(1, s));
+            else if (it->second.second >= 0) ++it->second.first;
+        }
+        std::vector<std::pair<int, int>> order;   // (-count, first scenario)
+        for (auto &kv : freq)
+            if (kv.second.second >= 0) order.push_back({-kv.second.first, kv.second.second});
+        std::sort(order.begin(), order.end());
+        const size_t old_size = c->pool.size();
+        for (auto &o : order) {
+            if ((int)c->pool.size() >= max_pool) break;
+            const int s = o.second;
+            const int r = pool_add(c, std::vector<int>(heads.begin() + (size_t)s * m, heads.begin() + (size_t)(s + 1) * m), false);
+            if (r < 0) return r;
+        }
+        if (c->pool.size() > old_size) {
+            if ((rc = upload_pool(c))) return rc;
+            if ((rc = run_lp(c, x, dval, nv, false, false))) return rc;
+            const int64_t piv1 = pivots_of_last_lp(c, nv);
+            std::vector<int> st2(nv);
+            HIPCHK(hipMemcpy(st2.data(), c->d_status, sizeof(int) * nv, hipMemcpyDeviceToHost));
+            const bool all_ok = std::all_of(st2.begin(), st2.end(), [](int v) { return v == TWOSD_LP_OPTIMAL; });
+            if (piv1 < 0 || piv0 < 0 || piv1 >= piv0 || !all_ok) {   // no gain: back to the old pool
+                c->pool.resize(old_size);
+                if ((rc = upload_pool(c))) return rc;
+            }
+        }
+    }
+    if (pool_size) *pool_size = (int)c->pool.size();
     return TWOSD_OK;
 }
 
@@ -487,51 +629,97 @@ extern "C" int twosd_epigraph_info(twosd_ctx *c, int epi, int *ns, double *tw) {
     return TWOSD_OK;
 }
 
-// per-x shared data: xbase = B0^{-1}(r - T x), B0K[e] = coef_e * B0^{-1}[:, row_e]
+// primal infeasibility of a basic variable at value x (h_infeas of lp_hyper.hip, tolerance 1e-9)
+static double host_infeas(double x, int bt) {
+    const double tol = 1e-9;
+    if (bt == BT_Y || bt == BT_L) return x < -tol ? x : 0.0;
+    if (bt == BT_G) return x > tol ? x : 0.0;
+    return std::fabs(x) > tol ? x : 0.0;
+}
+
+// per-x shared data: xbase = B0^{-1}(r - T x), B0K[e] = coef_e * B0^{-1}[:, row_e] (dense, primary
+// basis); for the hypersparse kernel, per pool basis p: xbase_p (MP) and the CSR by row of
+// coef_e * B_p^{-1}[i][row_e] as sliced ELL (kslot pool-strided, absolute into kix/kv)
 int twosd::prepare_x(twosd_ctx *c, const double *x) {
     const int m = c->L.m, MP = c->MP, k = c->k, n1 = c->n1;
     if (c->prep_valid && c->prep_x.size() == (size_t)n1 && (n1 == 0 || std::equal(c->prep_x.begin(), c->prep_x.end(), x)))
         return TWOSD_OK;
     std::vector<double> b;
     rhs_at(c, x, nullptr, b);
-    std::vector<double> xb(MP, 0.0), bk((size_t)std::max(k, 1) * MP, 0.0);
-    for (int i = 0; i < m; ++i) {
-        const double *row = &c->B0inv[(size_t)i * m];
-        double s = 0.0;
-        for (int j = 0; j < m; ++j) s += row[j] * b[j];
-        xb[i] = s;
+    const int P = (int)c->pool.size();
+    std::vector<double> xb((size_t)P * MP, 0.0), bk((size_t)std::max(k, 1) * MP, 0.0);
+    std::vector<int> ks, ki;
+    std::vector<double> kv;
+    // pool selection (P > 1): per basis the rows whose x_B does not depend on the scenario
+    // fold into cinf, the others are listed with their entries
+    std::vector<int8_t> bt(c->L.n + m);
+    if (P > 1) HIPCHK(hipMemcpy(bt.data(), c->d_btype, bt.size(), hipMemcpyDeviceToHost));
+    std::vector<double> cinf(P, 0.0), ax, qv;
+    std::vector<int> aptr(1, 0), abt, qptr(1, 0), qe;
+    for (int p = 0; p < P; ++p) {
+        const std::vector<double> &Bi = c->pool[p].Binv;
+        for (int i = 0; i < m; ++i) {
+            const double *row = &Bi[(size_t)i * m];
+            double s = 0.0;
+            for (int j = 0; j < m; ++j) s += row[j] * b[j];
+            xb[(size_t)p * MP + i] = s;
+        }
+        if (p == 0)
+            for (int e = 0; e < k; ++e) {
+                const int rr = c->pos_row[e], cc = c->pos_col[e];
+                const double coef = cc < 0 ? 1.0 : -x[cc];
+                for (int i = 0; i < m; ++i) bk[(size_t)e * MP + i] = coef * Bi[(size_t)i * m + rr];
+            }
+        if (c->CH > 0) {
+            double amax = 0.0;
+            for (double v : Bi) amax = std::max(amax, std::fabs(v));
+            const double drop = 1e-14 * amax;
+            std::vector<std::vector<std::pair<int, double>>> rows(m);
+            for (int i = 0; i < m; ++i)
+                for (int e = 0; e < k; ++e) {
+                    const double bv = Bi[(size_t)i * m + c->pos_row[e]];
+                    const double v = (c->pos_col[e] < 0 ? 1.0 : -x[c->pos_col[e]]) * bv;
+                    if (std::fabs(bv) > drop && v != 0.0) rows[i].push_back({e, v});
+                }
+            std::vector<int> sl, ix;
+            std::vector<double> vv;
+            build_ell(c->R, [&](int i, std::vector<std::pair<int, double>> &out) {
+                if (i < m) out = rows[i];
+            }, sl, ix, vv);
+            const int eoff = (int)(ki.size() / 64);
+            for (int v : sl) ks.push_back(v + eoff);
+            ki.insert(ki.end(), ix.begin(), ix.end());
+            kv.insert(kv.end(), vv.begin(), vv.end());
+            if (P > 1) {
+                for (int i = 0; i < m; ++i) {
+                    const int h = c->pool[p].head[i], t = bt[h];
+                    const double xv = xb[(size_t)p * MP + i];
+                    if (rows[i].empty()) { cinf[p] += std::fabs(host_infeas(xv, t)); continue; }
+                    ax.push_back(xv);
+                    abt.push_back(t);
+                    for (auto &ev : rows[i]) { qe.push_back(ev.first); qv.push_back(ev.second); }
+                    qptr.push_back((int)qe.size());
+                }
+                aptr.push_back((int)ax.size());
+            }
+        }
     }
-    for (int e = 0; e < k; ++e) {
-        const int rr = c->pos_row[e], cc = c->pos_col[e];
-        const double coef = cc < 0 ? 1.0 : -x[cc];
-        for (int i = 0; i < m; ++i) bk[(size_t)e * MP + i] = coef * c->B0inv[(size_t)i * m + rr];
+    if (P > 1 && c->CH > 0) {
+        int rc;
+        if ((rc = upload(&c->d_sel_cinf, cinf)) || (rc = upload(&c->d_sel_aptr, aptr)) || (rc = upload(&c->d_sel_ax, ax)) ||
+            (rc = upload(&c->d_sel_abt, abt)) || (rc = upload(&c->d_sel_qptr, qptr)) || (rc = upload(&c->d_sel_qe, qe)) ||
+            (rc = upload(&c->d_sel_qv, qv)))
+            return rc;
+        c->sel_rows = (int64_t)ax.size();
+        c->sel_nnz = (int64_t)qe.size();
     }
     int rc;
-    if ((rc = dalloc(&c->d_B0K, (size_t)std::max(k, 1) * MP))) return rc;
-    HIPCHK(hipMemcpyAsync(c->d_xbase, xb.data(), sizeof(double) * MP, hipMemcpyHostToDevice, c->stream));
+    if ((rc = dalloc(&c->d_B0K, (size_t)std::max(k, 1) * MP)) || (rc = dalloc(&c->d_xbase, (size_t)P * MP))) return rc;
+    HIPCHK(hipMemcpyAsync(c->d_xbase, xb.data(), sizeof(double) * xb.size(), hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->d_B0K, bk.data(), sizeof(double) * std::max(k, 1) * MP, hipMemcpyHostToDevice, c->stream));
-    // hypersparse kernel: the same B0K as CSR by row (row i: (e, coef_e B0^{-1}[i][row_e]))
-    std::vector<int> kp(MP + 1, 0), ki;
-    std::vector<double> kv;
     if (c->CH > 0) {
-        double amax = 0.0;
-        for (double v : c->B0inv) amax = std::max(amax, std::fabs(v));
-        const double drop = 1e-14 * amax;
-        for (int i = 0; i < MP; ++i) {
-            if (i < m)
-                for (int e = 0; e < k; ++e) {
-                    const double v = bk[(size_t)e * MP + i];
-                    if (std::fabs(c->B0inv[(size_t)i * m + c->pos_row[e]]) > drop && v != 0.0) { ki.push_back(e); kv.push_back(v); }
-                }
-            kp[i + 1] = (int)ki.size();
-        }
-        if ((rc = dalloc(&c->d_kptr, MP + 1)) || (rc = dalloc(&c->d_kidx, ki.size())) || (rc = dalloc(&c->d_kval, kv.size())))
-            return rc;
-        HIPCHK(hipMemcpyAsync(c->d_kptr, kp.data(), sizeof(int) * (MP + 1), hipMemcpyHostToDevice, c->stream));
-        if (!ki.empty()) {
-            HIPCHK(hipMemcpyAsync(c->d_kidx, ki.data(), sizeof(int) * ki.size(), hipMemcpyHostToDevice, c->stream));
-            HIPCHK(hipMemcpyAsync(c->d_kval, kv.data(), sizeof(double) * kv.size(), hipMemcpyHostToDevice, c->stream));
-        }
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if ((rc = upload(&c->d_kslot, ks)) || (rc = upload(&c->d_kix, ki)) || (rc = upload(&c->d_kv, kv))) return rc;
     }
     HIPCHK(hipStreamSynchronize(c->stream));
     c->prep_x.assign(x, x + n1);
@@ -567,7 +755,7 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
         const int kmax = c->kmax_override > 0 ? c->kmax_override : std::min(512, std::max(64, 2 * m + 32));
         const int ecap = std::max(4096, 32 * MP);
         const int CH = c->CH;
-        const int bpc = hyper_max_blocks_per_cu(R, CH, kmax);
+        const int bpc = hyper_max_blocks_per_cu(R, CH, kmax, c->k);
         const int nblocks = std::max(1, std::min((N + kWavesPerBlock - 1) / kWavesPerBlock, bpc * c->num_cus));
         const size_t slots = (size_t)nblocks * kWavesPerBlock;
         if (slots > c->earena_slots || ecap != c->earena_cap) {
@@ -579,13 +767,12 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
         HyperParams H{};
         H.m = m; H.n = n; H.k = c->k; H.N = N; H.kmax = kmax; H.ecap = ecap;
         H.colptr = c->d_colptr; H.rowidx = c->d_rowidx; H.val = c->d_val; H.q = c->d_q; H.btype = c->d_btype;
-        H.bcolptr = c->d_bcolptr; H.browidx = c->d_browidx; H.bval = c->d_bval;
         H.wslot = c->d_wslot; H.wix = c->d_wix; H.wv = c->d_wv;
         H.bslot = c->d_bslot; H.bix = c->d_bix; H.bv = c->d_bv;
         H.brptr = c->d_brptr; H.brcol = c->d_brcol; H.brval = c->d_brval;
         H.wrow4 = c->has_pack4 ? c->d_wrow4 : nullptr;
         H.wval4 = c->has_pack4 ? c->d_wval4 : nullptr;
-        H.kptr = c->d_kptr; H.kidx = c->d_kidx; H.kval = c->d_kval;
+        H.kslot = c->d_kslot; H.kix = c->d_kix; H.kv = c->d_kv;
         H.xbase = c->d_xbase; H.d0 = c->d_d0; H.hb0 = c->d_hb0;
         H.basic0 = c->d_basic0; H.fixedmask = c->d_fixedmask; H.ubmask = c->d_ubmask;
         H.dv = d_dv; H.eidx = c->d_eidx; H.evals = c->d_evals; H.queue = c->d_queue;
@@ -596,8 +783,31 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
             HIPCHK(hipMemset(c->d_stamps, 0, sizeof(unsigned long long) * 16));
         }
         H.stamps = c->d_stamps;
+        H.npool = (int)c->pool.size();
+        H.bnnz = c->d_bnnz;
+        if (c->want_head) {
+            if ((size_t)N > c->head_cap) {
+                if ((rc = dalloc(&c->d_head_out, (size_t)N * m))) return rc;
+                c->head_cap = N;
+            }
+            H.head_out = c->d_head_out;
+        }
+        if (H.npool > 1) {
+            if ((size_t)N > c->pick_cap) {
+                if ((rc = dalloc(&c->d_pool_pick, (size_t)N))) return rc;
+                c->pick_cap = N;
+            }
+            H.pool_pick = c->d_pool_pick;
+        }
         HIPCHK(hipEventRecord(c->ev[0], c->stream));
-        HIPCHK(launch_hyper(R, CH, H, nblocks, hyper_lds_bytes(R, kmax), c->stream));
+        if (H.npool > 1) {
+            PoolSelParams S{};
+            S.N = N; S.k = c->k; S.npool = H.npool; S.dv = d_dv;
+            S.cinf = c->d_sel_cinf; S.aptr = c->d_sel_aptr; S.ax = c->d_sel_ax; S.abt = c->d_sel_abt;
+            S.qptr = c->d_sel_qptr; S.qe = c->d_sel_qe; S.qv = c->d_sel_qv; S.pick = c->d_pool_pick;
+            HIPCHK(launch_pool_select(S, c->stream));
+        }
+        HIPCHK(launch_hyper(R, CH, H, nblocks, hyper_lds_bytes(R, kmax, c->k), c->stream));
         HIPCHK(hipEventRecord(c->ev[1], c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         float ms = 0;

@@ -79,10 +79,12 @@ __device__ __forceinline__ int h_get_row_i(const int (&a)[R], int p) {
     return __builtin_amdgcn_readlane(v, p & 63);
 }
 
-size_t hyper_lds_bytes(int R, int kmax) {
+// per-wave LDS slice: ut, rho (MP doubles each), etap (u16), etaoff (int), scenario deltas (k doubles)
+static __host__ __device__ inline size_t hyper_slice_bytes(int R, int kmax, int k) {
     const int kmaxp = (kmax + 3) & ~3;
-    return (size_t)kWavesPerBlock * (16 * 64 * R + 2 * kmaxp + 4 * (kmaxp + 4));
+    return (size_t)(16 * 64 * R + 2 * kmaxp + 4 * (kmaxp + 4)) + 8 * (size_t)((k + 1) & ~1);
 }
+size_t hyper_lds_bytes(int R, int kmax, int k) { return (size_t)kWavesPerBlock * hyper_slice_bytes(R, kmax, k); }
 
 // min waves per SIMD (VGPR budget 256 / 168): measured on MI355X, storm (R=9) is fastest
 // at 2 waves/SIMD, ssn (R=4) at 3 (tools/lp_speed.py)
@@ -96,11 +98,12 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
     const int wid = threadIdx.x >> 6;
     constexpr int MP = 64 * R;
     const int kmaxp = (P.kmax + 3) & ~3;
-    char *slice = reinterpret_cast<char *>(lds_raw) + (size_t)wid * (16 * MP + 2 * kmaxp + 4 * (kmaxp + 4));
+    char *slice = reinterpret_cast<char *>(lds_raw) + (size_t)wid * hyper_slice_bytes(R, P.kmax, P.k);
     double *ut = reinterpret_cast<double *>(slice);        // dense scratch vector (u, then alpha_q)
     double *rho = ut + MP;                                  // pivot row of B^{-1}
     unsigned short *etap = reinterpret_cast<unsigned short *>(rho + MP);
     int *etaoff = reinterpret_cast<int *>(etap + kmaxp);
+    double *dvl = reinterpret_cast<double *>(etaoff + kmaxp + 4);   // this scenario's deltas
 
     const int m = P.m, n = P.n;
     const int slot_id = blockIdx.x * kWavesPerBlock + wid;
@@ -121,26 +124,45 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         if (s >= P.N) break;
 
         const double *dvs = P.dv + (size_t)s * P.k;
+        for (int e = lane; e < P.k; e += 64) dvl[e] = dvs[e];
+        h_wave_sync();
+        // x_B of pool basis p at this scenario: xbase_p + sum_e coef_e B_p^{-1}[i][row_e] dv_e
+        // (sliced ELL by row: independent coalesced loads, deltas gathered from LDS)
+        auto xb_row = [&](int p, int t) -> double {
+            const int i = 64 * t + lane;
+            double x = P.xbase[(size_t)p * MP + i];
+            const int e0 = P.kslot[p * (R + 1) + t], e1 = P.kslot[p * (R + 1) + t + 1];
+#pragma unroll 2
+            for (int e = e0; e < e1; ++e) x = fma(P.kv[(size_t)e * 64 + lane], dvl[P.kix[(size_t)e * 64 + lane]], x);
+            return x;
+        };
+        // warm-start basis: chosen per scenario by pool_select_kernel (0 without a pool)
+        int pb = P.npool > 1 ? __builtin_amdgcn_readfirstlane(P.pool_pick[s]) : 0;
         double xB[R];
         float w[R];
         int hb[R];
-#pragma unroll
-        for (int t = 0; t < R; ++t) {
-            const int i = 64 * t + lane;
-            double x = P.xbase[i];
-            const int p0 = P.kptr[i], p1 = P.kptr[i + 1];
-            for (int p = p0; p < p1; ++p) x = fma(P.kval[p], dvs[P.kidx[p]], x);
-            xB[t] = x;
-            hb[t] = P.hb0[i];
-            w[t] = 1.0f;
-        }
         double d[C];
-#pragma unroll
-        for (int c = 0; c < C; ++c) d[c] = P.d0[64 * c + lane];
-        uint64_t bmask = P.basic0[lane];
+        uint64_t bmask;
+        const int *brptr, *bslot;
         int K = 0, it = 0, status = TWOSD_LP_OPTIMAL;
         int eoff = 0;
-        long long nops = P.kptr[MP];
+        long long nops = 0;
+        // a pool start that ends non-optimal (numerics, iteration cap) is retried from the
+        // primary basis, so the pool never changes which scenarios solve
+        for (int attempt = 0; attempt < 2; ++attempt) {
+        brptr = P.brptr + (size_t)pb * (MP + 1);
+        bslot = P.bslot + (size_t)pb * (R + 1);
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+            xB[t] = xb_row(pb, t);
+            hb[t] = P.hb0[(size_t)pb * MP + 64 * t + lane];
+            w[t] = 1.0f;
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) d[c] = P.d0[(size_t)pb * 64 * C + 64 * c + lane];
+        bmask = P.basic0[pb * 64 + lane];
+        K = 0; status = TWOSD_LP_OPTIMAL; eoff = 0;
+        nops += (long long)(P.kslot[pb * (R + 1) + R] - P.kslot[pb * (R + 1)]) * 64;
         if (lane == 0) etaoff[0] = 0;
         h_wave_sync();
         STAMP(0)
@@ -208,8 +230,8 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                     gi[g] = 0; gv[g] = 0.0; gn[g] = 0; go[g] = 0; gp[g] = 0;
                     if (tt >= 0) {
                         gp[g] = (tt == K) ? r : (int)etap[tt];
-                        go[g] = P.brptr[gp[g]];
-                        gn[g] = P.brptr[gp[g] + 1] - go[g];
+                        go[g] = brptr[gp[g]];
+                        gn[g] = brptr[gp[g] + 1] - go[g];
                         if (lane < gn[g]) { gi[g] = P.brcol[go[g] + lane]; gv[g] = P.brval[go[g] + lane]; }
                     }
                 }
@@ -335,7 +357,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                     const int cc = q >= n ? q - n : P.rowidx[pw];
                     const double aw = q >= n ? 1.0 : P.val[pw];
                     const int ts = cc >> 6, cl = cc & 63;
-                    const int e0 = P.bslot[ts], e1 = P.bslot[ts + 1];
+                    const int e0 = bslot[ts], e1 = bslot[ts + 1];
                     for (int e = e0 + lane; e < e1; e += 64) {
                         const double v = P.bv[e * 64 + cl];
                         if (v != 0.0) {
@@ -459,6 +481,9 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             h_wave_sync();
             STAMP(8)
         }
+        if (status == TWOSD_LP_OPTIMAL || pb == 0) break;
+        pb = 0;
+        }   // attempt
 
         // ---- vertex recovery: pi = c_B' B^{-1}
         double objv = NAN;
@@ -482,7 +507,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             double pmax = 0.0;
 #pragma unroll
             for (int t = 0; t < R; ++t) {
-                const int e0 = P.bslot[t], e1 = P.bslot[t + 1];
+                const int e0 = bslot[t], e1 = bslot[t + 1];
                 double a = 0.0;
 #pragma unroll 1
                 for (int e = e0; e < e1; ++e) {
@@ -492,7 +517,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 pv[t] = a;
                 pmax = fmax(pmax, fabs(a));
             }
-            nops += P.bcolptr[MP];
+            nops += P.bnnz[pb];
             pmax = wmax(pmax);
             const double zt = HPI_ZERO * (1.0 + pmax);
             double ob = 0.0;
@@ -529,16 +554,76 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             for (int t = 0; t < R; ++t)
                 if (64 * t + lane < m) po[64 * t + lane] = NAN;
         }
+        if (P.head_out) {
+#pragma unroll
+            for (int t = 0; t < R; ++t)
+                if (64 * t + lane < m) P.head_out[(size_t)s * m + 64 * t + lane] = hb[t] >> 2;
+        }
         if (lane == 0) {
             P.obj[s] = objv;
             P.status[s] = status;
             P.iters[s] = it;
             if (P.ops) P.ops[s] = nops;
+            if (P.npool > 1) P.pool_pick[s] = pb;   // 0 if the pool start was retried
         }
         h_wave_sync();
         STAMP(9)
     }
     STAMP_FLUSH
+}
+
+// ---- warm-start selection over the basis pool.  Lane = scenario (64 per block, deltas
+// staged transposed in LDS), the pool bases split over the block's 4 waves; the sparse
+// structure (active rows of every pool basis, their coef_e B_p^{-1}[i][row_e] entries) is
+// wave-uniform, so it streams through scalar loads and the per-lane work is LDS reads +
+// FMAs.  Key: total primal infeasibility sum_i |infeas(x_B,i)| at b_w (constant rows
+// precomputed in cinf); ties: lowest p.
+__global__ void __launch_bounds__(256) pool_select_kernel(PoolSelParams S) {
+    extern __shared__ double dvt[];   // k x 65 (padded)
+    __shared__ double bsum[kWavesPerBlock][64];
+    __shared__ int bidx[kWavesPerBlock][64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int s0 = blockIdx.x * 64;
+    const int k = S.k;
+    const int ns = min(64, S.N - s0);
+    for (int idx = threadIdx.x; idx < 64 * k; idx += 256) {
+        const int sl = idx / k, e = idx - sl * k;
+        dvt[e * 65 + sl] = sl < ns ? S.dv[(size_t)s0 * k + idx] : 0.0;
+    }
+    __syncthreads();
+    double best = INFINITY;
+    int bp = 0;
+    for (int p = wid; p < S.npool; p += kWavesPerBlock) {
+        double inf = S.cinf[p];
+        const int a0 = S.aptr[p], a1 = S.aptr[p + 1];
+        for (int a = a0; a < a1; ++a) {
+            double x = S.ax[a];
+            const int q0 = S.qptr[a], q1 = S.qptr[a + 1];
+            for (int q = q0; q < q1; ++q) x = fma(S.qv[q], dvt[S.qe[q] * 65 + lane], x);
+            inf += fabs(h_infeas(x, S.abt[a]));
+        }
+        if (inf < best) { best = inf; bp = p; }
+    }
+    bsum[wid][lane] = best;
+    bidx[wid][lane] = bp;
+    __syncthreads();
+    if (wid == 0 && lane < ns) {
+        for (int w = 1; w < kWavesPerBlock; ++w) {
+            const double v = bsum[w][lane];
+            const int pw = bidx[w][lane];
+            if (v < best || (v == best && pw < bp)) { best = v; bp = pw; }
+        }
+        S.pick[s0 + lane] = bp;
+    }
+}
+
+size_t pool_select_lds_bytes(int k) { return (size_t)8 * 65 * (size_t)std::max(k, 1); }
+
+hipError_t launch_pool_select(const PoolSelParams &p, hipStream_t s) {
+    if (p.N <= 0) return hipSuccess;
+    const int nb = (p.N + 63) / 64;
+    hipLaunchKernelGGL(pool_select_kernel, dim3(nb), dim3(256), pool_select_lds_bytes(p.k), s, p);
+    return hipGetLastError();
 }
 
 // ---- dispatch: R in {1,2,4,9,16}, C in {2,4,8,16,32,64}
@@ -589,8 +674,8 @@ hipError_t launch_hyper(int R, int C, const HyperParams &p, int nblocks, size_t 
     return hipErrorInvalidValue;
 }
 
-int hyper_max_blocks_per_cu(int R, int C, int kmax) {
-    const size_t lds = hyper_lds_bytes(R, kmax);
+int hyper_max_blocks_per_cu(int R, int C, int kmax, int k) {
+    const size_t lds = hyper_lds_bytes(R, kmax, k);
     switch (R) {
         case 1: HYPER_C_SWITCH(1, ho, lds); break;
         case 2: HYPER_C_SWITCH(2, ho, lds); break;

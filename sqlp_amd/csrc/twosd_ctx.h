@@ -16,6 +16,13 @@ struct EpiDevice {
     std::vector<double> w_host;
 };
 
+// one warm-start basis of the pool (pool[0] is the primary basis head0 / B0inv)
+struct PoolBasis {
+    std::vector<int> head;        // m basic columns (0-based over [y; slacks])
+    std::vector<double> Binv;     // m x m row-major
+    std::vector<double> pi0;      // c_B' B^{-1}
+};
+
 }  // namespace twosd
 
 struct twosd_ctx {
@@ -41,13 +48,22 @@ struct twosd_ctx {
     int *d_hb0 = nullptr;
     uint64_t *d_basic0 = nullptr;
     double *d_B0inv = nullptr, *d_B0invT = nullptr, *d_pi0 = nullptr, *d_xbase = nullptr, *d_B0K = nullptr;
+    std::vector<twosd::PoolBasis> pool;   // warm-start basis pool, pool[0] = head0
+    // pool selection data (per x, prepare_x): constant-row infeasibility, active rows, entries
+    double *d_sel_cinf = nullptr, *d_sel_ax = nullptr, *d_sel_qv = nullptr;
+    int *d_sel_aptr = nullptr, *d_sel_abt = nullptr, *d_sel_qptr = nullptr, *d_sel_qe = nullptr;
+    int64_t sel_nnz = 0, sel_rows = 0;
+    int *d_bnnz = nullptr;        // npool: nnz of each pool B^{-1} (FMA accounting)
+    int *d_head_out = nullptr, *d_pool_pick = nullptr;   // optional LP outputs (pool building)
+    size_t head_cap = 0, pick_cap = 0;
+    bool want_head = false;
     bool prep_valid = false;
     std::vector<double> prep_x;
     // hypersparse kernel data
     int CH = 0;                   // column slots per lane of the hypersparse kernel
     bool use_hyper = true;
-    int *d_bcolptr = nullptr, *d_browidx = nullptr, *d_kptr = nullptr, *d_kidx = nullptr;
-    double *d_bval = nullptr, *d_kval = nullptr, *d_d0 = nullptr;
+    int *d_kslot = nullptr, *d_kix = nullptr;
+    double *d_kv = nullptr, *d_d0 = nullptr;
     int *d_wslot = nullptr, *d_wix = nullptr, *d_bslot = nullptr, *d_bix = nullptr;
     double *d_wv = nullptr, *d_bv = nullptr;
     int *d_brptr = nullptr, *d_brcol = nullptr;

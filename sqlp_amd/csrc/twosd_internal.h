@@ -55,7 +55,6 @@ struct HyperParams {
     int m, n, k, N, kmax, ecap;
     const int *colptr, *rowidx; const double *val;      // W CSC
     const double *q; const int8_t *btype;
-    const int *bcolptr, *browidx; const double *bval;   // B0^{-1} CSC, MP columns (padded empty)
     // sliced-ELL copies (entry e of slot s for lane l at [(slot_off[s] + e) * 64 + l]; padding: idx 0, val 0):
     const int *wslot, *wix; const double *wv;           // columns of [W I], C slots (j = 64c + lane)
     const int *bslot, *bix; const double *bv;           // columns of B0^{-1}, R slots (c = 64t + lane)
@@ -63,7 +62,9 @@ struct HyperParams {
     // packed pricing (all columns of [W I] with <= 4 entries): rows of column 64c+l as four
     // 16-bit fields of wrow4[c*64+l] (0xFFFF = none), values at wval4[(c*4+e)*64+l]; null if unused
     const unsigned long long *wrow4; const double *wval4;
-    const int *kptr, *kidx; const double *kval;         // B0K CSR by row (MP rows): (e, coef_e B0^{-1}[i][row_e])
+    // per pool basis p, rows i = 64t + lane of coef_e B_p^{-1}[i][row_e] as sliced ELL (R slots,
+    // kslot pool-strided npool x (R+1), absolute into the concatenated kix (= e) / kv)
+    const int *kslot, *kix; const double *kv;
     const double *xbase;                                // MP
     const double *d0;                                   // 64*C reduced costs at B0 (lane-slot order j = 64c+lane)
     const int *hb0;                                     // MP
@@ -75,12 +76,31 @@ struct HyperParams {
     int *status, *iters;
     long long *ops;                                     // executed FMAs
     unsigned long long *stamps;                         // [10] phase cycles (TWOSD_STAMPS builds only)
+    // basis pool: xbase, hb0 (npool x MP), brptr (npool x (MP+1), absolute offsets),
+    // bslot (npool x (R+1), absolute), basic0 (npool x 64), d0 (npool x 64C) are pool-strided
+    int npool;
+    const int *bnnz;                                    // npool: nnz of B^{-1} (ops accounting)
+    int *head_out;                                      // N x m final basis (nullable)
+    int *pool_pick;                                     // N pool basis per scenario (in; npool > 1)
 };
-size_t hyper_lds_bytes(int R, int kmax);
+
+// warm-start selection over the basis pool (pool_select_kernel in lp_hyper.hip)
+struct PoolSelParams {
+    int N, k, npool;
+    const double *dv;                                   // N x k
+    const double *cinf;                                 // npool: infeasibility of the constant rows
+    const int *aptr;                                    // npool + 1 -> active rows (K row non-empty)
+    const double *ax; const int *abt;                   // active row: xbase, bound type
+    const int *qptr; const int *qe; const double *qv;   // active row entries (e, coef_e B^{-1}[i][row_e])
+    int *pick;                                          // N out
+};
+size_t pool_select_lds_bytes(int k);
+hipError_t launch_pool_select(const PoolSelParams &p, hipStream_t s);
+size_t hyper_lds_bytes(int R, int kmax, int k);
 int hyper_rows_per_lane(int m);
 int hyper_cols_per_lane(int ncols);
 hipError_t launch_hyper(int R, int C, const HyperParams &p, int nblocks, size_t lds, hipStream_t s);
-int hyper_max_blocks_per_cu(int R, int C, int kmax);
+int hyper_max_blocks_per_cu(int R, int C, int kmax, int k);
 
 int lp_rows_per_lane(int m);   // supported R for m, or -1
 hipError_t launch_lp(int R, const LpParams &p, int nblocks, size_t lds_bytes, hipStream_t s);

@@ -113,6 +113,32 @@ class SDContext:
         check(self.lib.twosd_get_basis(self.h, ptr(head)))
         return head
 
+    # -- warm-start basis pool (twosd_pool_*: fewer pivots, identical vertices) ---
+    def pool_add_basis(self, head) -> bool:
+        head = np.ascontiguousarray(head, dtype=np.int32)
+        added = C.c_int(0)
+        check(self.lib.twosd_pool_add_basis(self.h, ptr(head), C.byref(added)))
+        return bool(added.value)
+
+    def pool_build(self, epi, x, first, count, max_pool) -> int:
+        """Add the most frequent optimal bases of scenarios [first, first+count) of `epi`
+        at x to the pool (up to max_pool bases); returns the pool size."""
+        x = _f64(x)
+        n = C.c_int(0)
+        check(self.lib.twosd_pool_build(self.h, epi.index, ptr(x), int(first), int(count), int(max_pool),
+                                        C.byref(n)))
+        return n.value
+
+    def pool_size(self) -> int:
+        n = C.c_int(0)
+        check(self.lib.twosd_pool_size(self.h, C.byref(n)))
+        return n.value
+
+    def pool_get(self, p):
+        head = np.zeros(self.m, dtype=np.int32)
+        check(self.lib.twosd_pool_get(self.h, int(p), ptr(head)))
+        return head
+
     def scenario_values(self, scenario) -> np.ndarray:
         """spSmpsScenario (list of position => value) -> value vector in layout order.
         Elements a scenario omits keep their template value (delta 0)."""

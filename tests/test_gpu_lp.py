@@ -74,3 +74,49 @@ def test_lp_batch_matches_oracle(name, N):
     # same pivot rules -> same vertex as the oracle on (almost) every scenario
     same = np.mean([np.allclose(pi[s], o_pi[s], rtol=1e-9, atol=1e-9) for s in range(N)])
     assert same >= 0.95, same
+
+
+@pytest.mark.parametrize("name", ["storm", "ssn"])
+def test_lp_basis_pool(name):
+    """Warm-start basis pool: same optimal objectives as the oracle, valid duals; the pool
+    holds distinct dual-feasible bases, primary basis first.  pool_build keeps a grown pool
+    only when it saves pivots on its validation half: storm does (fewer pivots here too),
+    for ssn the pool may stay at the primary basis."""
+    from oracle import cpu
+    from sqlp_amd import smps, twosd
+    ctx, x = _ctx(name)
+    inst = I.load(name)
+    sp = inst["osp2"]
+    head0 = ctx.get_basis()
+    tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(tr, I.sample(name, 2048, seed=11))
+    N = 512
+    vals = I.sample(name, N, seed=7)
+    obj1, _, _, st1 = ctx.solve_values(x, vals)
+    piv1 = ctx.lp_stats()[0]
+    size = ctx.pool_build(tr, x, 0, 2048, 16)
+    assert 1 <= size <= 16 and ctx.pool_size() == size
+    if name == "storm":
+        assert size > 1
+    assert (ctx.pool_get(0) == head0).all()
+    heads = [frozenset(ctx.pool_get(p).tolist()) for p in range(size)]
+    assert len(set(heads)) == size
+    assert not ctx.pool_add_basis(ctx.pool_get(size - 1))      # already present
+    obj, _, pi, st = ctx.solve_values(x, vals, want_pi=True)
+    piv = ctx.lp_stats()[0]
+    assert (st == 0).all() and (st1 == 0).all()
+    if name == "storm":
+        assert piv < piv1, (piv, piv1)
+    np.testing.assert_allclose(obj, obj1, rtol=1e-9, atol=1e-9)
+    b = I.rhs_of(name, x, vals)
+    lp = cpu.CpuLP(sp.W, sp.q, sp.senses)
+    lp.set_basis(head0)
+    pos, rows, cols = smps.scenario_positions(inst["sp2"], inst["sto"])
+    o_obj, _, _, o_st, _ = lp.solve_batch(rows, sp.r - sp.T @ x, vals - sp.r[rows], nthreads=4)
+    np.testing.assert_allclose(obj, o_obj, rtol=1e-9, atol=1e-9)
+    for s in range(N):
+        assert abs(pi[s] @ b[s] - obj[s]) <= 1e-9 * (1 + abs(obj[s]))
+        assert _dual_feasible(sp, pi[s])
+    # set_basis resets the pool
+    ctx.set_basis(head0)
+    assert ctx.pool_size() == 1

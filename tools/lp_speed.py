@@ -23,6 +23,16 @@ def main():
     ctx = twosd.SDContext(sp2, sto)
     ctx.compute_basis(x, smps.mean_values(sto))
     vals = smps.sample_values(sto, N, np.random.default_rng(1))
+    pool = int(os.environ.get("POOL", "1"))
+    if pool > 1:   # warm-start basis pool from independent training scenarios
+        tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+        ntr = int(os.environ.get("POOL_TRAIN", "16384"))
+        twosd.add_scenarios(tr, smps.sample_values(sto, ntr, np.random.default_rng(99)))
+        rounds = int(os.environ.get("POOL_ROUNDS", "1"))
+        for r in range(rounds):
+            target = 1 + (pool - 1) * (r + 1) // rounds
+            ctx.pool_build(tr, x, 0, ntr, target)
+        print(f"pool size {ctx.pool_size()}")
     epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
     twosd.add_scenarios(epi, vals)
     twosd.solve_batch(epi, x, 0, min(N, 4096), want_pi=False)
