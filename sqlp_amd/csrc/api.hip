@@ -14,6 +14,7 @@
 #include <string>
 #include <vector>
 #include <map>
+#include <thread>
 #include "twosd_internal.h"
 #include "twosd_ctx.h"
 
@@ -135,9 +136,8 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_xbase); dfree(c->d_B0K); dfree(c->d_eta); dfree(c->d_queue);
     dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_ops);
     dfree(c->d_dvtmp);
-    dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ax); dfree(c->d_sel_qv); dfree(c->d_sel_aptr); dfree(c->d_sel_abt);
-    dfree(c->d_sel_qptr); dfree(c->d_sel_qe); dfree(c->d_head_out); dfree(c->d_pool_pick); c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
-    dfree(c->d_kslot); dfree(c->d_kix); dfree(c->d_kv);
+    dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); dfree(c->d_sel_val); dfree(c->d_head_out); dfree(c->d_pool_pick); c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
+    dfree(c->d_kslot); dfree(c->d_kix); dfree(c->d_kv); dfree(c->d_kcoef); c->k_valid = false;
     dfree(c->d_d0); dfree(c->d_eidx); dfree(c->d_evals); dfree(c->d_stamps);
     dfree(c->d_wslot); dfree(c->d_wix); dfree(c->d_wv); dfree(c->d_bslot); dfree(c->d_bix); dfree(c->d_bv);
     dfree(c->d_brptr); dfree(c->d_brcol); dfree(c->d_brval); dfree(c->d_wrow4); dfree(c->d_wval4);
@@ -295,6 +295,7 @@ extern "C" int twosd_set_random_positions(twosd_ctx *c, int k, const int *row, c
     }
     c->k = k;
     c->prep_valid = false;
+    c->k_valid = false;
     cut_invalidate_pk(c);
     return TWOSD_OK;
 }
@@ -322,22 +323,39 @@ static void rhs_at(const twosd_ctx *c, const double *x, const double *dv, std::v
         }
 }
 
-// validate a basis head: valid distinct columns, nonsingular, dual feasible for q
-static int make_pool_basis(twosd_ctx *c, const std::vector<int> &head, PoolBasis &pb) {
+// validate a basis head (valid distinct columns, nonsingular, dual feasible for q) and
+// compute its inverse; thread-safe, returns nullptr or the reason it was rejected
+static const char *compute_pool_basis(const twosd_ctx *c, const std::vector<int> &head, PoolBasis &pb) {
     const HostLP &L = c->L;
     const int m = L.m, n = L.n;
     std::vector<char> seen(n + m, 0);
     for (int i = 0; i < m; ++i) {
-        if (head[i] < 0 || head[i] >= n + m || seen[head[i]]) return fail(TWOSD_E_ARG, "basis head[%d] = %d invalid/duplicate", i, head[i]);
+        if (head[i] < 0 || head[i] >= n + m || seen[head[i]]) return "basis head has an invalid or duplicate column";
         seen[head[i]] = 1;
     }
     std::vector<double> B;
     basis_matrix(L, head, B);
-    if (!dense_inverse(m, B, pb.Binv)) return fail(TWOSD_E_ARG, "basis matrix is singular");
+    if (!dense_inverse(m, B, pb.Binv)) return "basis matrix is singular";
     const double dinf = basis_dual_infeasibility(L, head, pb.Binv, pb.pi0);
-    if (dinf > 1e-7) return fail(TWOSD_E_ARG, "basis is not dual feasible (max dual infeasibility %g)", dinf);
+    if (dinf > 1e-7) return "basis is not dual feasible";
     pb.head = head;
-    return TWOSD_OK;
+    double amax = 0.0;
+    for (double v : pb.Binv) amax = std::max(amax, std::fabs(v));
+    const double drop = 1e-14 * amax;
+    pb.rptr.assign(1, 0);
+    pb.rcol.clear(); pb.rval.clear();
+    for (int i = 0; i < m; ++i) {
+        for (int cc = 0; cc < m; ++cc) {
+            const double v = pb.Binv[(size_t)i * m + cc];
+            if (std::fabs(v) > drop) { pb.rcol.push_back(cc); pb.rval.push_back(v); }
+        }
+        pb.rptr.push_back((int)pb.rcol.size());
+    }
+    return nullptr;
+}
+static int make_pool_basis(twosd_ctx *c, const std::vector<int> &head, PoolBasis &pb) {
+    const char *why = compute_pool_basis(c, head, pb);
+    return why ? fail(TWOSD_E_ARG, "%s", why) : TWOSD_OK;
 }
 
 // Upload the hypersparse-kernel form of every pool basis, pool-strided (pool[0] first, so
@@ -362,9 +380,6 @@ static int upload_pool(twosd_ctx *c) {
             isb[B.head[i]] = 1;
         }
         if (c->CH <= 0) continue;
-        double amax = 0.0;
-        for (double v : B.Binv) amax = std::max(amax, std::fabs(v));
-        const double drop = 1e-14 * amax;
         std::vector<double> d0((size_t)64 * c->CH, 0.0);
         for (int j = 0; j < n + m; ++j) {
             if (isb[j]) continue;
@@ -375,31 +390,24 @@ static int upload_pool(twosd_ctx *c) {
             d0[j] = (j < n ? L.q[j] : 0.0) - s;
         }
         d0_all.insert(d0_all.end(), d0.begin(), d0.end());
+        // columns of B^{-1} (CSC from the row CSR; rows ascending within a column)
+        std::vector<std::vector<std::pair<int, double>>> cols(m);
+        for (int i = 0; i < m; ++i)
+            for (int q = B.rptr[i]; q < B.rptr[i + 1]; ++q) cols[B.rcol[q]].push_back({i, B.rval[q]});
         std::vector<int> bs, bi;
         std::vector<double> bvv;
-        int nnz = 0;
         build_ell(c->R, [&](int cc, std::vector<std::pair<int, double>> &out) {
-            if (cc < m)
-                for (int i = 0; i < m; ++i) {
-                    const double v = B.Binv[(size_t)i * m + cc];
-                    if (std::fabs(v) > drop) { out.push_back({i, v}); ++nnz; }
-                }
+            if (cc < m) out = cols[cc];
         }, bs, bi, bvv);
-        bnnz[p] = nnz;
+        bnnz[p] = (int)B.rcol.size();
         const int eoff = (int)(bi_all.size() / 64);
         for (int v : bs) bs_all.push_back(v + eoff);
         bi_all.insert(bi_all.end(), bi.begin(), bi.end());
         bv_all.insert(bv_all.end(), bvv.begin(), bvv.end());
         const int roff = (int)rc_all.size();
-        rp_all.push_back(roff);
-        for (int i = 0; i < MP; ++i) {
-            if (i < m)
-                for (int cc = 0; cc < m; ++cc) {
-                    const double v = B.Binv[(size_t)i * m + cc];
-                    if (std::fabs(v) > drop) { rc_all.push_back(cc); rv_all.push_back(v); }
-                }
-            rp_all.push_back((int)rc_all.size());
-        }
+        for (int i = 0; i <= MP; ++i) rp_all.push_back(roff + B.rptr[std::min(i, m)]);
+        rc_all.insert(rc_all.end(), B.rcol.begin(), B.rcol.end());
+        rv_all.insert(rv_all.end(), B.rval.begin(), B.rval.end());
     }
     int rc;
     if ((rc = upload(&c->d_hb0, hb)) || (rc = upload(&c->d_basic0, basic)) || (rc = upload(&c->d_bnnz, bnnz))) return rc;
@@ -411,6 +419,7 @@ static int upload_pool(twosd_ctx *c) {
         c->b0_nnz = bnnz[0];
     }
     c->prep_valid = false;
+    c->k_valid = false;
     return TWOSD_OK;
 }
 
@@ -435,6 +444,8 @@ static int install_basis(twosd_ctx *c, const std::vector<int> &head) {
     HIPCHK(hipMemcpy(c->d_B0invT, BTp.data(), sizeof(double) * m * MP, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d_pi0, pip.data(), sizeof(double) * MP, hipMemcpyHostToDevice));
     c->pool.clear();
+    c->sel_lo.clear();
+    c->sel_hi.clear();
     c->pool.push_back(std::move(pb));
     if ((rc = upload_pool(c))) return rc;
     c->has_basis = true;
@@ -534,6 +545,18 @@ extern "C" int twosd_pool_build(twosd_ctx *c, int epi, const double *x, int firs
     HIPCHK(hipSetDevice(c->device));
     const int m = c->L.m;
     const int nh = count / 2, nv = count - nh;
+    if (count > 0 && c->k > 0) {   // training box of the deltas (selection row pruning)
+        std::vector<double> dv((size_t)count * c->k);
+        HIPCHK(hipMemcpy(dv.data(), E.d_dv + (size_t)first * c->k, sizeof(double) * dv.size(), hipMemcpyDeviceToHost));
+        c->sel_lo.assign(c->k, INFINITY);
+        c->sel_hi.assign(c->k, -INFINITY);
+        for (int s = 0; s < count; ++s)
+            for (int e = 0; e < c->k; ++e) {
+                c->sel_lo[e] = std::min(c->sel_lo[e], dv[(size_t)s * c->k + e]);
+                c->sel_hi[e] = std::max(c->sel_hi[e], dv[(size_t)s * c->k + e]);
+            }
+        c->prep_valid = false;
+    }
     if (nh > 0 && (int)c->pool.size() < max_pool) {
         const double *dh = E.d_dv + (size_t)first * c->k, *dval = dh + (size_t)nh * c->k;
         int rc;
@@ -565,12 +588,24 @@ extern "C" int twosd_pool_build(twosd_ctx *c, int epi, const double *x, int firs
             if (kv.second.second >= 0) order.push_back({-kv.second.first, kv.second.second});
         std::sort(order.begin(), order.end());
         const size_t old_size = c->pool.size();
-        for (auto &o : order) {
-            if ((int)c->pool.size() >= max_pool) break;
-            const int s = o.second;
-            const int r = pool_add(c, std::vector<int>(heads.begin() + (size_t)s * m, heads.begin() + (size_t)(s + 1) * m), false);
-            if (r < 0) return r;
-        }
+        // candidates are distinct and new; their inverses are computed in parallel, and a
+        // candidate that fails validation (numerically singular / dual infeasible) is skipped
+        const size_t want = std::min(order.size(), (size_t)max_pool - old_size);
+        std::vector<PoolBasis> cand(want);
+        std::vector<int> ok(want, 0);
+        const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nth; ++t)
+            th.emplace_back([&, t]() {
+                for (size_t a = t; a < want; a += nth) {
+                    const int s = order[a].second;
+                    std::vector<int> head(heads.begin() + (size_t)s * m, heads.begin() + (size_t)(s + 1) * m);
+                    ok[a] = compute_pool_basis(c, head, cand[a]) == nullptr;
+                }
+            });
+        for (auto &t : th) t.join();
+        for (size_t a = 0; a < want; ++a)
+            if (ok[a]) c->pool.push_back(std::move(cand[a]));
         if (c->pool.size() > old_size) {
             if ((rc = upload_pool(c))) return rc;
             if ((rc = run_lp(c, x, dval, nv, false, false))) return rc;
@@ -629,6 +664,46 @@ extern "C" int twosd_epigraph_info(twosd_ctx *c, int epi, int *ns, double *tw) {
     return TWOSD_OK;
 }
 
+// x-independent element data of the pool (rebuilt when the pool or the positions change):
+// per basis p the rows of B_p^{-1}[:, row_e] over the random elements e (host CSR kptr/ke/
+// kraw, e ascending) and the same as sliced ELL on the device (kslot pool-strided, absolute
+// into kix/kv).  The kernels multiply the scenario deltas by coef_e(x) (d_kcoef) themselves.
+static int prepare_elements(twosd_ctx *c) {
+    const int m = c->L.m, k = c->k;
+    std::vector<std::vector<int>> bycol(m);   // random elements on each row
+    for (int e = 0; e < k; ++e) bycol[c->pos_row[e]].push_back(e);
+    std::vector<int> ks, ki;
+    std::vector<double> kv;
+    for (PoolBasis &B : c->pool) {
+        B.kptr.assign(1, 0);
+        B.ke.clear(); B.kraw.clear();
+        std::vector<std::pair<int, double>> row;
+        for (int i = 0; i < m; ++i) {
+            row.clear();
+            for (int q = B.rptr[i]; q < B.rptr[i + 1]; ++q)
+                for (int e : bycol[B.rcol[q]]) row.push_back({e, B.rval[q]});
+            std::sort(row.begin(), row.end());
+            for (auto &ev : row) { B.ke.push_back(ev.first); B.kraw.push_back(ev.second); }
+            B.kptr.push_back((int)B.ke.size());
+        }
+        if (c->CH <= 0) continue;
+        std::vector<int> sl, ix;
+        std::vector<double> vv;
+        build_ell(c->R, [&](int i, std::vector<std::pair<int, double>> &out) {
+            if (i < m)
+                for (int q = B.kptr[i]; q < B.kptr[i + 1]; ++q) out.push_back({B.ke[q], B.kraw[q]});
+        }, sl, ix, vv);
+        const int eoff = (int)(ki.size() / 64);
+        for (int v : sl) ks.push_back(v + eoff);
+        ki.insert(ki.end(), ix.begin(), ix.end());
+        kv.insert(kv.end(), vv.begin(), vv.end());
+    }
+    int rc;
+    if (c->CH > 0 && ((rc = upload(&c->d_kslot, ks)) || (rc = upload(&c->d_kix, ki)) || (rc = upload(&c->d_kv, kv)))) return rc;
+    c->k_valid = true;
+    return TWOSD_OK;
+}
+
 // primal infeasibility of a basic variable at value x (h_infeas of lp_hyper.hip, tolerance 1e-9)
 static double host_infeas(double x, int bt) {
     const double tol = 1e-9;
@@ -637,91 +712,79 @@ static double host_infeas(double x, int bt) {
     return std::fabs(x) > tol ? x : 0.0;
 }
 
-// per-x shared data: xbase = B0^{-1}(r - T x), B0K[e] = coef_e * B0^{-1}[:, row_e] (dense, primary
-// basis); for the hypersparse kernel, per pool basis p: xbase_p (MP) and the CSR by row of
-// coef_e * B_p^{-1}[i][row_e] as sliced ELL (kslot pool-strided, absolute into kix/kv)
+// per-x shared data: b = r - T x; per pool basis xbase_p = B_p^{-1} b (sparse rows);
+// coef_e(x); dense B0K[e] = coef_e B0^{-1}[:, row_e] for the dense kernel; with a pool, the
+// selection stream (active rows that can turn infeasible on the training box of the deltas)
 int twosd::prepare_x(twosd_ctx *c, const double *x) {
     const int m = c->L.m, MP = c->MP, k = c->k, n1 = c->n1;
     if (c->prep_valid && c->prep_x.size() == (size_t)n1 && (n1 == 0 || std::equal(c->prep_x.begin(), c->prep_x.end(), x)))
         return TWOSD_OK;
+    int rc;
+    if (!c->k_valid && (rc = prepare_elements(c))) return rc;
     std::vector<double> b;
     rhs_at(c, x, nullptr, b);
     const int P = (int)c->pool.size();
+    std::vector<double> coef(std::max(k, 1), 1.0);
+    for (int e = 0; e < k; ++e) coef[e] = c->pos_col[e] < 0 ? 1.0 : -x[c->pos_col[e]];
     std::vector<double> xb((size_t)P * MP, 0.0), bk((size_t)std::max(k, 1) * MP, 0.0);
-    std::vector<int> ks, ki;
-    std::vector<double> kv;
-    // pool selection (P > 1): per basis the rows whose x_B does not depend on the scenario
-    // fold into cinf, the others are listed with their entries
-    std::vector<int8_t> bt(c->L.n + m);
-    if (P > 1) HIPCHK(hipMemcpy(bt.data(), c->d_btype, bt.size(), hipMemcpyDeviceToHost));
-    std::vector<double> cinf(P, 0.0), ax, qv;
-    std::vector<int> aptr(1, 0), abt, qptr(1, 0), qe;
     for (int p = 0; p < P; ++p) {
-        const std::vector<double> &Bi = c->pool[p].Binv;
+        const PoolBasis &B = c->pool[p];
         for (int i = 0; i < m; ++i) {
-            const double *row = &Bi[(size_t)i * m];
             double s = 0.0;
-            for (int j = 0; j < m; ++j) s += row[j] * b[j];
+            for (int q = B.rptr[i]; q < B.rptr[i + 1]; ++q) s += B.rval[q] * b[B.rcol[q]];
             xb[(size_t)p * MP + i] = s;
         }
-        if (p == 0)
-            for (int e = 0; e < k; ++e) {
-                const int rr = c->pos_row[e], cc = c->pos_col[e];
-                const double coef = cc < 0 ? 1.0 : -x[cc];
-                for (int i = 0; i < m; ++i) bk[(size_t)e * MP + i] = coef * Bi[(size_t)i * m + rr];
-            }
-        if (c->CH > 0) {
-            double amax = 0.0;
-            for (double v : Bi) amax = std::max(amax, std::fabs(v));
-            const double drop = 1e-14 * amax;
-            std::vector<std::vector<std::pair<int, double>>> rows(m);
-            for (int i = 0; i < m; ++i)
-                for (int e = 0; e < k; ++e) {
-                    const double bv = Bi[(size_t)i * m + c->pos_row[e]];
-                    const double v = (c->pos_col[e] < 0 ? 1.0 : -x[c->pos_col[e]]) * bv;
-                    if (std::fabs(bv) > drop && v != 0.0) rows[i].push_back({e, v});
-                }
-            std::vector<int> sl, ix;
-            std::vector<double> vv;
-            build_ell(c->R, [&](int i, std::vector<std::pair<int, double>> &out) {
-                if (i < m) out = rows[i];
-            }, sl, ix, vv);
-            const int eoff = (int)(ki.size() / 64);
-            for (int v : sl) ks.push_back(v + eoff);
-            ki.insert(ki.end(), ix.begin(), ix.end());
-            kv.insert(kv.end(), vv.begin(), vv.end());
-            if (P > 1) {
-                for (int i = 0; i < m; ++i) {
-                    const int h = c->pool[p].head[i], t = bt[h];
-                    const double xv = xb[(size_t)p * MP + i];
-                    if (rows[i].empty()) { cinf[p] += std::fabs(host_infeas(xv, t)); continue; }
-                    ax.push_back(xv);
-                    abt.push_back(t);
-                    for (auto &ev : rows[i]) { qe.push_back(ev.first); qv.push_back(ev.second); }
-                    qptr.push_back((int)qe.size());
-                }
-                aptr.push_back((int)ax.size());
-            }
-        }
     }
+    for (int e = 0; e < k; ++e) {
+        const int rr = c->pos_row[e];
+        for (int i = 0; i < m; ++i) bk[(size_t)e * MP + i] = coef[e] * c->B0inv[(size_t)i * m + rr];
+    }
+    if ((rc = dalloc(&c->d_B0K, (size_t)std::max(k, 1) * MP)) || (rc = dalloc(&c->d_xbase, (size_t)P * MP)) ||
+        (rc = upload(&c->d_kcoef, coef)))
+        return rc;
+    HIPCHK(hipMemcpy(c->d_xbase, xb.data(), sizeof(double) * xb.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_B0K, bk.data(), sizeof(double) * std::max(k, 1) * MP, hipMemcpyHostToDevice));
     if (P > 1 && c->CH > 0) {
-        int rc;
-        if ((rc = upload(&c->d_sel_cinf, cinf)) || (rc = upload(&c->d_sel_aptr, aptr)) || (rc = upload(&c->d_sel_ax, ax)) ||
-            (rc = upload(&c->d_sel_abt, abt)) || (rc = upload(&c->d_sel_qptr, qptr)) || (rc = upload(&c->d_sel_qe, qe)) ||
-            (rc = upload(&c->d_sel_qv, qv)))
+        std::vector<int8_t> bt(c->L.n + m);
+        HIPCHK(hipMemcpy(bt.data(), c->d_btype, bt.size(), hipMemcpyDeviceToHost));
+        std::vector<double> cinf(P, 0.0), sval;
+        std::vector<int> sptr(1, 0), scode;
+        c->sel_rows = 0;
+        const bool box = !c->sel_lo.empty();
+        for (int p = 0; p < P; ++p) {
+            const PoolBasis &B = c->pool[p];
+            for (int i = 0; i < m; ++i) {
+                const int t = bt[B.head[i]];
+                const double xv = xb[(size_t)p * MP + i];
+                const int q0 = B.kptr[i], q1 = B.kptr[i + 1];
+                if (q0 == q1) { cinf[p] += std::fabs(host_infeas(xv, t)); continue; }
+                if (box) {
+                    // interval of x_i over the training box of the deltas: a row that stays
+                    // feasible on the whole box never contributes, so it is left out
+                    double lo = xv, hi = xv, mag = std::fabs(xv);
+                    for (int q = q0; q < q1; ++q) {
+                        const double g = coef[B.ke[q]] * B.kraw[q];
+                        const double a = g * c->sel_lo[B.ke[q]], bb = g * c->sel_hi[B.ke[q]];
+                        lo += std::min(a, bb);
+                        hi += std::max(a, bb);
+                        mag += std::max(std::fabs(a), std::fabs(bb));
+                    }
+                    const double tol = 1e-9 + 1e-12 * mag;
+                    const bool feasible_box = (t == BT_Y || t == BT_L) ? lo > tol : (t == BT_G) ? hi < -tol : false;
+                    if (std::isfinite(lo) && std::isfinite(hi) && feasible_box) continue;
+                }
+                scode.push_back(-1 - t);
+                sval.push_back(xv);
+                ++c->sel_rows;
+                for (int q = q0; q < q1; ++q) { scode.push_back(B.ke[q]); sval.push_back(B.kraw[q]); }
+            }
+            sptr.push_back((int)scode.size());
+        }
+        if ((rc = upload(&c->d_sel_cinf, cinf)) || (rc = upload(&c->d_sel_ptr, sptr)) || (rc = upload(&c->d_sel_code, scode)) ||
+            (rc = upload(&c->d_sel_val, sval)))
             return rc;
-        c->sel_rows = (int64_t)ax.size();
-        c->sel_nnz = (int64_t)qe.size();
+        c->sel_nnz = (int64_t)scode.size() - c->sel_rows;
     }
-    int rc;
-    if ((rc = dalloc(&c->d_B0K, (size_t)std::max(k, 1) * MP)) || (rc = dalloc(&c->d_xbase, (size_t)P * MP))) return rc;
-    HIPCHK(hipMemcpyAsync(c->d_xbase, xb.data(), sizeof(double) * xb.size(), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->d_B0K, bk.data(), sizeof(double) * std::max(k, 1) * MP, hipMemcpyHostToDevice, c->stream));
-    if (c->CH > 0) {
-        HIPCHK(hipStreamSynchronize(c->stream));
-        if ((rc = upload(&c->d_kslot, ks)) || (rc = upload(&c->d_kix, ki)) || (rc = upload(&c->d_kv, kv))) return rc;
-    }
-    HIPCHK(hipStreamSynchronize(c->stream));
     c->prep_x.assign(x, x + n1);
     c->prep_valid = true;
     return TWOSD_OK;
@@ -772,7 +835,7 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
         H.brptr = c->d_brptr; H.brcol = c->d_brcol; H.brval = c->d_brval;
         H.wrow4 = c->has_pack4 ? c->d_wrow4 : nullptr;
         H.wval4 = c->has_pack4 ? c->d_wval4 : nullptr;
-        H.kslot = c->d_kslot; H.kix = c->d_kix; H.kv = c->d_kv;
+        H.kslot = c->d_kslot; H.kix = c->d_kix; H.kv = c->d_kv; H.kcoef = c->d_kcoef;
         H.xbase = c->d_xbase; H.d0 = c->d_d0; H.hb0 = c->d_hb0;
         H.basic0 = c->d_basic0; H.fixedmask = c->d_fixedmask; H.ubmask = c->d_ubmask;
         H.dv = d_dv; H.eidx = c->d_eidx; H.evals = c->d_evals; H.queue = c->d_queue;
@@ -803,8 +866,9 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
         if (H.npool > 1) {
             PoolSelParams S{};
             S.N = N; S.k = c->k; S.npool = H.npool; S.dv = d_dv;
-            S.cinf = c->d_sel_cinf; S.aptr = c->d_sel_aptr; S.ax = c->d_sel_ax; S.abt = c->d_sel_abt;
-            S.qptr = c->d_sel_qptr; S.qe = c->d_sel_qe; S.qv = c->d_sel_qv; S.pick = c->d_pool_pick;
+            S.kcoef = c->d_kcoef;
+            S.cinf = c->d_sel_cinf; S.sptr = c->d_sel_ptr; S.code = c->d_sel_code; S.val = c->d_sel_val;
+            S.pick = c->d_pool_pick;
             HIPCHK(launch_pool_select(S, c->stream));
         }
         HIPCHK(launch_hyper(R, CH, H, nblocks, hyper_lds_bytes(R, kmax, c->k), c->stream));

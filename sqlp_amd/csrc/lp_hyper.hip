@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         if (s >= P.N) break;
 
         const double *dvs = P.dv + (size_t)s * P.k;
-        for (int e = lane; e < P.k; e += 64) dvl[e] = dvs[e];
+        for (int e = lane; e < P.k; e += 64) dvl[e] = P.kcoef[e] * dvs[e];   // coef_e(x) dv_e
         h_wave_sync();
         // x_B of pool basis p at this scenario: xbase_p + sum_e coef_e B_p^{-1}[i][row_e] dv_e
         // (sliced ELL by row: independent coalesced loads, deltas gathered from LDS)
@@ -582,26 +582,53 @@ __global__ void __launch_bounds__(256) pool_select_kernel(PoolSelParams S) {
     extern __shared__ double dvt[];   // k x 65 (padded)
     __shared__ double bsum[kWavesPerBlock][64];
     __shared__ int bidx[kWavesPerBlock][64];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar stream loads
     const int s0 = blockIdx.x * 64;
     const int k = S.k;
     const int ns = min(64, S.N - s0);
     for (int idx = threadIdx.x; idx < 64 * k; idx += 256) {
         const int sl = idx / k, e = idx - sl * k;
-        dvt[e * 65 + sl] = sl < ns ? S.dv[(size_t)s0 * k + idx] : 0.0;
+        dvt[e * 65 + sl] = sl < ns ? S.kcoef[e] * S.dv[(size_t)s0 * k + idx] : 0.0;
     }
     __syncthreads();
     double best = INFINITY;
     int bp = 0;
     for (int p = wid; p < S.npool; p += kWavesPerBlock) {
-        double inf = S.cinf[p];
-        const int a0 = S.aptr[p], a1 = S.aptr[p + 1];
-        for (int a = a0; a < a1; ++a) {
-            double x = S.ax[a];
-            const int q0 = S.qptr[a], q1 = S.qptr[a + 1];
-            for (int q = q0; q < q1; ++q) x = fma(S.qv[q], dvt[S.qe[q] * 65 + lane], x);
-            inf += fabs(h_infeas(x, S.abt[a]));
+        // one flat, wave-uniform stream per basis: a row-start record (code -1 - bound type,
+        // value xbase_i) followed by the row's entries (code e, value coef_e B^{-1}[i][row_e]);
+        // no load depends on the loop state, so the stream pipelines through the scalar cache
+        double inf = S.cinf[p], x = 0.0;
+        int bt = -1;
+        const int j0 = S.sptr[p], j1 = S.sptr[p + 1];
+        auto step = [&](int code, double v, double dl) {
+            if (code < 0) {
+                if (bt >= 0) inf += fabs(h_infeas(x, bt));
+                x = v;
+                bt = -1 - code;
+            } else {
+                x = fma(v, dl, x);
+            }
+        };
+        int j = (__ballot(inf < best) == 0) ? j1 : j0;   // constant rows alone already lose
+        for (; j + 8 <= j1; j += 8) {   // batches of 8 records: scalar loads and LDS reads in flight together
+            int cd[8];
+            double vv[8], dl[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) { cd[u] = S.code[j + u]; vv[u] = S.val[j + u]; }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) dl[u] = dvt[(cd[u] < 0 ? 0 : cd[u]) * 65 + lane];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) step(cd[u], vv[u], dl[u]);
+            // exact pruning: inf only grows (sum of nonnegative terms), so once no lane can
+            // still beat its best, this basis cannot win for any of the 64 scenarios
+            if (__ballot(inf < best) == 0) { bt = -1; inf = INFINITY; j = j1; break; }
         }
+        for (; j < j1; ++j) {
+            const int cd = S.code[j];
+            step(cd, S.val[j], dvt[(cd < 0 ? 0 : cd) * 65 + lane]);
+        }
+        if (bt >= 0) inf += fabs(h_infeas(x, bt));
         if (inf < best) { best = inf; bp = p; }
     }
     bsum[wid][lane] = best;

@@ -21,6 +21,10 @@ struct PoolBasis {
     std::vector<int> head;        // m basic columns (0-based over [y; slacks])
     std::vector<double> Binv;     // m x m row-major
     std::vector<double> pi0;      // c_B' B^{-1}
+    std::vector<int> rptr, rcol;  // B^{-1} rows, CSR (|v| > 1e-14 max|B^{-1}|)
+    std::vector<double> rval;
+    std::vector<int> kptr, ke;    // rows of B^{-1}[:, row_e] over the random elements e (x-independent)
+    std::vector<double> kraw;
 };
 
 }  // namespace twosd
@@ -50,14 +54,17 @@ struct twosd_ctx {
     double *d_B0inv = nullptr, *d_B0invT = nullptr, *d_pi0 = nullptr, *d_xbase = nullptr, *d_B0K = nullptr;
     std::vector<twosd::PoolBasis> pool;   // warm-start basis pool, pool[0] = head0
     // pool selection data (per x, prepare_x): constant-row infeasibility, active rows, entries
-    double *d_sel_cinf = nullptr, *d_sel_ax = nullptr, *d_sel_qv = nullptr;
-    int *d_sel_aptr = nullptr, *d_sel_abt = nullptr, *d_sel_qptr = nullptr, *d_sel_qe = nullptr;
+    double *d_sel_cinf = nullptr, *d_sel_val = nullptr;
+    int *d_sel_ptr = nullptr, *d_sel_code = nullptr;
     int64_t sel_nnz = 0, sel_rows = 0;
+    std::vector<double> sel_lo, sel_hi;   // training box of the deltas (empty: no row pruning)
     int *d_bnnz = nullptr;        // npool: nnz of each pool B^{-1} (FMA accounting)
     int *d_head_out = nullptr, *d_pool_pick = nullptr;   // optional LP outputs (pool building)
     size_t head_cap = 0, pick_cap = 0;
     bool want_head = false;
     bool prep_valid = false;
+    bool k_valid = false;         // K rows / ELL of the pool (depend on the pool and the positions)
+    double *d_kcoef = nullptr;    // k: coef_e(x) = 1 (RHS element) or -x[col] (T element)
     std::vector<double> prep_x;
     // hypersparse kernel data
     int CH = 0;                   // column slots per lane of the hypersparse kernel

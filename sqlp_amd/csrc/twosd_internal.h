@@ -64,7 +64,8 @@ struct HyperParams {
     const unsigned long long *wrow4; const double *wval4;
     // per pool basis p, rows i = 64t + lane of coef_e B_p^{-1}[i][row_e] as sliced ELL (R slots,
     // kslot pool-strided npool x (R+1), absolute into the concatenated kix (= e) / kv)
-    const int *kslot, *kix; const double *kv;
+    const int *kslot, *kix; const double *kv;           // values B_p^{-1}[i][row_e] (x-independent)
+    const double *kcoef;                                // k: coef_e(x) applied to the deltas
     const double *xbase;                                // MP
     const double *d0;                                   // 64*C reduced costs at B0 (lane-slot order j = 64c+lane)
     const int *hb0;                                     // MP
@@ -88,10 +89,10 @@ struct HyperParams {
 struct PoolSelParams {
     int N, k, npool;
     const double *dv;                                   // N x k
+    const double *kcoef;                                // k: coef_e(x)
     const double *cinf;                                 // npool: infeasibility of the constant rows
-    const int *aptr;                                    // npool + 1 -> active rows (K row non-empty)
-    const double *ax; const int *abt;                   // active row: xbase, bound type
-    const int *qptr; const int *qe; const double *qv;   // active row entries (e, coef_e B^{-1}[i][row_e])
+    const int *sptr;                                    // npool + 1 -> flat stream of active rows
+    const int *code; const double *val;                 // row start: (-1 - bound type, xbase_i); entry: (e, coef)
     int *pick;                                          // N out
 };
 size_t pool_select_lds_bytes(int k);

@@ -28,23 +28,27 @@ def main():
         tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
         ntr = int(os.environ.get("POOL_TRAIN", "16384"))
         twosd.add_scenarios(tr, smps.sample_values(sto, ntr, np.random.default_rng(99)))
-        rounds = int(os.environ.get("POOL_ROUNDS", "1"))
-        for r in range(rounds):
-            target = 1 + (pool - 1) * (r + 1) // rounds
-            ctx.pool_build(tr, x, 0, ntr, target)
-        print(f"pool size {ctx.pool_size()}")
+        import time
+        t0 = time.perf_counter()
+        ctx.pool_build(tr, x, 0, ntr, pool)
+        print(f"pool size {ctx.pool_size()} built in {time.perf_counter() - t0:.2f} s")
     epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
     twosd.add_scenarios(epi, vals)
     twosd.solve_batch(epi, x, 0, min(N, 4096), want_pi=False)
-    ts = []
-    for _ in range(reps):
-        obj, _, _, st = twosd.solve_batch(epi, x, 0, N, want_pi=False)
+    ts, walls = [], []
+    import time
+    for rep in range(reps):
+        # XALT=1: alternate x between reps (per-x host preparation inside the wall time)
+        xr = x * (1.0 + 1e-3 * (rep % 2)) if os.environ.get("XALT") else x
+        t0 = time.perf_counter()
+        obj, _, _, st = twosd.solve_batch(epi, xr, 0, N, want_pi=False)
+        walls.append((time.perf_counter() - t0) * 1e3)
         ts.append(ctx.timings_us()[0] / 1e3)
     piv, pmax = ctx.lp_stats()
     t = min(ts)
     print(f"{os.environ.get('TWOSD_LIB', 'default')} {name} N={N} lp_ms={t:.2f} ({' '.join(f'{v:.1f}' for v in ts)}) "
           f"scen/s={N / t * 1e3:.0f} pivots/scen={piv / N:.2f} max={pmax} status_ok={(st == 0).mean():.4f} "
-          f"objsum={obj.sum():.6e}")
+          f"objsum={obj.sum():.6e} wall_ms={' '.join(f'{v:.1f}' for v in walls)}")
 
 
 if __name__ == "__main__":
