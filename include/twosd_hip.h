@@ -100,6 +100,14 @@ int twosd_pool_build(twosd_ctx *ctx, int epi, const double *x, int first, int co
                      int *pool_size);
 int twosd_pool_size(twosd_ctx *ctx, int *size);
 int twosd_pool_get(twosd_ctx *ctx, int p, int *head);
+/* Pool basis each scenario of the last LP batch started from (first N of it; 0 = the
+ * primary basis, also after a pool start was retried from it). */
+int twosd_last_pool_picks(twosd_ctx *ctx, int N, int *picks);
+
+/* Drop the per-x data cached from the last x (x_B of every pool basis, coef_e(x), the
+ * pool-selection stream, the cut's per-x products); the next call at any x rebuilds it.
+ * Results never depend on it -- benchmarks call it so each pass pays its per-x setup. */
+int twosd_invalidate_x(twosd_ctx *ctx);
 
 /* Epigraphs (sdEpigraph, epigraph.jl:17-61): per-epigraph scenario pool + weights. */
 int twosd_epigraph_create(twosd_ctx *ctx, int *epi_out);

@@ -38,6 +38,8 @@ SIGNATURES = [
     ("twosd_pool_build", I, [P, I, P, I, I, I, P]),
     ("twosd_pool_size", I, [P, P]),
     ("twosd_pool_get", I, [P, I, P]),
+    ("twosd_last_pool_picks", I, [P, I, P]),
+    ("twosd_invalidate_x", I, [P]),
     ("twosd_epigraph_create", I, [P, P]),
     ("twosd_add_scenarios", I, [P, I, I, P, P]),
     ("twosd_epigraph_info", I, [P, I, P, P]),

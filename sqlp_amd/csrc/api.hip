@@ -623,6 +623,23 @@ extern "C" int twosd_pool_build(twosd_ctx *c, int epi, const double *x, int firs
     return TWOSD_OK;
 }
 
+extern "C" int twosd_last_pool_picks(twosd_ctx *c, int N, int *picks) {
+    if (!c || !picks || N < 0 || N > c->last_lp_N) return fail(TWOSD_E_ARG, "last_pool_picks: bad arguments");
+    if (c->pool.size() <= 1 || !c->d_pool_pick) {
+        std::fill(picks, picks + N, 0);
+        return TWOSD_OK;
+    }
+    HIPCHK(hipMemcpy(picks, c->d_pool_pick, sizeof(int) * N, hipMemcpyDeviceToHost));
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_invalidate_x(twosd_ctx *c) {
+    if (!c) return fail(TWOSD_E_ARG, "invalidate_x: NULL context");
+    c->prep_valid = false;
+    cut_invalidate_pk(c);
+    return TWOSD_OK;
+}
+
 extern "C" int twosd_epigraph_create(twosd_ctx *c, int *epi_out) {
     if (!c || !c->has_template || !epi_out) return fail(TWOSD_E_STATE, "epigraph_create: no template");
     c->epis.emplace_back();

@@ -129,6 +129,16 @@ class SDContext:
                                         C.byref(n)))
         return n.value
 
+    def last_pool_picks(self, N):
+        """Pool basis every scenario of the last LP batch started from."""
+        picks = np.zeros(N, dtype=np.int32)
+        check(self.lib.twosd_last_pool_picks(self.h, int(N), ptr(picks)))
+        return picks
+
+    def invalidate_x(self):
+        """Drop the per-x cache (next solve / cut recomputes it; results unchanged)."""
+        check(self.lib.twosd_invalidate_x(self.h))
+
     def pool_size(self) -> int:
         n = C.c_int(0)
         check(self.lib.twosd_pool_size(self.h, C.byref(n)))

@@ -117,6 +117,21 @@ def test_lp_basis_pool(name):
     for s in range(N):
         assert abs(pi[s] @ b[s] - obj[s]) <= 1e-9 * (1 + abs(obj[s]))
         assert _dual_feasible(sp, pi[s])
+    # vertex parity: the oracle dual simplex started from the pool basis each scenario
+    # picked reaches the same vertex (same pivot rules)
+    picks = ctx.last_pool_picks(N)
+    assert picks.min() >= 0 and picks.max() < size
+    if name == "storm":
+        assert len(np.unique(picks)) > 1
+    o_pi = np.zeros_like(pi)
+    for p in np.unique(picks):
+        sel = np.nonzero(picks == p)[0]
+        lp.set_basis(ctx.pool_get(p))
+        o2, o_pi[sel], _, o2st, _ = lp.solve_batch(rows, sp.r - sp.T @ x, vals[sel] - sp.r[rows], nthreads=4)
+        assert (o2st == 0).all()
+        np.testing.assert_allclose(o2, obj[sel], rtol=1e-9, atol=1e-9)
+    same = np.mean([np.allclose(pi[s], o_pi[s], rtol=1e-9, atol=1e-9) for s in range(N)])
+    assert same >= 0.95, same
     # set_basis resets the pool
     ctx.set_basis(head0)
     assert ctx.pool_size() == 1
