@@ -139,8 +139,8 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); dfree(c->d_sel_val); dfree(c->d_head_out); dfree(c->d_pool_pick); c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
     dfree(c->d_kslot); dfree(c->d_kix); dfree(c->d_kv); dfree(c->d_kcoef); c->k_valid = false;
     dfree(c->d_d0); dfree(c->d_eidx); dfree(c->d_evals); dfree(c->d_stamps);
-    dfree(c->d_wslot); dfree(c->d_wix); dfree(c->d_wv); dfree(c->d_bslot); dfree(c->d_bix); dfree(c->d_bv);
-    dfree(c->d_brptr); dfree(c->d_brcol); dfree(c->d_brval); dfree(c->d_wrow4); dfree(c->d_wval4);
+    dfree(c->d_wrptr); dfree(c->d_wcol); dfree(c->d_wval); dfree(c->d_bslot); dfree(c->d_bix); dfree(c->d_bv);
+    dfree(c->d_brptr); dfree(c->d_brcol); dfree(c->d_brval);
     c->earena_slots = 0; c->earena_cap = 0;
     for (auto &e : c->epis) { dfree(e.d_dv); dfree(e.d_w); }
     c->epis.clear();
@@ -235,43 +235,22 @@ extern "C" int twosd_set_template(twosd_ctx *c, int m2, int n1, int n2, const in
     HIPCHK(hipMemcpy(c->d_btype, bt.data(), n2 + m2, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d_fixedmask, fixedm.data(), sizeof(uint64_t) * 64, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d_ubmask, ubm.data(), sizeof(uint64_t) * 64, hipMemcpyHostToDevice));
-    if (c->CH > 0) {   // sliced ELL of the columns of [W I] for the hypersparse kernel
-        std::vector<int> ws, wi;
-        std::vector<double> wvv;
-        build_ell(c->CH, [&](int j, std::vector<std::pair<int, double>> &out) {
-            if (j < n2)
-                for (int p = L.colptr[j]; p < L.colptr[j + 1]; ++p) out.push_back({L.rowidx[p], L.val[p]});
-            else if (j < n2 + m2)
-                out.push_back({j - n2, 1.0});
-        }, ws, wi, wvv);
-        if ((rc = upload(&c->d_wslot, ws)) || (rc = upload(&c->d_wix, wi)) || (rc = upload(&c->d_wv, wvv))) return rc;
-        // packed-4 pricing layout when every column has <= 4 entries and m2 < 0xFFFF
-        int maxnnz = 1;
-        for (int j = 0; j < n2; ++j) maxnnz = std::max(maxnnz, L.colptr[j + 1] - L.colptr[j]);
-        // opt-in (TWOSD_PACK4=1): measured slower than sliced ELL on storm (divergent branches)
-        c->has_pack4 = maxnnz <= 4 && m2 < 0xFFFF && getenv("TWOSD_PACK4") && std::string(getenv("TWOSD_PACK4")) == "1";
-        if (c->has_pack4) {
-            const int S = c->CH;
-            std::vector<unsigned long long> pk((size_t)S * 64, ~0ull);
-            std::vector<double> pv((size_t)S * 256, 0.0);
-            for (int j = 0; j < 64 * S && j < n2 + m2; ++j) {
-                const int s = j >> 6, l = j & 63;
-                unsigned long long word = ~0ull;
-                int e = 0;
-                auto put = [&](int row, double v) {
-                    word &= ~(0xFFFFull << (16 * e));
-                    word |= (unsigned long long)row << (16 * e);
-                    pv[((size_t)s * 4 + e) * 64 + l] = v;
-                    ++e;
-                };
-                if (j < n2)
-                    for (int p = L.colptr[j]; p < L.colptr[j + 1]; ++p) put(L.rowidx[p], L.val[p]);
-                else
-                    put(j - n2, 1.0);
-                pk[(size_t)s * 64 + l] = word;
+    if (c->CH > 0) {   // W by rows (CSR, columns ascending) for the row-wise pricing scatter
+        std::vector<int> rp(m2 + 1, 0), rcn;
+        std::vector<double> rvv;
+        for (int j = 0; j < n2; ++j)
+            for (int p = L.colptr[j]; p < L.colptr[j + 1]; ++p) ++rp[L.rowidx[p] + 1];
+        for (int i = 0; i < m2; ++i) rp[i + 1] += rp[i];
+        rcn.resize(rp[m2]);
+        rvv.resize(rp[m2]);
+        std::vector<int> fill(rp.begin(), rp.end() - 1);
+        for (int j = 0; j < n2; ++j)
+            for (int p = L.colptr[j]; p < L.colptr[j + 1]; ++p) {
+                const int at = fill[L.rowidx[p]]++;
+                rcn[at] = j;
+                rvv[at] = L.val[p];
             }
-            if ((rc = upload(&c->d_wrow4, pk)) || (rc = upload(&c->d_wval4, pv))) return rc;
-        }
+        if ((rc = upload(&c->d_wrptr, rp)) || (rc = upload(&c->d_wcol, rcn)) || (rc = upload(&c->d_wval, rvv))) return rc;
     }
     c->has_template = true;
     c->k = 0;
@@ -832,10 +811,12 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
     }
     if (!c->d_queue && (rc = dalloc(&c->d_queue, 4))) return rc;
     if (c->use_hyper) {
-        const int kmax = c->kmax_override > 0 ? c->kmax_override : std::min(512, std::max(64, 2 * m + 32));
+        // eta capacity (pivots per scenario): 256 keeps two 4-wave blocks per CU within the LDS
+        const int kmax = c->kmax_override > 0 ? c->kmax_override : std::min(256, std::max(64, 2 * m + 32));
         const int ecap = std::max(4096, 32 * MP);
         const int CH = c->CH;
         const int bpc = hyper_max_blocks_per_cu(R, CH, kmax, c->k);
+        if (bpc < 1) return fail(TWOSD_E_UNSUPPORTED, "LP kernel: LDS slice too large (m = %d, k = %d)", m, c->k);
         const int nblocks = std::max(1, std::min((N + kWavesPerBlock - 1) / kWavesPerBlock, bpc * c->num_cus));
         const size_t slots = (size_t)nblocks * kWavesPerBlock;
         if (slots > c->earena_slots || ecap != c->earena_cap) {
@@ -847,11 +828,9 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
         HyperParams H{};
         H.m = m; H.n = n; H.k = c->k; H.N = N; H.kmax = kmax; H.ecap = ecap;
         H.colptr = c->d_colptr; H.rowidx = c->d_rowidx; H.val = c->d_val; H.q = c->d_q; H.btype = c->d_btype;
-        H.wslot = c->d_wslot; H.wix = c->d_wix; H.wv = c->d_wv;
+        H.wrptr = c->d_wrptr; H.wcol = c->d_wcol; H.wval = c->d_wval;
         H.bslot = c->d_bslot; H.bix = c->d_bix; H.bv = c->d_bv;
         H.brptr = c->d_brptr; H.brcol = c->d_brcol; H.brval = c->d_brval;
-        H.wrow4 = c->has_pack4 ? c->d_wrow4 : nullptr;
-        H.wval4 = c->has_pack4 ? c->d_wval4 : nullptr;
         H.kslot = c->d_kslot; H.kix = c->d_kix; H.kv = c->d_kv; H.kcoef = c->d_kcoef;
         H.xbase = c->d_xbase; H.d0 = c->d_d0; H.hb0 = c->d_hb0;
         H.basic0 = c->d_basic0; H.fixedmask = c->d_fixedmask; H.ubmask = c->d_ubmask;
@@ -888,7 +867,7 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
             S.pick = c->d_pool_pick;
             HIPCHK(launch_pool_select(S, c->stream));
         }
-        HIPCHK(launch_hyper(R, CH, H, nblocks, hyper_lds_bytes(R, kmax, c->k), c->stream));
+        HIPCHK(launch_hyper(R, CH, H, nblocks, hyper_lds_bytes(R, CH, kmax, c->k), c->stream));
         HIPCHK(hipEventRecord(c->ev[1], c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         float ms = 0;

@@ -79,12 +79,15 @@ __device__ __forceinline__ int h_get_row_i(const int (&a)[R], int p) {
     return __builtin_amdgcn_readlane(v, p & 63);
 }
 
-// per-wave LDS slice: ut, rho (MP doubles each), etap (u16), etaoff (int), scenario deltas (k doubles)
-static __host__ __device__ inline size_t hyper_slice_bytes(int R, int kmax, int k) {
+// per-wave LDS slice: a union of {ut, rho} (MP doubles each) and alpha (64C doubles, the
+// pivot row over all columns during pricing), the scenario deltas (k doubles), etap (u16),
+// etaoff (int)
+static __host__ __device__ inline int hyper_union_doubles(int R, int C) { return 128 * R > 64 * C ? 128 * R : 64 * C; }
+static __host__ __device__ inline size_t hyper_slice_bytes(int R, int C, int kmax, int k) {
     const int kmaxp = (kmax + 3) & ~3;
-    return (size_t)(16 * 64 * R + 2 * kmaxp + 4 * (kmaxp + 4)) + 8 * (size_t)((k + 1) & ~1);
+    return 8 * (size_t)hyper_union_doubles(R, C) + 8 * (size_t)((k + 1) & ~1) + 2 * kmaxp + 4 * (kmaxp + 4);
 }
-size_t hyper_lds_bytes(int R, int kmax, int k) { return (size_t)kWavesPerBlock * hyper_slice_bytes(R, kmax, k); }
+size_t hyper_lds_bytes(int R, int C, int kmax, int k) { return (size_t)kWavesPerBlock * hyper_slice_bytes(R, C, kmax, k); }
 
 // min waves per SIMD (VGPR budget 256 / 168): measured on MI355X, storm (R=9) is fastest
 // at 2 waves/SIMD, ssn (R=4) at 3 (tools/lp_speed.py)
@@ -98,12 +101,13 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
     const int wid = threadIdx.x >> 6;
     constexpr int MP = 64 * R;
     const int kmaxp = (P.kmax + 3) & ~3;
-    char *slice = reinterpret_cast<char *>(lds_raw) + (size_t)wid * hyper_slice_bytes(R, P.kmax, P.k);
+    char *slice = reinterpret_cast<char *>(lds_raw) + (size_t)wid * hyper_slice_bytes(R, C, P.kmax, P.k);
     double *ut = reinterpret_cast<double *>(slice);        // dense scratch vector (u, then alpha_q)
     double *rho = ut + MP;                                  // pivot row of B^{-1}
-    unsigned short *etap = reinterpret_cast<unsigned short *>(rho + MP);
+    double *alpha = ut;                                     // pricing: alpha~_j over the same space
+    double *dvl = ut + hyper_union_doubles(R, C);           // this scenario's coef_e(x) dv_e
+    unsigned short *etap = reinterpret_cast<unsigned short *>(dvl + ((P.k + 1) & ~1));
     int *etaoff = reinterpret_cast<int *>(etap + kmaxp);
-    double *dvl = reinterpret_cast<double *>(etaoff + kmaxp + 4);   // this scenario's deltas
 
     const int m = P.m, n = P.n;
     const int slot_id = blockIdx.x * kWavesPerBlock + wid;
@@ -112,8 +116,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
     const uint64_t fixedm = P.fixedmask[lane];
     const uint64_t ubm = P.ubmask[lane];
 
-#pragma unroll
-    for (int t = 0; t < R; ++t) { ut[64 * t + lane] = 0.0; rho[64 * t + lane] = 0.0; }
+    for (int j = lane; j < hyper_union_doubles(R, C); j += 64) ut[j] = 0.0;
     h_wave_sync();
     STAMP_DECL
 
@@ -253,41 +256,64 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             }
             STAMP(3)
 
-            // ---- 3. Harris ratio test over nonbasic columns.  d lives in registers; the pivot
-            // row alpha~ is recomputed (same gathers, same order -> same bits) in passes 2/3
-            // only for the few columns pass 1 found nonzero / eligible (rho is ~2-5 % dense).
-            auto alpha_col = [&](int c) -> double {
-                const int e0 = P.wslot[c], e1 = P.wslot[c + 1];
-                double a = 0.0;
-#pragma unroll 1
-                for (int e = e0; e < e1; ++e) {
-                    const double v = P.wv[e * 64 + lane];
-                    a = fma(rho[P.wix[e * 64 + lane]], v, a);
+            // ---- 3. pricing: alpha~_j = rho' a_j for every column as a row-wise scatter over
+            // the nonzeros of rho (2-5 % of the rows).  Rows go in ascending order, one row per
+            // wave step (its columns are distinct lanes), so alpha_j accumulates over i
+            // ascending: the same FMAs in the same order as a column-wise gather.  alpha lives
+            // in LDS over the ut/rho space (both zero here once rho is in registers).
+            double rv[R];
+#pragma unroll
+            for (int t = 0; t < R; ++t) rv[t] = rho[64 * t + lane];
+            h_wave_sync();
+#pragma unroll
+            for (int t = 0; t < R; ++t) rho[64 * t + lane] = 0.0;
+            h_wave_sync();
+#pragma unroll
+            for (int t = 0; t < R; ++t) {
+                uint64_t msk = __ballot(rv[t] != 0.0);
+                while (msk) {
+                    // up to 4 rows per group: their entries are loaded together
+                    int gi[4], gn[4], go[4], gc[4];
+                    double gr[4], gw[4];
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        gi[g] = -1; gn[g] = 0; go[g] = 0; gc[g] = 0; gr[g] = 0.0; gw[g] = 0.0;
+                        if (msk) {
+                            const int l = __builtin_ctzll(msk);
+                            msk &= msk - 1;
+                            gi[g] = 64 * t + l;
+                            gr[g] = readlane_dbl(rv[t], l);
+                            go[g] = P.wrptr[gi[g]];
+                            gn[g] = P.wrptr[gi[g] + 1] - go[g];
+                            if (lane < gn[g]) { gc[g] = P.wcol[go[g] + lane]; gw[g] = P.wval[go[g] + lane]; }
+                        }
+                    }
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        if (gi[g] < 0) break;
+                        if (lane < gn[g]) alpha[gc[g]] = fma(gr[g], gw[g], alpha[gc[g]]);
+                        for (int e = 64 + lane; e < gn[g]; e += 64) {
+                            const int cc = P.wcol[go[g] + e];
+                            alpha[cc] = fma(gr[g], P.wval[go[g] + e], alpha[cc]);
+                        }
+                        if (lane == 0) alpha[n + gi[g]] = gr[g];   // slack of row i: entry 1 in row i only
+                        nops += gn[g] + 1;
+                        h_wave_sync();
+                    }
                 }
-                return a;
-            };
+            }
+            STAMP(4)
+
+            // Harris ratio test over the nonbasic columns (d in registers, alpha~ from LDS)
             const double sg = delta > 0 ? 1.0 : -1.0;
             double thmax = INFINITY;
             uint64_t nzm = 0, elm = 0;
-            // per-lane register list of the first kLCap nonzero alpha~ (slot, value, d)
-            constexpr int kLCap = 6;
-            double lv[kLCap], ld[kLCap];
-            int ls[kLCap];
-            int lcnt = 0;
-#pragma unroll
-            for (int i = 0; i < kLCap; ++i) { lv[i] = 0.0; ld[i] = 0.0; ls[i] = -1; }
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 const uint64_t bit = 1ull << c;
                 if ((bmask | fixedm) & bit) continue;
-                const double a = sg * alpha_col(c);
-                if (a != 0.0) {
-                    nzm |= bit;
-#pragma unroll
-                    for (int i = 0; i < kLCap; ++i)
-                        if (i == lcnt) { lv[i] = a; ld[i] = d[c]; ls[i] = c; }
-                    ++lcnt;
-                }
+                const double a = sg * alpha[64 * c + lane];
+                if (a != 0.0) nzm |= bit;
                 const bool atlb = !(ubm & bit);
                 if (atlb ? a > HTOL_PIV : a < -HTOL_PIV) {
                     elm |= bit;
@@ -295,30 +321,20 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 }
             }
             thmax = wmin(thmax);
-            STAMP(4)
             if (thmax == INFINITY) {
                 status = TWOSD_LP_INFEASIBLE;
                 h_wave_sync();
 #pragma unroll
-                for (int t = 0; t < R; ++t) rho[64 * t + lane] = 0.0;
+                for (int c = 0; c < C; ++c) alpha[64 * c + lane] = 0.0;
                 break;
             }
             double bA = 0.0, bD = 0.0, bAs = 0.0;
             int bq = 0x7fffffff;
-            // eligible columns held in the list (slot order, so the scan order is unchanged)
 #pragma unroll
-            for (int i = 0; i < kLCap; ++i) {
-                if (ls[i] < 0 || !((elm >> ls[i]) & 1ull)) continue;
-                const double a = lv[i];
-                if (ld[i] / a <= thmax && fabs(a) > bA) { bA = fabs(a); bq = 64 * ls[i] + lane; bD = ld[i]; bAs = a; }
-            }
-            if (lcnt > kLCap) {   // rare overflow: slots past the list are recomputed
-#pragma unroll
-                for (int c = 0; c < C; ++c) {
-                    if (!(elm & (1ull << c)) || c <= ls[kLCap - 1]) continue;
-                    const double a = sg * alpha_col(c);
-                    if (d[c] / a <= thmax && fabs(a) > bA) { bA = fabs(a); bq = 64 * c + lane; bD = d[c]; bAs = a; }
-                }
+            for (int c = 0; c < C; ++c) {
+                if (!(elm & (1ull << c))) continue;
+                const double a = sg * alpha[64 * c + lane];
+                if (d[c] / a <= thmax && fabs(a) > bA) { bA = fabs(a); bq = 64 * c + lane; bD = d[c]; bAs = a; }
             }
             const ArgBest eq = warg_max(bA, bq, bD, bAs);
             const int q = eq.idx;
@@ -327,26 +343,18 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 status = TWOSD_LP_NUMERIC;
                 h_wave_sync();
 #pragma unroll
-                for (int t = 0; t < R; ++t) rho[64 * t + lane] = 0.0;
+                for (int c = 0; c < C; ++c) alpha[64 * c + lane] = 0.0;
                 break;
             }
             const double thetaD = eq.p0 / eq.p1;
-            // pass 3: d_j -= thetaD * alpha~_j for every nonbasic column with alpha_j != 0
+            // d_j -= thetaD * alpha~_j for every nonbasic column with alpha_j != 0
 #pragma unroll
-            for (int c = 0; c < C; ++c) {
-                if (!(nzm & (1ull << c))) continue;
-                double a = 0.0;
-                bool inlist = false;
-#pragma unroll
-                for (int i = 0; i < kLCap; ++i)
-                    if (ls[i] == c) { a = lv[i]; inlist = true; }
-                if (!inlist) a = sg * alpha_col(c);
-                d[c] = fma(-thetaD, a, d[c]);
-            }
+            for (int c = 0; c < C; ++c)
+                if (nzm & (1ull << c)) d[c] = fma(-thetaD, sg * alpha[64 * c + lane], d[c]);
             h_wave_sync();
 #pragma unroll
-            for (int t = 0; t < R; ++t) rho[64 * t + lane] = 0.0;   // rho is rebuilt by scatter next pivot
-            nops += P.wslot[C] * 64;
+            for (int c = 0; c < C; ++c) alpha[64 * c + lane] = 0.0;   // back to all-zero ut / rho
+            h_wave_sync();
             STAMP(6)
 
             // ---- 4. FTRAN: ut = E_K..E_1 B0^{-1} a_q (ut is all zeros here).  Column cc of
@@ -702,7 +710,7 @@ hipError_t launch_hyper(int R, int C, const HyperParams &p, int nblocks, size_t 
 }
 
 int hyper_max_blocks_per_cu(int R, int C, int kmax, int k) {
-    const size_t lds = hyper_lds_bytes(R, kmax, k);
+    const size_t lds = hyper_lds_bytes(R, C, kmax, k);
     switch (R) {
         case 1: HYPER_C_SWITCH(1, ho, lds); break;
         case 2: HYPER_C_SWITCH(2, ho, lds); break;

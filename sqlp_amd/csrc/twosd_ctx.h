@@ -71,13 +71,10 @@ struct twosd_ctx {
     bool use_hyper = true;
     int *d_kslot = nullptr, *d_kix = nullptr;
     double *d_kv = nullptr, *d_d0 = nullptr;
-    int *d_wslot = nullptr, *d_wix = nullptr, *d_bslot = nullptr, *d_bix = nullptr;
-    double *d_wv = nullptr, *d_bv = nullptr;
+    int *d_wrptr = nullptr, *d_wcol = nullptr, *d_bslot = nullptr, *d_bix = nullptr;
+    double *d_wval = nullptr, *d_bv = nullptr;
     int *d_brptr = nullptr, *d_brcol = nullptr;
     double *d_brval = nullptr;
-    bool has_pack4 = false;
-    unsigned long long *d_wrow4 = nullptr;
-    double *d_wval4 = nullptr;
     int *d_eidx = nullptr;
     double *d_evals = nullptr;
     size_t earena_slots = 0;

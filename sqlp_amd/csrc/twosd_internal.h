@@ -55,13 +55,10 @@ struct HyperParams {
     int m, n, k, N, kmax, ecap;
     const int *colptr, *rowidx; const double *val;      // W CSC
     const double *q; const int8_t *btype;
-    // sliced-ELL copies (entry e of slot s for lane l at [(slot_off[s] + e) * 64 + l]; padding: idx 0, val 0):
-    const int *wslot, *wix; const double *wv;           // columns of [W I], C slots (j = 64c + lane)
-    const int *bslot, *bix; const double *bv;           // columns of B0^{-1}, R slots (c = 64t + lane)
-    const int *brptr, *brcol; const double *brval;      // B0^{-1} CSR (MP rows)
-    // packed pricing (all columns of [W I] with <= 4 entries): rows of column 64c+l as four
-    // 16-bit fields of wrow4[c*64+l] (0xFFFF = none), values at wval4[(c*4+e)*64+l]; null if unused
-    const unsigned long long *wrow4; const double *wval4;
+    const int *wrptr, *wcol; const double *wval;        // W by rows (CSR, columns ascending)
+    // sliced ELL (entry e of slot s for lane l at [(slot_off[s] + e) * 64 + l]; padding: idx 0, val 0):
+    const int *bslot, *bix; const double *bv;           // columns of B^{-1}, R slots (c = 64t + lane)
+    const int *brptr, *brcol; const double *brval;      // B^{-1} CSR (MP rows)
     // per pool basis p, rows i = 64t + lane of coef_e B_p^{-1}[i][row_e] as sliced ELL (R slots,
     // kslot pool-strided npool x (R+1), absolute into the concatenated kix (= e) / kv)
     const int *kslot, *kix; const double *kv;           // values B_p^{-1}[i][row_e] (x-independent)
@@ -97,7 +94,7 @@ struct PoolSelParams {
 };
 size_t pool_select_lds_bytes(int k);
 hipError_t launch_pool_select(const PoolSelParams &p, hipStream_t s);
-size_t hyper_lds_bytes(int R, int kmax, int k);
+size_t hyper_lds_bytes(int R, int C, int kmax, int k);
 int hyper_rows_per_lane(int m);
 int hyper_cols_per_lane(int ncols);
 hipError_t launch_hyper(int R, int C, const HyperParams &p, int nblocks, size_t lds, hipStream_t s);

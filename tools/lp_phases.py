@@ -30,6 +30,11 @@ def main():
     ctx = twosd.SDContext(sp2, sto)
     ctx.compute_basis(x, smps.mean_values(sto))
     vals = smps.sample_values(sto, N, np.random.default_rng(1))
+    pool = int(os.environ.get("POOL", "1"))
+    if pool > 1:
+        tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+        twosd.add_scenarios(tr, smps.sample_values(sto, 16384, np.random.default_rng(99)))
+        ctx.pool_build(tr, x, 0, 16384, pool)
     ctx.solve_values(x, vals[:1024], want_pi=False)
     st = np.zeros(10, dtype=np.uint64)
     ctx.lib.twosd_debug_stamps(ctx.h, st.ctypes.data_as(C.c_void_p), 1)
