@@ -268,36 +268,43 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
 #pragma unroll
             for (int t = 0; t < R; ++t) rho[64 * t + lane] = 0.0;
             h_wave_sync();
+            // W rows as row-ELL of width WR <= 64 (padding column -1): one load round trip serves
+            // a group of 8 rows.  A row longer than 64 keeps 63 entries here; slot 63 holds
+            // column -2 - o and value n_rest: its remaining entries sit in an overflow CSR at o.
+            const int WR = P.wr_width;
 #pragma unroll
             for (int t = 0; t < R; ++t) {
                 uint64_t msk = __ballot(rv[t] != 0.0);
                 while (msk) {
-                    // up to 4 rows per group: their entries are loaded together
-                    int gi[4], gn[4], go[4], gc[4];
-                    double gr[4], gw[4];
+                    constexpr int G = 8;
+                    int gi[G], gc[G];
+                    double gr[G], gw[G];
 #pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        gi[g] = -1; gn[g] = 0; go[g] = 0; gc[g] = 0; gr[g] = 0.0; gw[g] = 0.0;
+                    for (int g = 0; g < G; ++g) {
+                        gi[g] = -1; gc[g] = -1; gr[g] = 0.0; gw[g] = 0.0;
                         if (msk) {
                             const int l = __builtin_ctzll(msk);
                             msk &= msk - 1;
                             gi[g] = 64 * t + l;
                             gr[g] = readlane_dbl(rv[t], l);
-                            go[g] = P.wrptr[gi[g]];
-                            gn[g] = P.wrptr[gi[g] + 1] - go[g];
-                            if (lane < gn[g]) { gc[g] = P.wcol[go[g] + lane]; gw[g] = P.wval[go[g] + lane]; }
+                            if (lane < WR) { gc[g] = P.wr_col[(size_t)gi[g] * WR + lane]; gw[g] = P.wr_val[(size_t)gi[g] * WR + lane]; }
                         }
                     }
 #pragma unroll
-                    for (int g = 0; g < 4; ++g) {
+                    for (int g = 0; g < G; ++g) {
                         if (gi[g] < 0) break;
-                        if (lane < gn[g]) alpha[gc[g]] = fma(gr[g], gw[g], alpha[gc[g]]);
-                        for (int e = 64 + lane; e < gn[g]; e += 64) {
-                            const int cc = P.wcol[go[g] + e];
-                            alpha[cc] = fma(gr[g], P.wval[go[g] + e], alpha[cc]);
+                        if (gc[g] >= 0) alpha[gc[g]] = fma(gr[g], gw[g], alpha[gc[g]]);
+                        if (__ballot(gc[g] < -1)) {   // long row (rare): the rest, columns ascending
+                            const int o = -2 - __builtin_amdgcn_readlane(gc[g], 63);
+                            const int nr = (int)readlane_dbl(gw[g], 63);
+                            h_wave_sync();
+                            for (int e = lane; e < nr; e += 64) {
+                                const int cc = P.wr_ocol[o + e];
+                                alpha[cc] = fma(gr[g], P.wr_oval[o + e], alpha[cc]);
+                            }
                         }
                         if (lane == 0) alpha[n + gi[g]] = gr[g];   // slack of row i: entry 1 in row i only
-                        nops += gn[g] + 1;
+                        nops += WR + 1;
                         h_wave_sync();
                     }
                 }

@@ -71,8 +71,11 @@ struct twosd_ctx {
     bool use_hyper = true;
     int *d_kslot = nullptr, *d_kix = nullptr;
     double *d_kv = nullptr, *d_d0 = nullptr;
-    int *d_wrptr = nullptr, *d_wcol = nullptr, *d_bslot = nullptr, *d_bix = nullptr;
-    double *d_wval = nullptr, *d_bv = nullptr;
+    int wr_width = 1;             // W row-ELL width (max row length)
+    int *d_wr_col = nullptr, *d_bslot = nullptr, *d_bix = nullptr;
+    double *d_wr_val = nullptr, *d_bv = nullptr;
+    int *d_wr_ocol = nullptr;
+    double *d_wr_oval = nullptr;
     int *d_brptr = nullptr, *d_brcol = nullptr;
     double *d_brval = nullptr;
     int *d_eidx = nullptr;

@@ -55,7 +55,9 @@ struct HyperParams {
     int m, n, k, N, kmax, ecap;
     const int *colptr, *rowidx; const double *val;      // W CSC
     const double *q; const int8_t *btype;
-    const int *wrptr, *wcol; const double *wval;        // W by rows (CSR, columns ascending)
+    int wr_width;                                       // W by rows as row-ELL (columns ascending, width
+    const int *wr_col; const double *wr_val;            //   min(max row length, 64), padding column -1);
+    const int *wr_ocol; const double *wr_oval;          //   long rows continue in an overflow CSR
     // sliced ELL (entry e of slot s for lane l at [(slot_off[s] + e) * 64 + l]; padding: idx 0, val 0):
     const int *bslot, *bix; const double *bv;           // columns of B^{-1}, R slots (c = 64t + lane)
     const int *brptr, *brcol; const double *brval;      // B^{-1} CSR (MP rows)
