@@ -82,12 +82,18 @@ __device__ __forceinline__ int h_get_row_i(const int (&a)[R], int p) {
 // per-wave LDS slice: a union of {ut, rho} (MP doubles each) and alpha (64C doubles, the
 // pivot row over all columns during pricing), the scenario deltas (k doubles), etap (u16),
 // etaoff (int)
-static __host__ __device__ inline int hyper_union_doubles(int R, int C) { return 128 * R > 64 * C ? 128 * R : 64 * C; }
-static __host__ __device__ inline size_t hyper_slice_bytes(int R, int C, int kmax, int k) {
-    const int kmaxp = (kmax + 3) & ~3;
-    return 8 * (size_t)hyper_union_doubles(R, C) + 8 * (size_t)((k + 1) & ~1) + 2 * kmaxp + 4 * (kmaxp + 4);
+// (alpha spans the ncol = n + m real columns), the scenario deltas (k doubles), the dual
+// Devex weights (MP floats), etap (u16), etaoff (int)
+static __host__ __device__ inline int hyper_union_doubles(int R, int ncol) {
+    const int a = (ncol + 1) & ~1;
+    return 128 * R > a ? 128 * R : a;
 }
-size_t hyper_lds_bytes(int R, int C, int kmax, int k) { return (size_t)kWavesPerBlock * hyper_slice_bytes(R, C, kmax, k); }
+static __host__ __device__ inline size_t hyper_slice_bytes(int R, int ncol, int kmax, int k) {
+    const int kmaxp = (kmax + 3) & ~3;
+    return 8 * (size_t)hyper_union_doubles(R, ncol) + 8 * (size_t)((k + 1) & ~1) + 4 * (size_t)(64 * R) + 2 * kmaxp +
+           4 * (kmaxp + 4);
+}
+size_t hyper_lds_bytes(int R, int ncol, int kmax, int k) { return (size_t)kWavesPerBlock * hyper_slice_bytes(R, ncol, kmax, k); }
 
 // min waves per SIMD (VGPR budget 256 / 168): measured on MI355X, storm (R=9) is fastest
 // at 2 waves/SIMD, ssn (R=4) at 3 (tools/lp_speed.py)
@@ -101,12 +107,14 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
     const int wid = threadIdx.x >> 6;
     constexpr int MP = 64 * R;
     const int kmaxp = (P.kmax + 3) & ~3;
-    char *slice = reinterpret_cast<char *>(lds_raw) + (size_t)wid * hyper_slice_bytes(R, C, P.kmax, P.k);
+    const int ncol = P.n + P.m;
+    char *slice = reinterpret_cast<char *>(lds_raw) + (size_t)wid * hyper_slice_bytes(R, ncol, P.kmax, P.k);
     double *ut = reinterpret_cast<double *>(slice);        // dense scratch vector (u, then alpha_q)
     double *rho = ut + MP;                                  // pivot row of B^{-1}
     double *alpha = ut;                                     // pricing: alpha~_j over the same space
-    double *dvl = ut + hyper_union_doubles(R, C);           // this scenario's coef_e(x) dv_e
-    unsigned short *etap = reinterpret_cast<unsigned short *>(dvl + ((P.k + 1) & ~1));
+    double *dvl = ut + hyper_union_doubles(R, ncol);        // this scenario's coef_e(x) dv_e
+    float *w = reinterpret_cast<float *>(dvl + ((P.k + 1) & ~1));   // dual Devex weights (row i at w[i])
+    unsigned short *etap = reinterpret_cast<unsigned short *>(w + MP);
     int *etaoff = reinterpret_cast<int *>(etap + kmaxp);
 
     const int m = P.m, n = P.n;
@@ -116,7 +124,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
     const uint64_t fixedm = P.fixedmask[lane];
     const uint64_t ubm = P.ubmask[lane];
 
-    for (int j = lane; j < hyper_union_doubles(R, C); j += 64) ut[j] = 0.0;
+    for (int j = lane; j < hyper_union_doubles(R, ncol); j += 64) ut[j] = 0.0;
     h_wave_sync();
     STAMP_DECL
 
@@ -142,7 +150,6 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         // warm-start basis: chosen per scenario by pool_select_kernel (0 without a pool)
         int pb = P.npool > 1 ? __builtin_amdgcn_readfirstlane(P.pool_pick[s]) : 0;
         double xB[R];
-        float w[R];
         int hb[R];
         double d[C];
         uint64_t bmask;
@@ -159,7 +166,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         for (int t = 0; t < R; ++t) {
             xB[t] = xb_row(pb, t);
             hb[t] = P.hb0[(size_t)pb * MP + 64 * t + lane];
-            w[t] = 1.0f;
+            w[64 * t + lane] = 1.0f;
         }
 #pragma unroll
         for (int c = 0; c < C; ++c) d[c] = P.d0[(size_t)pb * 64 * C + 64 * c + lane];
@@ -179,7 +186,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 if (hb[t] < 0) continue;
                 const double dl = h_infeas(xB[t], hb[t] & 3);
                 if (dl != 0.0) {
-                    const double sc = dl * dl / (double)w[t];
+                    const double sc = dl * dl / (double)w[64 * t + lane];
                     if (sc > best) { best = sc; br = 64 * t + lane; bdel = dl; }
                 }
             }
@@ -332,7 +339,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 status = TWOSD_LP_INFEASIBLE;
                 h_wave_sync();
 #pragma unroll
-                for (int c = 0; c < C; ++c) alpha[64 * c + lane] = 0.0;
+                for (int c = 0; c < C; ++c) if (64 * c + lane < ncol) alpha[64 * c + lane] = 0.0;
                 break;
             }
             double bA = 0.0, bD = 0.0, bAs = 0.0;
@@ -350,7 +357,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 status = TWOSD_LP_NUMERIC;
                 h_wave_sync();
 #pragma unroll
-                for (int c = 0; c < C; ++c) alpha[64 * c + lane] = 0.0;
+                for (int c = 0; c < C; ++c) if (64 * c + lane < ncol) alpha[64 * c + lane] = 0.0;
                 break;
             }
             const double thetaD = eq.p0 / eq.p1;
@@ -360,7 +367,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 if (nzm & (1ull << c)) d[c] = fma(-thetaD, sg * alpha[64 * c + lane], d[c]);
             h_wave_sync();
 #pragma unroll
-            for (int c = 0; c < C; ++c) alpha[64 * c + lane] = 0.0;   // back to all-zero ut / rho
+            for (int c = 0; c < C; ++c) if (64 * c + lane < ncol) alpha[64 * c + lane] = 0.0;   // back to all-zero ut / rho
             h_wave_sync();
             STAMP(6)
 
@@ -428,15 +435,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             // ---- 5. updates: primal, Devex, sparse eta, basis, reduced costs of q / leaving
             const double thetaP = delta / arq;
             const double inv_arq = 1.0 / arq;
-            float wrr = 0.0f;
-            {
-                const int slot = r >> 6;
-                float v = w[0];
-#pragma unroll
-                for (int t = 1; t < R; ++t)
-                    if (t == slot) v = w[t];
-                wrr = __shfl(v, r & 63);
-            }
+            const float wrr = w[r];
             int cnt = 0;
 #pragma unroll
             for (int t = 0; t < R; ++t) cnt += __popcll(__ballot(col[t] != 0.0));
@@ -455,11 +454,12 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                     if (i == r) {
                         xB[t] = thetaP;
                         const float nw = (float)((double)wrr * inv_arq * inv_arq);
-                        w[t] = nw > 1.0f ? nw : 1.0f;
+                        w[i] = nw > 1.0f ? nw : 1.0f;
                     } else {
                         xB[t] = fma(-thetaP, col[t], xB[t]);
                         const float cand = (float)(ratio * ratio * (double)wrr);
-                        w[t] = cand > w[t] ? cand : w[t];
+                        const float wo = w[i];
+                        w[i] = cand > wo ? cand : wo;
                     }
                 }
                 base += __popcll(bal);
@@ -716,8 +716,8 @@ hipError_t launch_hyper(int R, int C, const HyperParams &p, int nblocks, size_t 
     return hipErrorInvalidValue;
 }
 
-int hyper_max_blocks_per_cu(int R, int C, int kmax, int k) {
-    const size_t lds = hyper_lds_bytes(R, C, kmax, k);
+int hyper_max_blocks_per_cu(int R, int C, int ncol, int kmax, int k) {
+    const size_t lds = hyper_lds_bytes(R, ncol, kmax, k);
     switch (R) {
         case 1: HYPER_C_SWITCH(1, ho, lds); break;
         case 2: HYPER_C_SWITCH(2, ho, lds); break;

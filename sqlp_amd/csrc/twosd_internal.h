@@ -96,11 +96,11 @@ struct PoolSelParams {
 };
 size_t pool_select_lds_bytes(int k);
 hipError_t launch_pool_select(const PoolSelParams &p, hipStream_t s);
-size_t hyper_lds_bytes(int R, int C, int kmax, int k);
+size_t hyper_lds_bytes(int R, int ncol, int kmax, int k);   // ncol = n + m
 int hyper_rows_per_lane(int m);
 int hyper_cols_per_lane(int ncols);
 hipError_t launch_hyper(int R, int C, const HyperParams &p, int nblocks, size_t lds, hipStream_t s);
-int hyper_max_blocks_per_cu(int R, int C, int kmax, int k);
+int hyper_max_blocks_per_cu(int R, int C, int ncol, int kmax, int k);
 
 int lp_rows_per_lane(int m);   // supported R for m, or -1
 hipError_t launch_lp(int R, const LpParams &p, int nblocks, size_t lds_bytes, hipStream_t s);
