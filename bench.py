@@ -141,7 +141,7 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier()
-    t_lp = t_dd = t_cut = t_fin = 0.0
+    t_lp = t_dd = t_cut = t_fin = t_sel = 0.0
     flops_lp = 0.0
     piv_sum = 0
     piv_max = 0
@@ -149,7 +149,7 @@ def main():
     for _ in range(args.steps):
         alpha = step()
         tm = ctx.timings_us()
-        t_lp += tm[0]; t_dd += tm[1]; t_cut += tm[2]; t_fin += tm[3]
+        t_lp += tm[0]; t_dd += tm[1]; t_cut += tm[2]; t_fin += tm[3]; t_sel += tm[4]
         flops_lp += ctx.lp_flops()
         ps, pm = ctx.lp_stats()
         piv_sum += ps; piv_max = max(piv_max, pm)
@@ -193,10 +193,10 @@ def main():
                    "instance": name, "scenarios": N, "vertices": nv, "k": k, "m2": m,
                    "basis_pool": pool_size, "pool_build_s": round(t_pool, 3),
                    "parallelism": f"scenario-dp{world}"},
-        "phases_ms_per_step": {"lp_kernel": lp_us / 1e3, "dedup": t_dd / K / 1e3, "cut_partial": cut_us / 1e3,
+        "phases_ms_per_step": {"pool_select": t_sel / K / 1e3, "lp_kernel": lp_us / 1e3, "dedup": t_dd / K / 1e3, "cut_partial": cut_us / 1e3,
                                "cut_finalize": t_fin / K / 1e3},
         "lp_pivots_mean": piv_sum / (K * n_local), "lp_pivots_max": piv_max,
-        "roofline": {"kernel": "lp_dual_simplex_kernel", "bound": "mfma",
+        "roofline": {"kernel": "lp_hyper_kernel", "bound": "mfma",
                      "note": "fp64 peak (vector == matrix on gfx950); achieved = counted fp64 FLOPs of the executed pivot path / LP kernel time",
                      "achieved": lp_tflops, "peak": PEAK_FP64_TFS, "unit": "TFLOP/s",
                      "frac": lp_tflops / PEAK_FP64_TFS, "traffic": None},

@@ -174,8 +174,9 @@ int twosd_cut_finalize(twosd_ctx *ctx, const double *x, const uint64_t *d_hist_u
                        double *alpha, double *beta);
 
 /* Timing of the last kernel phases on the context's stream (HIP events), microseconds:
- * [0] LP batch, [1] dedup push, [2] argmax+cut partial, [3] cut finalize. */
-int twosd_last_timings(twosd_ctx *ctx, double *us4);
+ * [0] LP kernel, [1] dedup push, [2] argmax+cut partial, [3] cut finalize,
+ * [4] warm-start pool selection of the last LP batch (0 without a pool). */
+int twosd_last_timings(twosd_ctx *ctx, double *us5);
 
 /* Statistics of the last LP batch: sum of simplex pivots, max pivots. */
 int twosd_last_lp_stats(twosd_ctx *ctx, int64_t *pivots_sum, int *pivots_max);

@@ -877,12 +877,15 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
             S.pick = c->d_pool_pick;
             HIPCHK(launch_pool_select(S, c->stream));
         }
+        HIPCHK(hipEventRecord(c->ev[2], c->stream));
         HIPCHK(launch_hyper(R, CH, H, nblocks, hyper_lds_bytes(R, n + m, kmax, c->k), c->stream));
         HIPCHK(hipEventRecord(c->ev[1], c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
-        float ms = 0;
-        hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
+        float ms = 0, ms_sel = 0;
+        hipEventElapsedTime(&ms, c->ev[2], c->ev[1]);
+        hipEventElapsedTime(&ms_sel, c->ev[0], c->ev[2]);
         c->t_us[0] = 1e3 * ms;
+        c->t_us[4] = 1e3 * ms_sel;
         c->last_lp_N = N;
         c->last_lp_blocks = nblocks;
         c->last_ops_width = 1;
@@ -915,6 +918,7 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
     float ms = 0;
     hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
     c->t_us[0] = 1e3 * ms;
+    c->t_us[4] = 0.0;
     c->last_lp_N = N;
     c->last_lp_blocks = nblocks;
     return TWOSD_OK;
@@ -970,9 +974,9 @@ extern "C" int twosd_solve_values(twosd_ctx *c, const double *x, int N, const do
     return copy_lp_outputs(c, N, obj, pi, y, status);
 }
 
-extern "C" int twosd_last_timings(twosd_ctx *c, double *us4) {
-    if (!c || !us4) return fail(TWOSD_E_ARG, "last_timings: NULL");
-    for (int i = 0; i < 4; ++i) us4[i] = c->t_us[i];
+extern "C" int twosd_last_timings(twosd_ctx *c, double *us5) {
+    if (!c || !us5) return fail(TWOSD_E_ARG, "last_timings: NULL");
+    for (int i = 0; i < 5; ++i) us5[i] = c->t_us[i];
     return TWOSD_OK;
 }
 

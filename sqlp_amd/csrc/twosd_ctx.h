@@ -35,7 +35,7 @@ struct twosd_ctx {
     hipEvent_t ev[8] = {};
     int num_cus = 256;
     int kmax_override = 0;
-    double t_us[4] = {0, 0, 0, 0};
+    double t_us[5] = {0, 0, 0, 0, 0};   // LP kernel, dedup, cut partial, cut finalize, pool select
     // template
     bool has_template = false, has_basis = false;
     twosd::HostLP L;              // W CSC, q, sense (host)

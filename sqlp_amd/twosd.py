@@ -165,7 +165,8 @@ class SDContext:
         return v
 
     def timings_us(self):
-        t = np.zeros(4)
+        """[LP kernel, dedup, cut partial, cut finalize, pool selection] of the last calls."""
+        t = np.zeros(5)
         check(self.lib.twosd_last_timings(self.h, ptr(t)))
         return t
 

@@ -1,0 +1,80 @@
+"""Summarise one profile_round.sh run into profiles/<tag>/pmc_summary.json.
+
+Usage: python tools/pmc_summarize.py <gpurun_out/tag> <profiles/tag> <scenarios>
+
+Reads the rocprofv3 kernel trace (trace/run_kernel_trace.csv, stats copied alongside) and
+the two separate PMC passes (pmc_fetch, pmc_write: FETCH_SIZE / WRITE_SIZE in KiB per
+dispatch) and writes, per kernel of the hot path, for its LARGEST dispatch (the full
+1M-scenario launch; setup launches such as the pool build and the |V| pool are smaller):
+duration, PMC bytes per launch (the gfx950 correction
+of MI355X_MICROARCH.md: hbm_bytes = 1024 * (2 * FETCH_SIZE + WRITE_SIZE), an upper
+estimate for narrow accesses), scratch bytes per lane.  Also copies the CSVs it used.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+KERNELS = ["lp_hyper_kernel", "pool_select_kernel", "cut_argmax_kernel", "cut_fixup_kernel", "cut_vbase_kernel",
+           "cut_pk_kernel", "dvs_batch_kernel", "dvs_lookup_kernel", "dvs_assign_kernel"]
+
+
+def short(name):
+    for k in KERNELS:
+        if k in name:
+            return k
+    return None
+
+
+def main():
+    src, dst, scen = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    os.makedirs(dst, exist_ok=True)
+    stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    dur = {}
+    if stats:
+        shutil.copy(stats[0], os.path.join(dst, "kernel_stats.csv"))
+    traces = glob.glob(os.path.join(src, "trace", "**", "*kernel_trace.csv"), recursive=True)
+    if traces:
+        for r in csv.DictReader(open(traces[0])):
+            k = short(r["Kernel_Name"])
+            if k:
+                d = (float(r["End_Timestamp"]) - float(r["Start_Timestamp"])) / 1e6
+                dur[k] = max(dur.get(k, 0.0), d)
+    pmc = defaultdict(lambda: defaultdict(list))
+    scratch = {}
+    for tag in ("pmc_fetch", "pmc_write"):
+        fs = glob.glob(os.path.join(src, tag, "**", "*counter_collection.csv"), recursive=True)
+        if not fs:
+            continue
+        shutil.copy(fs[0], os.path.join(dst, f"{tag}.csv"))
+        for r in csv.DictReader(open(fs[0])):
+            k = short(r["Kernel_Name"])
+            if k:
+                pmc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                scratch[k] = int(float(r["Scratch_Size"]))
+    out = {"workload": f"storm {scen} scenarios, bench.py defaults, 1 MI355X",
+           "source": "rocprofv3 --kernel-trace --stats; separate --pmc FETCH_SIZE / --pmc WRITE_SIZE passes (tools/profile_round.sh)",
+           "correction": "FETCH_SIZE/WRITE_SIZE are KiB; gfx950 FETCH_SIZE counts 1/2 of wide coalesced reads, so "
+                         "hbm_bytes = 1024*(2*FETCH_SIZE + WRITE_SIZE) (upper estimate for narrow accesses)",
+           "scenarios": scen, "kernels": {}}
+    for k in KERNELS:
+        c = pmc.get(k)
+        if not c and k not in dur:
+            continue
+        e = {"duration_ms": dur.get(k)}
+        if c:
+            f = max(c.get("FETCH_SIZE", [0.0]))
+            w = max(c.get("WRITE_SIZE", [0.0]))
+            e.update({"FETCH_SIZE_KiB": f, "WRITE_SIZE_KiB": w, "hbm_bytes_per_launch": 1024.0 * (2 * f + w),
+                      "scratch_bytes_per_lane": scratch.get(k)})
+        out["kernels"][k] = e
+    with open(os.path.join(dst, "pmc_summary.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
