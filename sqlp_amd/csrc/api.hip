@@ -136,7 +136,7 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_xbase); dfree(c->d_B0K); dfree(c->d_eta); dfree(c->d_queue);
     dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_ops);
     dfree(c->d_dvtmp);
-    dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); dfree(c->d_sel_val); dfree(c->d_head_out); dfree(c->d_pool_pick); c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
+    dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); dfree(c->d_sel_val); dfree(c->d_head_out); dfree(c->d_pool_pick); dfree(c->d_order); dfree(c->d_sort_tmp); c->order_cap = 0; c->sort_tmp_bytes = 0; c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
     dfree(c->d_kslot); dfree(c->d_kix); dfree(c->d_kv); dfree(c->d_kcoef); c->k_valid = false;
     dfree(c->d_d0); dfree(c->d_eidx); dfree(c->d_evals); dfree(c->d_stamps);
     dfree(c->d_wr_col); dfree(c->d_wr_val); dfree(c->d_wr_ocol); dfree(c->d_wr_oval); dfree(c->d_bslot); dfree(c->d_bix); dfree(c->d_bv);
@@ -876,6 +876,15 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
             S.cinf = c->d_sel_cinf; S.sptr = c->d_sel_ptr; S.code = c->d_sel_code; S.val = c->d_sel_val;
             S.pick = c->d_pool_pick;
             HIPCHK(launch_pool_select(S, c->stream));
+            size_t tb = 0;
+            HIPCHK(sort_by_pool(c->d_pool_pick, nullptr, N, H.npool, nullptr, &tb, c->stream));
+            if ((size_t)N > c->order_cap || tb > c->sort_tmp_bytes) {
+                if ((rc = dalloc(&c->d_order, (size_t)N)) || (rc = dalloc(&c->d_sort_tmp, tb))) return rc;
+                c->order_cap = N;
+                c->sort_tmp_bytes = tb;
+            }
+            HIPCHK(sort_by_pool(c->d_pool_pick, c->d_order, N, H.npool, c->d_sort_tmp, &tb, c->stream));
+            H.order = c->d_order;
         }
         HIPCHK(hipEventRecord(c->ev[2], c->stream));
         HIPCHK(launch_hyper(R, CH, H, nblocks, hyper_lds_bytes(R, n + m, kmax, c->k), c->stream));

@@ -133,6 +133,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         if (lane == 0) s = atomicAdd(P.queue, 1);
         s = __builtin_amdgcn_readfirstlane(__shfl(s, 0));
         if (s >= P.N) break;
+        if (P.order) s = __builtin_amdgcn_readfirstlane(P.order[s]);   // grouped by pool basis
 
         const double *dvs = P.dv + (size_t)s * P.k;
         for (int e = lane; e < P.k; e += 64) dvl[e] = P.kcoef[e] * dvs[e];   // coef_e(x) dv_e

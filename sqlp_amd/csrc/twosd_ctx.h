@@ -61,6 +61,9 @@ struct twosd_ctx {
     int *d_bnnz = nullptr;        // npool: nnz of each pool B^{-1} (FMA accounting)
     int *d_head_out = nullptr, *d_pool_pick = nullptr;   // optional LP outputs (pool building)
     size_t head_cap = 0, pick_cap = 0;
+    int *d_order = nullptr;       // LP visiting order grouped by pool basis
+    char *d_sort_tmp = nullptr;
+    size_t order_cap = 0, sort_tmp_bytes = 0;
     bool want_head = false;
     bool prep_valid = false;
     bool k_valid = false;         // K rows / ELL of the pool (depend on the pool and the positions)

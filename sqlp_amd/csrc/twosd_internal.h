@@ -82,6 +82,7 @@ struct HyperParams {
     const int *bnnz;                                    // npool: nnz of B^{-1} (ops accounting)
     int *head_out;                                      // N x m final basis (nullable)
     int *pool_pick;                                     // N pool basis per scenario (in; npool > 1)
+    const int *order;                                   // N visiting order of the scenarios (nullable)
 };
 
 // warm-start selection over the basis pool (pool_select_kernel in lp_hyper.hip)
@@ -95,6 +96,8 @@ struct PoolSelParams {
     int *pick;                                          // N out
 };
 size_t pool_select_lds_bytes(int k);
+// stable sort of scenarios [0, N) by pool pick -> order (pool_sort.hip); tmp == nullptr: size query
+hipError_t sort_by_pool(const int *pick, int *order, int N, int npool, void *tmp, size_t *tmp_bytes, hipStream_t s);
 hipError_t launch_pool_select(const PoolSelParams &p, hipStream_t s);
 size_t hyper_lds_bytes(int R, int ncol, int kmax, int k);   // ncol = n + m
 int hyper_rows_per_lane(int m);
