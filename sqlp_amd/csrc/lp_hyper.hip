@@ -594,23 +594,24 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
 // wave-uniform, so it streams through scalar loads and the per-lane work is LDS reads +
 // FMAs.  Key: total primal infeasibility sum_i |infeas(x_B,i)| at b_w (constant rows
 // precomputed in cinf); ties: lowest p.
-__global__ void __launch_bounds__(256) pool_select_kernel(PoolSelParams S) {
+constexpr int kSelWaves = 16;   // 16 waves share one staged 64-scenario tile (latency hiding)
+__global__ void __launch_bounds__(64 * kSelWaves) pool_select_kernel(PoolSelParams S) {
     extern __shared__ double dvt[];   // k x 65 (padded)
-    __shared__ double bsum[kWavesPerBlock][64];
-    __shared__ int bidx[kWavesPerBlock][64];
+    __shared__ double bsum[kSelWaves][64];
+    __shared__ int bidx[kSelWaves][64];
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar stream loads
     const int s0 = blockIdx.x * 64;
     const int k = S.k;
     const int ns = min(64, S.N - s0);
-    for (int idx = threadIdx.x; idx < 64 * k; idx += 256) {
+    for (int idx = threadIdx.x; idx < 64 * k; idx += 64 * kSelWaves) {
         const int sl = idx / k, e = idx - sl * k;
         dvt[e * 65 + sl] = sl < ns ? S.kcoef[e] * S.dv[(size_t)s0 * k + idx] : 0.0;
     }
     __syncthreads();
     double best = INFINITY;
     int bp = 0;
-    for (int p = wid; p < S.npool; p += kWavesPerBlock) {
+    for (int p = wid; p < S.npool; p += kSelWaves) {
         // one flat, wave-uniform stream per basis: a row-start record (code -1 - bound type,
         // value xbase_i) followed by the row's entries (code e, value coef_e B^{-1}[i][row_e]);
         // no load depends on the loop state, so the stream pipelines through the scalar cache
@@ -651,7 +652,7 @@ __global__ void __launch_bounds__(256) pool_select_kernel(PoolSelParams S) {
     bidx[wid][lane] = bp;
     __syncthreads();
     if (wid == 0 && lane < ns) {
-        for (int w = 1; w < kWavesPerBlock; ++w) {
+        for (int w = 1; w < kSelWaves; ++w) {
             const double v = bsum[w][lane];
             const int pw = bidx[w][lane];
             if (v < best || (v == best && pw < bp)) { best = v; bp = pw; }
@@ -665,7 +666,7 @@ size_t pool_select_lds_bytes(int k) { return (size_t)8 * 65 * (size_t)std::max(k
 hipError_t launch_pool_select(const PoolSelParams &p, hipStream_t s) {
     if (p.N <= 0) return hipSuccess;
     const int nb = (p.N + 63) / 64;
-    hipLaunchKernelGGL(pool_select_kernel, dim3(nb), dim3(256), pool_select_lds_bytes(p.k), s, p);
+    hipLaunchKernelGGL(pool_select_kernel, dim3(nb), dim3(64 * kSelWaves), pool_select_lds_bytes(p.k), s, p);
     return hipGetLastError();
 }
 
