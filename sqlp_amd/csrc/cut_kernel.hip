@@ -35,6 +35,7 @@ namespace twosd {
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int kVT = 32;            // vertices per LDS chunk (2 MFMA column tiles)
+constexpr int kCutTile = 64;       // scenarios per block tile (4 waves x one MFMA row tile of 16)
 constexpr int kLdsStride = 48;     // doubles per k-row in LDS (== 16 mod 32: conflict-free b64 reads)
 constexpr double kFix = 4611686018427387904.0;   // 2^62 fixed-point scale of p_w
 
@@ -80,96 +81,131 @@ __global__ void __launch_bounds__(256) cut_vbase_kernel(int nv, int m, const dou
 
 __device__ __forceinline__ double tolf(double M, double rel) { return rel * (1.0 + fabs(M)); }
 
+// Running (max, argmax) of one scenario row over the vertices one lane sees, in increasing
+// vertex order: M = max so far, I = lowest vertex within tolf(M) of M, SV = its score,
+// F = the exact rule cannot be decided from this state (left to cut_fixup_kernel).
+struct RowBest { double M, SV; int I, F; };
+
+__device__ __forceinline__ void row_update(RowBest &b, double s, int v, double rel) {
+    if (s == -INFINITY) return;
+    if (b.M == -INFINITY || s > b.M + tolf(b.M, rel)) {
+        // a new max beyond the old band; if the old candidate still lies within the new
+        // band the lowest-index rule would keep it -> flag (rare: scores 1e-12 apart)
+        if (b.M != -INFINITY && b.SV >= s - tolf(s, rel)) b.F = 1;
+        b.M = s; b.I = v; b.SV = s;
+    } else if (s > b.M) {
+        // max slides up inside the band: the candidate must stay within the new band
+        if (!(b.SV >= s - tolf(s, rel))) b.F = 1;
+        b.M = s;
+    }
+    // s within the band but not above M: a later (higher) index never wins
+}
+
 template <int KB>
-__global__ void __launch_bounds__(256) cut_argmax_kernel(CutParams P) {
+__global__ void __launch_bounds__(256, 2) cut_argmax_kernel(CutParams P) {
     __shared__ double Bs[4 * KB * kLdsStride];
     __shared__ double bs[kVT];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const int g = lane >> 4, j = lane & 15;
-    const int ntiles = (P.N + 63) / 64;
+    const int ntiles = (P.N + kCutTile - 1) / kCutTile;
     const int nchunks = (P.nv + kVT - 1) / kVT;
     // per-wave partial sums (lanes stride over elements)
     double pv_sum = 0.0;
     double Sacc[2] = {0.0, 0.0};
 
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int s0 = tile * 64 + wid * 16;
-        // A fragments: lane holds DR[s0 + j][4kb + g] * coef
-        double a[KB];
-        {
-            const int s = s0 + j;
+        // this wave: scenarios s0 .. s0+15 as one 16-row MFMA A tile
+        const int s0 = tile * kCutTile + wid * 16;
+        double a0[KB];
 #pragma unroll
-            for (int kb = 0; kb < KB; ++kb) {
-                const int e = 4 * kb + g;
-                a[kb] = (s < P.N && e < P.k) ? P.dv[(size_t)s * P.k + e] * P.coef[e] : 0.0;
-            }
+        for (int kb = 0; kb < KB; ++kb) {
+            const int e = 4 * kb + g;
+            const int sa = s0 + j;
+            a0[kb] = (sa < P.N && e < P.k) ? P.dv[(size_t)sa * P.k + e] * P.coef[e] : 0.0;
         }
-        double M[4], SV[4];
-        int I[4], F[4];
+        // lane (g, j) tracks rows g + 4r over the vertex columns j, 16 + j of every chunk
+        // (its own increasing vertex subsequence); lanes are combined once at the end
+        RowBest rb[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) { M[r] = -INFINITY; SV[r] = -INFINITY; I[r] = -1; F[r] = 0; }
+        for (int r = 0; r < 4; ++r) { rb[r].M = -INFINITY; rb[r].SV = -INFINITY; rb[r].I = -1; rb[r].F = 0; }
 
+        // chunk staging is software-pipelined: chunk ch+1 is loaded into registers while
+        // the MFMAs of chunk ch run, then written to LDS
+        constexpr int NPRE = (4 * KB * kVT + 255) / 256;
+        double pre[NPRE];
+        double preb = -INFINITY;
+        auto load_chunk = [&](int v0) {
+#pragma unroll
+            for (int u = 0; u < NPRE; ++u) {
+                const int idx = threadIdx.x + 256 * u;
+                const int kk = idx / kVT, vv = idx % kVT;
+                const int v = v0 + vv;
+                pre[u] = (idx < 4 * KB * kVT && v < P.nv && kk < P.k4) ? P.PKT[(size_t)kk * P.vcap + v] : 0.0;
+            }
+            if (threadIdx.x < kVT) preb = v0 + (int)threadIdx.x < P.nv ? P.base[v0 + threadIdx.x] : -INFINITY;
+        };
+        load_chunk(0);
         for (int ch = 0; ch < nchunks; ++ch) {
             const int v0 = ch * kVT;
             __syncthreads();
-            // stage PKT[0..4KB)[v0..v0+VT) -> Bs[kk][v] and base
-            for (int idx = threadIdx.x; idx < 4 * KB * kVT; idx += 256) {
-                const int kk = idx / kVT, vv = idx % kVT;
-                const int v = v0 + vv;
-                Bs[kk * kLdsStride + vv] = (v < P.nv && kk < P.k4) ? P.PKT[(size_t)kk * P.vcap + v] : 0.0;
+#pragma unroll
+            for (int u = 0; u < NPRE; ++u) {
+                const int idx = threadIdx.x + 256 * u;
+                if (idx < 4 * KB * kVT) Bs[(idx / kVT) * kLdsStride + idx % kVT] = pre[u];
             }
-            if (threadIdx.x < kVT) {
-                const int v = v0 + threadIdx.x;
-                bs[threadIdx.x] = v < P.nv ? P.base[v] : -INFINITY;
-            }
+            if (threadIdx.x < kVT) bs[threadIdx.x] = preb;
             __syncthreads();
-            d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+            if (ch + 1 < nchunks) load_chunk(v0 + kVT);
+            d4 c00 = {0.0, 0.0, 0.0, 0.0}, c01 = c00;
 #pragma unroll
             for (int kb = 0; kb < KB; ++kb) {
                 const double b0 = Bs[(4 * kb + g) * kLdsStride + j];
                 const double b1 = Bs[(4 * kb + g) * kLdsStride + 16 + j];
-                acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[kb], b0, acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[kb], b1, acc1, 0, 0, 0);
+                c00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[kb], b0, c00, 0, 0, 0);
+                c01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[kb], b1, c01, 0, 0, 0);
             }
-            // epilogue: rows i = g + 4r, columns v0 + j (tile 0) and v0 + 16 + j (tile 1)
+            // C/D layout: acc[r] is row g + 4r, column j of its 16x16 tile
             const int va = v0 + j, vb = v0 + 16 + j;
-            const double ba = bs[j], bb = bs[16 + j];
+            const double ba = va < P.nv ? bs[j] : -INFINITY, bb = vb < P.nv ? bs[16 + j] : -INFINITY;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const double sa = va < P.nv ? ba + acc0[r] : -INFINITY;
-                const double sb = vb < P.nv ? bb + acc1[r] : -INFINITY;
-                double mt = fmax(sa, sb);
-#pragma unroll
-                for (int o = 8; o > 0; o >>= 1) mt = fmax(mt, __shfl_xor(mt, o));
-                const double tt = tolf(mt, P.tie_rel);
-                int it = 0x7fffffff;
-                double st = -INFINITY;
-                if (sb >= mt - tt) { it = vb; st = sb; }
-                if (sa >= mt - tt) { it = va; st = sa; }
-#pragma unroll
-                for (int o = 8; o > 0; o >>= 1) {
-                    const int i2 = __shfl_xor(it, o);
-                    const double s2 = __shfl_xor(st, o);
-                    if (i2 < it) { it = i2; st = s2; }
-                }
-                if (mt == -INFINITY) continue;
-                if (M[r] == -INFINITY || mt > M[r] + tolf(M[r], P.tie_rel)) { M[r] = mt; I[r] = it; SV[r] = st; }
-                else if (mt > M[r]) {
-                    // max slides up inside the tolerance band
-                    if (!(SV[r] >= mt - tolf(mt, P.tie_rel))) F[r] = 1;
-                    M[r] = mt;
-                }
+                row_update(rb[r], ba + c00[r], va, P.tie_rel);
+                row_update(rb[r], bb + c01[r], vb, P.tie_rel);
             }
+        }
+        // combine the 16 lanes (j) of each row: global max M, threshold M - tolf(M); the
+        // answer is the lowest lane candidate inside the band.  A lane whose max reaches
+        // the band but whose candidate does not (or that flagged) -> exact fixup.
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            double M = rb[r].M;
+#pragma unroll
+            for (int o = 8; o > 0; o >>= 1) M = fmax(M, __shfl_xor(M, o));
+            const double thr = M - tolf(M, P.tie_rel);
+            const bool reach = rb[r].M != -INFINITY && rb[r].M >= thr;
+            int it = (reach && rb[r].SV >= thr) ? rb[r].I : 0x7fffffff;
+            double st = rb[r].SV;
+            int fl = reach && (rb[r].F || !(rb[r].SV >= thr));
+#pragma unroll
+            for (int o = 8; o > 0; o >>= 1) {
+                const int i2 = __shfl_xor(it, o);
+                const double s2 = __shfl_xor(st, o);
+                fl |= __shfl_xor(fl, o);
+                if (i2 < it) { it = i2; st = s2; }
+            }
+            rb[r].I = (M == -INFINITY || it == 0x7fffffff) ? -1 : it;
+            rb[r].SV = st;
+            rb[r].F = fl;
         }
         // write results, accumulate partials for decided rows
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int s = s0 + g + 4 * r;
             if (j == 0 && s < P.N) {
-                P.arg[s] = I[r];
-                P.val[s] = SV[r];
-                P.flag[s] = F[r];
+                P.arg[s] = rb[r].I;
+                P.val[s] = rb[r].SV;
+                P.flag[s] = rb[r].F;
             }
         }
         // partial sums: loop the 16 rows of this wave (uniform)
@@ -178,9 +214,9 @@ __global__ void __launch_bounds__(256) cut_argmax_kernel(CutParams P) {
 #pragma unroll
             for (int gg = 0; gg < 4; ++gg) {
                 const int s = s0 + gg + 4 * r;
-                const int ai = __shfl(I[r], gg * 16);
-                const int fl = __shfl(F[r], gg * 16);
-                const double vl = __shfl(SV[r], gg * 16);
+                const int ai = __shfl(rb[r].I, gg * 16);
+                const int fl = __shfl(rb[r].F, gg * 16);
+                const double vl = __shfl(rb[r].SV, gg * 16);
                 if (s >= P.N || fl || ai < 0) continue;
                 const double p = P.w[s] * P.inv_total;
                 if (lane == 0) {
@@ -456,7 +492,7 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     }
     HIPCHK(hipMemcpyAsync(w->coef, coef.data(), sizeof(double) * k4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(w->bvec, bvec.data(), sizeof(double) * m, hipMemcpyHostToDevice, c->stream));
-    const int ntiles = (N + 63) / 64;
+    const int ntiles = (N + kCutTile - 1) / kCutTile;
     const int nblocks = std::max(1, std::min(ntiles, 3 * c->num_cus));
     const int fix_blocks = std::max(1, std::min((N + 3) / 4, c->num_cus));
     const size_t slots = (size_t)nblocks * 4 + (size_t)fix_blocks * 4;

@@ -18,3 +18,18 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def data_dir():
     return DATA
+
+
+def pytest_collection_modifyitems(config, items):
+    # GPU sessions: bring up torch's HIP runtime before libtwosd_hip.so touches the device,
+    # as bench.py does (tests that hand torch device tensors to the library need torch's
+    # runtime; initialising it after the library's has been seen to find no devices)
+    if "not gpu" in (config.getoption("-m") or ""):
+        return
+    if any(item.get_closest_marker("gpu") for item in items):
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except Exception:
+            pass
