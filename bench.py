@@ -63,7 +63,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-dedup", action="store_true")
-    ap.add_argument("--pool", type=int, default=256, help="warm-start basis pool size (1 = primary basis only)")
+    ap.add_argument("--pool", type=int, default=512, help="warm-start basis pool size (1 = primary basis only)")
     ap.add_argument("--pool-train", type=int, default=16384, help="training scenarios of the pool build")
     args = ap.parse_args()
 

@@ -136,7 +136,7 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_xbase); dfree(c->d_B0K); dfree(c->d_eta); dfree(c->d_queue);
     dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_ops);
     dfree(c->d_dvtmp);
-    dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); dfree(c->d_sel_val); dfree(c->d_head_out); dfree(c->d_pool_pick); dfree(c->d_order); dfree(c->d_sort_tmp); c->order_cap = 0; c->sort_tmp_bytes = 0; c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
+    dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); dfree(c->d_head_out); dfree(c->d_pool_pick); dfree(c->d_order); dfree(c->d_sort_tmp); c->order_cap = 0; c->sort_tmp_bytes = 0; c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
     dfree(c->d_kslot); dfree(c->d_kix); dfree(c->d_kv); dfree(c->d_kcoef); c->k_valid = false;
     dfree(c->d_d0); dfree(c->d_eidx); dfree(c->d_evals); dfree(c->d_stamps);
     dfree(c->d_wr_col); dfree(c->d_wr_val); dfree(c->d_wr_ocol); dfree(c->d_wr_oval); dfree(c->d_bslot); dfree(c->d_bix); dfree(c->d_bv);
@@ -752,8 +752,15 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
     if (P > 1 && c->CH > 0) {
         std::vector<int8_t> bt(c->L.n + m);
         HIPCHK(hipMemcpy(bt.data(), c->d_btype, bt.size(), hipMemcpyDeviceToHost));
-        std::vector<double> cinf(P, 0.0), sval;
-        std::vector<int> sptr(1, 0), scode;
+        std::vector<float> cinf(P, 0.0f);
+        std::vector<int> sptr(1, 0), scode;   // interleaved (code, float bits) records
+        auto rec = [&](int code, double v) {
+            const float f = (float)v;
+            int bits;
+            std::memcpy(&bits, &f, 4);
+            scode.push_back(code);
+            scode.push_back(bits);
+        };
         c->sel_rows = 0;
         const bool box = !c->sel_lo.empty();
         for (int p = 0; p < P; ++p) {
@@ -762,7 +769,7 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
                 const int t = bt[B.head[i]];
                 const double xv = xb[(size_t)p * MP + i];
                 const int q0 = B.kptr[i], q1 = B.kptr[i + 1];
-                if (q0 == q1) { cinf[p] += std::fabs(host_infeas(xv, t)); continue; }
+                if (q0 == q1) { cinf[p] += (float)std::fabs(host_infeas(xv, t)); continue; }
                 if (box) {
                     // interval of x_i over the training box of the deltas: a row that stays
                     // feasible on the whole box never contributes, so it is left out
@@ -778,17 +785,15 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
                     const bool feasible_box = (t == BT_Y || t == BT_L) ? lo > tol : (t == BT_G) ? hi < -tol : false;
                     if (std::isfinite(lo) && std::isfinite(hi) && feasible_box) continue;
                 }
-                scode.push_back(-1 - t);
-                sval.push_back(xv);
+                rec(-1 - t, xv);
                 ++c->sel_rows;
-                for (int q = q0; q < q1; ++q) { scode.push_back(B.ke[q]); sval.push_back(B.kraw[q]); }
+                for (int q = q0; q < q1; ++q) rec(B.ke[q], B.kraw[q]);
             }
-            sptr.push_back((int)scode.size());
+            sptr.push_back((int)scode.size() / 2);
         }
-        if ((rc = upload(&c->d_sel_cinf, cinf)) || (rc = upload(&c->d_sel_ptr, sptr)) || (rc = upload(&c->d_sel_code, scode)) ||
-            (rc = upload(&c->d_sel_val, sval)))
+        if ((rc = upload(&c->d_sel_cinf, cinf)) || (rc = upload(&c->d_sel_ptr, sptr)) || (rc = upload(&c->d_sel_code, scode)))
             return rc;
-        c->sel_nnz = (int64_t)scode.size() - c->sel_rows;
+        c->sel_nnz = (int64_t)scode.size() / 2 - c->sel_rows;
     }
     c->prep_x.assign(x, x + n1);
     c->prep_valid = true;
@@ -873,7 +878,7 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
             PoolSelParams S{};
             S.N = N; S.k = c->k; S.npool = H.npool; S.dv = d_dv;
             S.kcoef = c->d_kcoef;
-            S.cinf = c->d_sel_cinf; S.sptr = c->d_sel_ptr; S.code = c->d_sel_code; S.val = c->d_sel_val;
+            S.cinf = c->d_sel_cinf; S.sptr = c->d_sel_ptr; S.rec = reinterpret_cast<const int2 *>(c->d_sel_code);
             S.pick = c->d_pool_pick;
             HIPCHK(launch_pool_select(S, c->stream));
             size_t tb = 0;

@@ -54,8 +54,8 @@ struct twosd_ctx {
     double *d_B0inv = nullptr, *d_B0invT = nullptr, *d_pi0 = nullptr, *d_xbase = nullptr, *d_B0K = nullptr;
     std::vector<twosd::PoolBasis> pool;   // warm-start basis pool, pool[0] = head0
     // pool selection data (per x, prepare_x): constant-row infeasibility, active rows, entries
-    double *d_sel_cinf = nullptr, *d_sel_val = nullptr;
-    int *d_sel_ptr = nullptr, *d_sel_code = nullptr;
+    float *d_sel_cinf = nullptr;
+    int *d_sel_ptr = nullptr, *d_sel_code = nullptr;   // code: (code, float bits) record pairs
     int64_t sel_nnz = 0, sel_rows = 0;
     std::vector<double> sel_lo, sel_hi;   // training box of the deltas (empty: no row pruning)
     int *d_bnnz = nullptr;        // npool: nnz of each pool B^{-1} (FMA accounting)

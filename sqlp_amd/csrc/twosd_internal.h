@@ -90,9 +90,10 @@ struct PoolSelParams {
     int N, k, npool;
     const double *dv;                                   // N x k
     const double *kcoef;                                // k: coef_e(x)
-    const double *cinf;                                 // npool: infeasibility of the constant rows
+    const float *cinf;                                  // npool: infeasibility of the constant rows
     const int *sptr;                                    // npool + 1 -> flat stream of active rows
-    const int *code; const double *val;                 // row start: (-1 - bound type, xbase_i); entry: (e, coef)
+    const int2 *rec;                                    // (code, float bits): row start (-1 - bound type,
+                                                        //   xbase_i); entry (e, B^{-1}[i][row_e])
     int *pick;                                          // N out
 };
 size_t pool_select_lds_bytes(int k);
