@@ -594,10 +594,19 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
 // wave-uniform, so it streams through scalar loads and the per-lane work is LDS reads +
 // FMAs.  Key: total primal infeasibility sum_i |infeas(x_B,i)| at b_w (constant rows
 // precomputed in cinf); ties: lowest p.
+// The selection is a heuristic (any pool basis is a valid start; the choice only changes
+// pivot counts), so it runs in fp32: half the LDS traffic of the staged deltas, 8-byte
+// records (code, value) -- deterministic like everything else.
+__device__ __forceinline__ float h_infeas_f(float x, int bt) {
+    if (bt == BT_Y || bt == BT_L) return x < -1e-9f ? -x : 0.0f;
+    if (bt == BT_G) return x > 1e-9f ? x : 0.0f;
+    return fabsf(x) > 1e-9f ? fabsf(x) : 0.0f;
+}
+
 constexpr int kSelWaves = 16;   // 16 waves share one staged 64-scenario tile (latency hiding)
 __global__ void __launch_bounds__(64 * kSelWaves) pool_select_kernel(PoolSelParams S) {
-    extern __shared__ double dvt[];   // k x 65 (padded)
-    __shared__ double bsum[kSelWaves][64];
+    extern __shared__ float dvt[];   // k x 65 (padded)
+    __shared__ float bsum[kSelWaves][64];
     __shared__ int bidx[kSelWaves][64];
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar stream loads
@@ -606,46 +615,46 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_select_kernel(PoolSelPara
     const int ns = min(64, S.N - s0);
     for (int idx = threadIdx.x; idx < 64 * k; idx += 64 * kSelWaves) {
         const int sl = idx / k, e = idx - sl * k;
-        dvt[e * 65 + sl] = sl < ns ? S.kcoef[e] * S.dv[(size_t)s0 * k + idx] : 0.0;
+        dvt[e * 65 + sl] = sl < ns ? (float)(S.kcoef[e] * S.dv[(size_t)s0 * k + idx]) : 0.0f;
     }
     __syncthreads();
-    double best = INFINITY;
+    float best = INFINITY;
     int bp = 0;
     for (int p = wid; p < S.npool; p += kSelWaves) {
         // one flat, wave-uniform stream per basis: a row-start record (code -1 - bound type,
-        // value xbase_i) followed by the row's entries (code e, value coef_e B^{-1}[i][row_e]);
+        // value xbase_i) followed by the row's entries (code e, value B^{-1}[i][row_e]);
         // no load depends on the loop state, so the stream pipelines through the scalar cache
-        double inf = S.cinf[p], x = 0.0;
+        float inf = S.cinf[p], x = 0.0f;
         int bt = -1;
         const int j0 = S.sptr[p], j1 = S.sptr[p + 1];
-        auto step = [&](int code, double v, double dl) {
+        auto step = [&](int code, float v, float dl) {
             if (code < 0) {
-                if (bt >= 0) inf += fabs(h_infeas(x, bt));
+                if (bt >= 0) inf += h_infeas_f(x, bt);
                 x = v;
                 bt = -1 - code;
             } else {
-                x = fma(v, dl, x);
+                x = fmaf(v, dl, x);
             }
         };
         int j = (__ballot(inf < best) == 0) ? j1 : j0;   // constant rows alone already lose
         for (; j + 8 <= j1; j += 8) {   // batches of 8 records: scalar loads and LDS reads in flight together
-            int cd[8];
-            double vv[8], dl[8];
+            int2 rc[8];
+            float dl[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) { cd[u] = S.code[j + u]; vv[u] = S.val[j + u]; }
+            for (int u = 0; u < 8; ++u) rc[u] = S.rec[j + u];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) dl[u] = dvt[(cd[u] < 0 ? 0 : cd[u]) * 65 + lane];
+            for (int u = 0; u < 8; ++u) dl[u] = dvt[(rc[u].x < 0 ? 0 : rc[u].x) * 65 + lane];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) step(cd[u], vv[u], dl[u]);
+            for (int u = 0; u < 8; ++u) step(rc[u].x, __int_as_float(rc[u].y), dl[u]);
             // exact pruning: inf only grows (sum of nonnegative terms), so once no lane can
             // still beat its best, this basis cannot win for any of the 64 scenarios
             if (__ballot(inf < best) == 0) { bt = -1; inf = INFINITY; j = j1; break; }
         }
         for (; j < j1; ++j) {
-            const int cd = S.code[j];
-            step(cd, S.val[j], dvt[(cd < 0 ? 0 : cd) * 65 + lane]);
+            const int2 r = S.rec[j];
+            step(r.x, __int_as_float(r.y), dvt[(r.x < 0 ? 0 : r.x) * 65 + lane]);
         }
-        if (bt >= 0) inf += fabs(h_infeas(x, bt));
+        if (bt >= 0) inf += h_infeas_f(x, bt);
         if (inf < best) { best = inf; bp = p; }
     }
     bsum[wid][lane] = best;
@@ -653,7 +662,7 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_select_kernel(PoolSelPara
     __syncthreads();
     if (wid == 0 && lane < ns) {
         for (int w = 1; w < kSelWaves; ++w) {
-            const double v = bsum[w][lane];
+            const float v = bsum[w][lane];
             const int pw = bidx[w][lane];
             if (v < best || (v == best && pw < bp)) { best = v; bp = pw; }
         }
@@ -661,7 +670,7 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_select_kernel(PoolSelPara
     }
 }
 
-size_t pool_select_lds_bytes(int k) { return (size_t)8 * 65 * (size_t)std::max(k, 1); }
+size_t pool_select_lds_bytes(int k) { return (size_t)4 * 65 * (size_t)std::max(k, 1); }
 
 hipError_t launch_pool_select(const PoolSelParams &p, hipStream_t s) {
     if (p.N <= 0) return hipSuccess;
