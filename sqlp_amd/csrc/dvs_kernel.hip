@@ -20,80 +20,47 @@
 #include <algorithm>
 #include <vector>
 #include "twosd_ctx.h"
+#include "dvs_keys.h"
 
 namespace twosd {
 
-__device__ __forceinline__ double round16(double x) {
-    // Julia round(x; base=2, sigdigits=16): non-finite -> x; 0 -> x;
-    // digits = 16 - (1 + exponent(x)); scale by an exact power of two, ties to even.
-    if (!isfinite(x) || x == 0.0) return x;
-    int e2;
-    frexp(x, &e2);                    // x = f * 2^e2, 0.5 <= |f| < 1 -> exponent(x) = e2 - 1
-    const int digits = 16 - e2;
-    double r;
-    if (digits >= 0) {
-        const double sc = ldexp(1.0, digits);
-        r = rint(x * sc) / sc;
-    } else {
-        const double isc = ldexp(1.0, -digits);
-        r = rint(x / isc) * isc;
-    }
-    return isfinite(r) ? r : x;
-}
-
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-    z += 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-
-// key component bits: round16 with -0.0 folded onto +0.0 (Julia: -0.0 != 0.0 is false)
-__device__ __forceinline__ uint64_t comp_bits(double x) {
-    double r = round16(x);
-    if (r == 0.0) r = 0.0;
-    return (uint64_t)__double_as_longlong(r);
-}
-
-__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, o);
-    return v;
-}
-
-// Phase 1: one wavefront per candidate -> hash (reference, sequential L1 order),
-// fingerprint, has-NaN flag.
+// Phase 1: one LANE per candidate -> hash (reference, sequential L1 order), fingerprint,
+// has-NaN flag.  The sequential sum is a dependent chain per vector, so each lane walks
+// its own vector; the block's 256 vectors are staged through LDS 16 columns at a time
+// (coalesced 128-byte row segments in, conflict-free stride-17 reads out).
+constexpr int kKeyCols = 16;
 __global__ void __launch_bounds__(256) dvs_key_kernel(int count, int m, const double *__restrict__ pis,
                                                       uint64_t *__restrict__ hash, uint64_t *__restrict__ fp,
                                                       int *__restrict__ nanflag) {
-    const int lane = threadIdx.x & 63;
-    const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int nw = (gridDim.x * blockDim.x) >> 6;
-    for (int c = gw; c < count; c += nw) {
-        const double *p = pis + (size_t)c * m;
-        double acc = 0.0;           // sequential sum in index order (dual_set.jl:47-50)
-        uint64_t f = 0;
-        int hasnan = 0;
-        for (int b = 0; b < m; b += 64) {
-            const int i = b + lane;
-            const double v = i < m ? p[i] : 0.0;
-            if (i < m) {
-                hasnan |= isnan(v);
-                f += mix64(comp_bits(v) ^ (0xD6E8FEB86659FD93ull * (uint64_t)(i + 1)));
-            }
-            const double a = fabs(v);
-            const int lim = min(64, m - b);
-            for (int l = 0; l < lim; ++l) acc += __shfl(a, l);
+    __shared__ double tile[256 * (kKeyCols + 1)];
+    const int c0 = blockIdx.x * 256;
+    const int c = c0 + threadIdx.x;
+    double acc = 0.0;               // sequential sum in index order (dual_set.jl:47-50)
+    uint64_t f = 0;
+    int hasnan = 0;
+    for (int i0 = 0; i0 < m; i0 += kKeyCols) {
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kKeyCols; ++u) {
+            // element u*256 + t of the chunk: vector (u*256+t)/16, column (u*256+t)%16
+            const int q = u * 256 + threadIdx.x, vr = q / kKeyCols, col = q % kKeyCols;
+            const int cv = c0 + vr, i = i0 + col;
+            tile[vr * (kKeyCols + 1) + col] = (cv < count && i < m) ? pis[(size_t)cv * m + i] : 0.0;
         }
-        f = wave_sum_u64(f);
-        hasnan = __any(hasnan);
-        if (lane == 0) {
-            const uint64_t h = (uint64_t)__double_as_longlong(round16(acc));
-            hash[c] = h;
-            fp[c] = mix64(f ^ h);
-            nanflag[c] = hasnan;
+        __syncthreads();
+        const int lim = min(kKeyCols, m - i0);
+        for (int col = 0; col < lim; ++col) {
+            const double v = tile[threadIdx.x * (kKeyCols + 1) + col];
+            hasnan |= isnan(v);
+            f += mix64(comp_bits(v) ^ (0xD6E8FEB86659FD93ull * (uint64_t)(i0 + col + 1)));
+            acc += fabs(v);
         }
     }
+    if (c >= count) return;
+    const uint64_t h = (uint64_t)__double_as_longlong(round16(acc));
+    hash[c] = h;
+    fp[c] = mix64(f ^ h);
+    nanflag[c] = hasnan;
 }
 
 // full key equality of candidate row a (hash ha) and row b (hash hb); one wavefront
@@ -314,7 +281,8 @@ static int ws_grow(T **p, size_t need) {
 
 // Push `count` candidates already on the device (row-major count x m).  d_out_index
 // (nullable, device) receives the vertex index of every candidate.
-int dvs_push_device(twosd_ctx *c, int count, const double *d_pis, int *d_out_index) {
+int dvs_push_device(twosd_ctx *c, int count, const double *d_pis, int *d_out_index, const uint64_t *d_hash,
+                    const uint64_t *d_fp, const int *d_nan) {
     if (count <= 0) return TWOSD_OK;
     DvsDevice &D = c->dvs;
     DvsWs *w = ws_of(c);
@@ -345,7 +313,14 @@ int dvs_push_device(twosd_ctx *c, int count, const double *d_pis, int *d_out_ind
     const int ttmask = (int)w->ttcap - 1;
     const int nb = nblocks_for(count);
     hipLaunchKernelGGL(dvs_fill_kernel, dim3((w->ttcap + 255) / 256), dim3(256), 0, c->stream, w->tt, (int)w->ttcap, -1);
-    hipLaunchKernelGGL(dvs_key_kernel, dim3(nb), dim3(256), 0, c->stream, count, m, d_pis, w->chash, w->cfp, w->nanflag);
+    if (d_hash) {   // keys computed by the producer (LP kernel epilogue)
+        HIPCHK(hipMemcpyAsync(w->chash, d_hash, sizeof(uint64_t) * count, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(w->cfp, d_fp, sizeof(uint64_t) * count, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(w->nanflag, d_nan, sizeof(int) * count, hipMemcpyDeviceToDevice, c->stream));
+    } else {
+        hipLaunchKernelGGL(dvs_key_kernel, dim3((count + 255) / 256), dim3(256), 0, c->stream, count, m, d_pis, w->chash,
+                           w->cfp, w->nanflag);
+    }
     hipLaunchKernelGGL(dvs_lookup_kernel, dim3(nb), dim3(256), 0, c->stream, count, m, d_pis, w->chash, w->cfp,
                        w->nanflag, D.V, D.hash, D.fp, D.table, D.tcap - 1, w->out);
     hipLaunchKernelGGL(dvs_batch_kernel, dim3(nb), dim3(256), 0, c->stream, count, m, d_pis, w->chash, w->cfp,
@@ -386,7 +361,7 @@ extern "C" int twosd_dvs_push(twosd_ctx *c, int count, const double *pis, int *o
         HIPCHK(hipMemcpy(w->pis, pis, sizeof(double) * need, hipMemcpyHostToDevice));
         hipEvent_t e0 = c->ev[2], e1 = c->ev[3];
         HIPCHK(hipEventRecord(e0, c->stream));
-        int rc = dvs_push_device(c, count, w->pis, nullptr);
+        int rc = dvs_push_device(c, count, w->pis, nullptr, nullptr, nullptr, nullptr);
         if (rc) return rc;
         HIPCHK(hipEventRecord(e1, c->stream));
         HIPCHK(hipEventSynchronize(e1));

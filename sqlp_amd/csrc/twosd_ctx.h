@@ -123,7 +123,9 @@ int run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool want_p
 // dual vertex set (dvs_kernel.hip)
 int dvs_init(twosd_ctx *c);
 void dvs_free(twosd_ctx *c);
-int dvs_push_device(twosd_ctx *c, int count, const double *d_pis, int *d_out_index);
+// d_hash / d_fp / d_nan: keys precomputed by the producer (nullable: computed here)
+int dvs_push_device(twosd_ctx *c, int count, const double *d_pis, int *d_out_index, const uint64_t *d_hash = nullptr,
+                    const uint64_t *d_fp = nullptr, const int *d_nan = nullptr);
 // cut (cut_kernel.hip)
 void cut_free(twosd_ctx *c);
 void cut_invalidate_pk(twosd_ctx *c);
