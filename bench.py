@@ -65,6 +65,8 @@ def main():
     ap.add_argument("--no-dedup", action="store_true")
     ap.add_argument("--pool", type=int, default=512, help="warm-start basis pool size (1 = primary basis only)")
     ap.add_argument("--pool-train", type=int, default=16384, help="training scenarios of the pool build")
+    ap.add_argument("--sampler", choices=["device", "host"], default="device",
+                    help="scenario draws: on-device Philox4x32-10 sampler (twosd_add_sampled_scenarios) or numpy PCG64")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -89,12 +91,22 @@ def main():
     ctx = twosd.SDContext(sp2, sto, device=local_rank)
     ctx.compute_basis(x, smps.mean_values(sto, positions))
 
+    if args.sampler == "device":
+        ctx.set_distributions(sto)
+
+    def scenarios(epi_, lo_, hi_, seed_):
+        """Scenarios [lo_, hi_) of the global stream `seed_` appended to epi_ (sharding-invariant)."""
+        if args.sampler == "device":
+            twosd.add_sampled_scenarios(epi_, hi_ - lo_, seed_, first_index=lo_)
+        else:
+            twosd.add_scenarios(epi_, chunked_values(sto, positions, lo_, hi_, seed_))
+
     # warm-start basis pool (setup, untimed like compute_basis): optimal bases of independent
     # training scenarios of the same distribution (seed + 2, identical on every rank)
     t_pool = time.perf_counter()
     if args.pool > 1:
         tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
-        twosd.add_scenarios(tr, chunked_values(sto, positions, 0, args.pool_train, args.seed + 2))
+        scenarios(tr, 0, args.pool_train, args.seed + 2)
         ctx.pool_build(tr, x, 0, args.pool_train, args.pool)
     pool_size = ctx.pool_size()
     t_pool = time.perf_counter() - t_pool
@@ -102,17 +114,19 @@ def main():
     N = args.scenarios
     lo, hi = sdist.shard_range(N, rank, world)
     n_local = hi - lo
-    vals = chunked_values(sto, positions, lo, hi, args.seed)
+    t_gen = time.perf_counter()
     epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
-    twosd.add_scenarios(epi, vals)
+    scenarios(epi, lo, hi, args.seed)
+    t_gen = time.perf_counter() - t_gen
     total_weight = float(N)        # all weights 1.0 (sd_iteration! uses 1.0, algorithm.jl:46)
 
-    # |V| pool: duals of the first scenarios of the global stream (identical on every rank)
+    # |V| pool: duals of the first scenarios of the global stream seed + 1 (identical on every rank)
     V = twosd.sdDualVertexSet(ctx)
-    pool_src = chunked_values(sto, positions, 0, 1 << 18, args.seed + 1)
+    src = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    scenarios(src, 0, 1 << 18, args.seed + 1)
     at = 0
-    while len(V) < args.vertices and at < pool_src.shape[0]:
-        _, _, pis, st = ctx.solve_values(x, pool_src[at:at + 16384], want_pi=True)
+    while len(V) < args.vertices and at < (1 << 18):
+        _, _, pis, st = twosd.solve_batch(src, x, at, 16384, want_pi=True)
         V.push_batch(pis[st == 0])
         at += 16384
     if len(V) > args.vertices:
@@ -187,7 +201,9 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic: i.i.d. scenarios of storm.sto (numpy PCG64), x = EV solution",
+        "data": (f"synthetic: i.i.d. scenarios of {name}.sto drawn on the device (Philox4x32-10, seed {args.seed}, "
+                 f"{t_gen:.2f} s for the shard)" if args.sampler == "device" else
+                 f"synthetic: i.i.d. scenarios of {name}.sto (numpy PCG64, seed {args.seed})") + ", x = EV solution",
         "config": {"workload": f"{name} {N} scenarios sharded over {world} GPU(s), |V|={nv}, "
                                f"warm-start pool {pool_size}, LP solve + dual dedup + build_sasa_cut per step",
                    "instance": name, "scenarios": N, "vertices": nv, "k": k, "m2": m,
@@ -219,6 +235,7 @@ def main():
         if kc:
             out["cutgen"]["traffic"] = kc["hbm_bytes_per_launch"]
     if rank == 0 and world == 1 and not args.no_cpu:
+        vals = twosd.get_scenarios(epi, 0, min(n_local, 1 << 19))   # the CPU sample: same scenarios
         out["cpu_baseline"] = cpu_baseline(sp2, ctx, x, vals, V.matrix(), positions, args)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -117,6 +117,24 @@ int twosd_add_scenarios(twosd_ctx *ctx, int epi, int N, const double *values, co
 int twosd_epigraph_info(twosd_ctx *ctx, int epi, int *num_scenarios, double *total_weight);
 
 /*
+ * On-device scenario sampling (rand(rng, sto), smps_sto.jl:117-149).
+ * set_distributions: one distribution per random element (position order): kind[e] =
+ *   0 DISCRETE (nsupport[e] (value, probability) pairs, concatenated over elements in
+ *   values/probs; sorted by value like DiscreteNonParametric), 1 NORMAL (param0 = mean,
+ *   param1 = VARIANCE: Normal(mean, sqrt(variance)), smps_sto.jl:122-125), 2 UNIFORM
+ *   (param0 = left, param1 = right).  Reset by twosd_set_random_positions.
+ * add_sampled_scenarios: appends N i.i.d. scenarios to epigraph epi (weights NULL = 1.0).
+ *   Element e of scenario number first_index + s is drawn from Philox4x32-10(counter =
+ *   (index, e), key = seed), so a stream is reproducible under any sharding.
+ * get_scenarios: element values (template + stored delta) of scenarios [first, first+count).
+ */
+int twosd_set_distributions(twosd_ctx *ctx, int k, const int *kind, const int *nsupport, const double *values,
+                            const double *probs, const double *param0, const double *param1);
+int twosd_add_sampled_scenarios(twosd_ctx *ctx, int epi, int N, uint64_t seed, uint64_t first_index,
+                                const double *weights);
+int twosd_get_scenarios(twosd_ctx *ctx, int epi, int first, int count, double *values);
+
+/*
  * solve_problem! (smps_routines.jl:50-62) for scenarios [first, first+count) of epigraph
  * `epi` at first-stage x[n1].  obj[count], status[count] required; pi[count*m2] and
  * y[count*n2] nullable.  Returns TWOSD_E_LP if any status != OPTIMAL (outputs still set).

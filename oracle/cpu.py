@@ -40,6 +40,8 @@ def lib():
         L.oracle_build_cut.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P, P, P,
                                        C.c_double, P, P, P, P, C.c_int]
         L.oracle_dense_inverse.argtypes = [C.c_int, P, P]
+        L.oracle_philox4x32_10.argtypes = [P, P, P]
+        L.oracle_sample.argtypes = [C.c_int, C.c_int, C.c_uint64, C.c_uint64, P, P, P, P, P, P, P, P]
         _lib = L
     return _lib
 
@@ -123,3 +125,36 @@ def build_cut(r, T, x, V, rows, DR, w, tie_rel=0.0, nthreads=0):
     lib().oracle_build_cut(m, n1, nv, N, k, _p(rows), _p(r), _p(T), _p(x), _p(V), _p(DR), _p(w),
                            float(tie_rel), C.byref(alpha), _p(beta), _p(mv), _p(ma), nthreads)
     return alpha.value, beta, mv, ma
+
+
+def philox4x32_10(ctr, key):
+    """Philox4x32-10 block (published algorithm, restated in oracle/sampler.c)."""
+    c = np.ascontiguousarray(ctr, dtype=np.uint32)
+    k = np.ascontiguousarray(key, dtype=np.uint32)
+    out = np.zeros(4, dtype=np.uint32)
+    lib().oracle_philox4x32_10(_p(c), _p(k), _p(out))
+    return out
+
+
+def sample_deltas(sto, positions, template_values, N, seed, first_index=0):
+    """N x k scenario deltas (value - template) of the device sampler's stream."""
+    kinds, off, vals, probs, p0, p1 = [], [0], [], [], [], []
+    for pos in positions:
+        d = sto.indep[pos]
+        if d[0] == "DISCRETE":
+            order = np.argsort(np.asarray(d[1]), kind="stable")
+            kinds.append(0); vals += list(np.asarray(d[1])[order]); probs += list(np.asarray(d[2])[order])
+            p0.append(0.0); p1.append(0.0)
+        elif d[0] == "NORMAL":
+            kinds.append(1); p0.append(d[1]); p1.append(float(np.sqrt(d[2])))
+        else:
+            kinds.append(2); p0.append(d[1]); p1.append(d[2])
+        off.append(len(vals))
+    k = len(positions)
+    a = [np.ascontiguousarray(kinds, dtype=np.int32), np.ascontiguousarray(off, dtype=np.int32),
+         np.ascontiguousarray(vals if vals else [0.0]), np.ascontiguousarray(probs if probs else [0.0]),
+         np.ascontiguousarray(p0, dtype=np.float64), np.ascontiguousarray(p1, dtype=np.float64),
+         np.ascontiguousarray(template_values, dtype=np.float64)]
+    out = np.zeros((N, k))
+    lib().oracle_sample(int(N), k, C.c_uint64(seed), C.c_uint64(first_index), *[_p(v) for v in a], _p(out))
+    return out

@@ -137,6 +137,8 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_ops);
     dfree(c->d_dvtmp);
     dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); dfree(c->d_head_out); dfree(c->d_pool_pick); dfree(c->d_order); dfree(c->d_sort_tmp); c->order_cap = 0; c->sort_tmp_bytes = 0; c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
+    dfree(c->d_dist_kind); dfree(c->d_dist_off); dfree(c->d_dist_val); dfree(c->d_dist_prob); dfree(c->d_dist_p0);
+    dfree(c->d_dist_p1); dfree(c->d_dist_tmpl); c->has_dist = false;
     dfree(c->d_kslot); dfree(c->d_kix); dfree(c->d_kv); dfree(c->d_kcoef); c->k_valid = false;
     dfree(c->d_d0); dfree(c->d_eidx); dfree(c->d_evals); dfree(c->d_stamps);
     dfree(c->d_wr_col); dfree(c->d_wr_val); dfree(c->d_wr_ocol); dfree(c->d_wr_oval); dfree(c->d_bslot); dfree(c->d_bix); dfree(c->d_bv);
@@ -284,6 +286,7 @@ extern "C" int twosd_set_random_positions(twosd_ctx *c, int k, const int *row, c
     c->k = k;
     c->prep_valid = false;
     c->k_valid = false;
+    c->has_dist = false;
     cut_invalidate_pk(c);
     return TWOSD_OK;
 }
@@ -659,6 +662,98 @@ extern "C" int twosd_add_scenarios(twosd_ctx *c, int epi, int N, const double *v
     E.w_host.insert(E.w_host.end(), w.begin(), w.end());
     for (int s = 0; s < N; ++s) E.total_weight += w[s];   // epigraph.jl:89, in insertion order
     E.count += N;
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_set_distributions(twosd_ctx *c, int k, const int *kind, const int *nsupport, const double *values,
+                                       const double *probs, const double *param0, const double *param1) {
+    if (!c || !c->has_template) return fail(TWOSD_E_STATE, "set_distributions: no template");
+    if (k != c->k) return fail(TWOSD_E_ARG, "set_distributions: %d distributions for %d random elements", k, c->k);
+    if (k > 0 && (!kind || !nsupport || !param0 || !param1)) return fail(TWOSD_E_ARG, "set_distributions: NULL argument");
+    HIPCHK(hipSetDevice(c->device));
+    std::vector<int> kd(std::max(k, 1), 0), off(k + 1, 0);
+    std::vector<double> val, prob, p0(std::max(k, 1), 0.0), p1(std::max(k, 1), 0.0), tmpl(std::max(k, 1), 0.0);
+    size_t at = 0;
+    for (int e = 0; e < k; ++e) {
+        kd[e] = kind[e];
+        tmpl[e] = template_value(c, e);
+        if (kind[e] == 0) {   // DISCRETE: DiscreteNonParametric sorts its support, values unique
+            const int n = nsupport[e];
+            if (n < 1 || !values || !probs) return fail(TWOSD_E_ARG, "set_distributions: element %d has an empty support", e);
+            std::vector<std::pair<double, double>> sp(n);
+            for (int i = 0; i < n; ++i) sp[i] = {values[at + i], probs[at + i]};
+            at += n;
+            std::stable_sort(sp.begin(), sp.end(), [](const std::pair<double, double> &a, const std::pair<double, double> &b) { return a.first < b.first; });
+            for (int i = 0; i < n; ++i) {
+                if (i && sp[i].first == sp[i - 1].first) return fail(TWOSD_E_ARG, "set_distributions: element %d support values not unique", e);
+                if (!(sp[i].second >= 0.0)) return fail(TWOSD_E_ARG, "set_distributions: element %d has a negative probability", e);
+                val.push_back(sp[i].first);
+                prob.push_back(sp[i].second);
+            }
+        } else if (kind[e] == 1) {   // NORMAL(mean, variance) -> Normal(mean, sqrt(variance)), smps_sto.jl:122-125
+            if (!(param1[e] >= 0.0)) return fail(TWOSD_E_ARG, "set_distributions: element %d has a negative variance", e);
+            p0[e] = param0[e];
+            p1[e] = std::sqrt(param1[e]);
+        } else if (kind[e] == 2) {   // UNIFORM(left, right)
+            p0[e] = param0[e];
+            p1[e] = param1[e];
+        } else {
+            return fail(TWOSD_E_ARG, "set_distributions: element %d has unknown kind %d", e, kind[e]);
+        }
+        off[e + 1] = (int)val.size();
+    }
+    int rc;
+    if ((rc = upload(&c->d_dist_kind, kd)) || (rc = upload(&c->d_dist_off, off)) || (rc = upload(&c->d_dist_val, val)) ||
+        (rc = upload(&c->d_dist_prob, prob)) || (rc = upload(&c->d_dist_p0, p0)) || (rc = upload(&c->d_dist_p1, p1)) ||
+        (rc = upload(&c->d_dist_tmpl, tmpl)))
+        return rc;
+    c->has_dist = true;
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_add_sampled_scenarios(twosd_ctx *c, int epi, int N, uint64_t seed, uint64_t first_index,
+                                           const double *weights) {
+    if (!c || !c->has_template) return fail(TWOSD_E_STATE, "add_sampled_scenarios: no template");
+    if (!c->has_dist) return fail(TWOSD_E_STATE, "add_sampled_scenarios: no distributions (twosd_set_distributions)");
+    if (epi < 0 || epi >= (int)c->epis.size()) return fail(TWOSD_E_ARG, "add_sampled_scenarios: epigraph %d does not exist", epi);
+    if (N < 0) return fail(TWOSD_E_ARG, "add_sampled_scenarios: N < 0");
+    if (N == 0) return TWOSD_OK;
+    HIPCHK(hipSetDevice(c->device));
+    EpiDevice &E = c->epis[epi];
+    const int k = c->k;
+    std::vector<double> w(N, 1.0);
+    if (weights)
+        for (int s = 0; s < N; ++s) {
+            if (!(weights[s] >= 0.0) || !std::isfinite(weights[s])) return fail(TWOSD_E_ARG, "weight[%d] = %g must be finite and >= 0", s, weights[s]);
+            w[s] = weights[s];
+        }
+    int rc;
+    if ((rc = dgrow(&E.d_dv, &E.dv_cap, (size_t)(E.count + N) * k, (size_t)E.count * k, c->stream))) return rc;
+    if ((rc = dgrow(&E.d_w, &E.w_cap, (size_t)(E.count + N), (size_t)E.count, c->stream))) return rc;
+    SampleParams S{};
+    S.N = N; S.k = k; S.seed = seed; S.first_index = first_index;
+    S.kind = c->d_dist_kind; S.off = c->d_dist_off; S.val = c->d_dist_val; S.prob = c->d_dist_prob;
+    S.p0 = c->d_dist_p0; S.p1 = c->d_dist_p1; S.tmpl = c->d_dist_tmpl; S.out = E.d_dv + (size_t)E.count * k;
+    HIPCHK(launch_sample(S, c->stream));
+    HIPCHK(hipMemcpyAsync(E.d_w + E.count, w.data(), sizeof(double) * N, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    E.w_host.insert(E.w_host.end(), w.begin(), w.end());
+    for (int s = 0; s < N; ++s) E.total_weight += w[s];   // epigraph.jl:89, in insertion order
+    E.count += N;
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_get_scenarios(twosd_ctx *c, int epi, int first, int count, double *values) {
+    if (!c || epi < 0 || epi >= (int)c->epis.size()) return fail(TWOSD_E_ARG, "get_scenarios: bad epigraph");
+    const EpiDevice &E = c->epis[epi];
+    if (first < 0 || count < 0 || first + count > E.count || (count > 0 && c->k > 0 && !values))
+        return fail(TWOSD_E_ARG, "get_scenarios: range [%d,%d) outside %d scenarios", first, first + count, E.count);
+    if (count == 0 || c->k == 0) return TWOSD_OK;
+    HIPCHK(hipSetDevice(c->device));
+    const int k = c->k;
+    HIPCHK(hipMemcpy(values, E.d_dv + (size_t)first * k, sizeof(double) * count * k, hipMemcpyDeviceToHost));
+    for (int s = 0; s < count; ++s)
+        for (int e = 0; e < k; ++e) values[(size_t)s * k + e] += template_value(c, e);
     return TWOSD_OK;
 }
 

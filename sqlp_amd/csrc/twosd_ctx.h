@@ -105,6 +105,10 @@ struct twosd_ctx {
     int last_lp_N = 0, last_lp_blocks = 0;
     int64_t last_pivots_sum = 0;
     int last_pivots_max = 0;
+    // scenario distributions (on-device sampler)
+    bool has_dist = false;
+    int *d_dist_kind = nullptr, *d_dist_off = nullptr;
+    double *d_dist_val = nullptr, *d_dist_prob = nullptr, *d_dist_p0 = nullptr, *d_dist_p1 = nullptr, *d_dist_tmpl = nullptr;
     // epigraphs
     std::vector<twosd::EpiDevice> epis;
     // dual vertex set

@@ -111,6 +111,19 @@ hipError_t launch_lp(int R, const LpParams &p, int nblocks, size_t lds_bytes, hi
 size_t lp_lds_bytes(int R, int kmax);
 int lp_max_blocks_per_cu(int R, int kmax);
 
+// ---- on-device scenario sampler (sampler.hip)
+struct SampleParams {
+    int N, k;
+    unsigned long long seed, first_index;
+    const int *kind;                      // k: 0 DISCRETE, 1 NORMAL, 2 UNIFORM
+    const int *off;                       // k + 1: DISCRETE support ranges into val / prob
+    const double *val, *prob;             // DISCRETE support (ascending) and probabilities
+    const double *p0, *p1;                // NORMAL mean / sd, UNIFORM left / right
+    const double *tmpl;                   // k template values
+    double *out;                          // N x k deltas
+};
+hipError_t launch_sample(const SampleParams &S, hipStream_t st);
+
 // ---- host-side setup (host_basis.cpp) --------------------------------------------
 struct HostLP {
     int m = 0, n = 0;

@@ -149,6 +149,23 @@ class SDContext:
         check(self.lib.twosd_pool_get(self.h, int(p), ptr(head)))
         return head
 
+    # -- on-device scenario sampler (rand(rng, sto), smps_sto.jl:117-149) ----------
+    def set_distributions(self, sto):
+        """Upload the independent distribution of every random element (position order)."""
+        kinds, nsup, vals, probs, p0, p1 = [], [], [], [], [], []
+        for pos in self.positions:
+            d = sto.indep[pos]
+            if d[0] == "DISCRETE":
+                kinds.append(0); nsup.append(len(d[1])); vals += list(d[1]); probs += list(d[2])
+                p0.append(0.0); p1.append(0.0)
+            elif d[0] == "NORMAL":
+                kinds.append(1); nsup.append(0); p0.append(d[1]); p1.append(d[2])
+            else:
+                kinds.append(2); nsup.append(0); p0.append(d[1]); p1.append(d[2])
+        a = [np.ascontiguousarray(kinds, dtype=np.int32), np.ascontiguousarray(nsup, dtype=np.int32),
+             _f64(vals if vals else [0.0]), _f64(probs if probs else [0.0]), _f64(p0), _f64(p1)]
+        check(self.lib.twosd_set_distributions(self.h, self.k, *[ptr(v) for v in a]))
+
     def scenario_values(self, scenario) -> np.ndarray:
         """spSmpsScenario (list of position => value) -> value vector in layout order.
         Elements a scenario omits keep their template value (delta 0)."""
@@ -304,6 +321,24 @@ def add_scenarios(epi: sdEpigraph, values, weights=None):
     w = None if weights is None else _f64(weights)
     check(epi.ctx.lib.twosd_add_scenarios(epi.ctx.h, epi.index, N, ptr(values), ptr(w)))
     epi.scenario_weight.extend([1.0] * N if w is None else list(w))
+
+
+def add_sampled_scenarios(epi: sdEpigraph, N, seed, first_index=0, weights=None):
+    """N scenarios drawn on the device (Philox4x32-10 stream (seed, first_index + s, e))
+    appended to epi -- add_scenario!(epi, rand(rng, sto)) N times without a host copy."""
+    w = None if weights is None else _f64(weights)
+    check(epi.ctx.lib.twosd_add_sampled_scenarios(epi.ctx.h, epi.index, int(N), C.c_uint64(seed),
+                                                   C.c_uint64(first_index), ptr(w)))
+    epi.scenario_weight.extend([1.0] * N if w is None else list(w))
+
+
+def get_scenarios(epi: sdEpigraph, first=0, count=None) -> np.ndarray:
+    """Element values (template + stored delta) of scenarios [first, first+count)."""
+    if count is None:
+        count = epi.num_scenarios - first
+    out = np.zeros((count, epi.ctx.k))
+    check(epi.ctx.lib.twosd_get_scenarios(epi.ctx.h, epi.index, int(first), int(count), ptr(out)))
+    return out
 
 
 def solve_batch(epi: sdEpigraph, x, first=0, count=None, want_pi=True, want_y=False):

@@ -201,3 +201,42 @@ def test_extensive_form_kat(lands):
     c = np.concatenate([sp1.q] + [p[s] * sp2.q for s in range(len(S))])
     res = linprog(c, A_ub=np.vstack([-A[G], A[L]]), b_ub=np.concatenate([-b[G], b[L]]), method="highs")
     assert res.fun == pytest.approx(381.8533333, abs=1e-6)
+
+
+# ---- on-device sampler's oracle (oracle/sampler.c): Philox4x32-10 known answers ------------
+# Random123 kat_vectors (Salmon et al., SC'11) for philox4x32 with 10 rounds.
+PHILOX_KAT = [
+    ([0, 0, 0, 0], [0, 0], [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]),
+    ([0xffffffff] * 4, [0xffffffff] * 2, [0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd]),
+    ([0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344], [0xa4093822, 0x299f31d0],
+     [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]),
+]
+
+
+@pytest.mark.parametrize("ctr,key,expect", PHILOX_KAT)
+def test_philox_kat(ctr, key, expect):
+    from oracle import cpu
+    assert list(cpu.philox4x32_10(ctr, key)) == expect
+
+
+def test_sampler_oracle_distributions():
+    """rand(rng, sto) transforms (smps_sto.jl:117-130): DiscreteNonParametric frequencies
+    and sorted support, Normal(mean, sqrt(variance)), Uniform(left, right)."""
+    from oracle import cpu
+    from sqlp_amd.smps import spStoType, spSmpsPosition
+    sto = spStoType("t", {})
+    pa, pb, pc = spSmpsPosition("RHS", "A"), spSmpsPosition("RHS", "B"), spSmpsPosition("RHS", "C")
+    sto.indep[pa] = ("DISCRETE", [7.0, 3.0, 5.0], [0.3, 0.3, 0.4])     # unsorted support
+    sto.indep[pb] = ("NORMAL", 10.0, 4.0)                               # variance 4 -> sd 2
+    sto.indep[pc] = ("UNIFORM", -1.0, 3.0)
+    N = 200000
+    d = cpu.sample_deltas(sto, [pa, pb, pc], [0.0, 0.0, 0.0], N, seed=12345)
+    vals, cnt = np.unique(d[:, 0], return_counts=True)
+    assert list(vals) == [3.0, 5.0, 7.0]
+    np.testing.assert_allclose(cnt / N, [0.3, 0.4, 0.3], atol=0.005)   # probabilities follow the sorted support
+    assert abs(d[:, 1].mean() - 10.0) < 0.02 and abs(d[:, 1].std() - 2.0) < 0.02
+    assert d[:, 2].min() >= -1.0 and d[:, 2].max() < 3.0 and abs(d[:, 2].mean() - 1.0) < 0.01
+    # a stream is a function of (seed, index, element): shards reproduce it
+    d2 = np.vstack([cpu.sample_deltas(sto, [pa, pb, pc], [0.0] * 3, 1000, 12345, 0),
+                    cpu.sample_deltas(sto, [pa, pb, pc], [0.0] * 3, 1000, 12345, 1000)])
+    np.testing.assert_array_equal(d2, d[:2000])
