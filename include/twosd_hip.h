@@ -134,6 +134,13 @@ int twosd_add_sampled_scenarios(twosd_ctx *ctx, int epi, int N, uint64_t seed, u
                                 const double *weights);
 int twosd_get_scenarios(twosd_ctx *ctx, int epi, int first, int count, double *values);
 
+/* evaluate(sp1, sp2, sto, x; N) (smps_routines.jl:67-82), stage-2 part, on device-drawn
+ * scenarios [first, first+count) of the stream `seed` (a shard of N_total):
+ * *s2 = sum in index order of (1/N_total) * obj.  The caller adds c'x (and, across ranks,
+ * the shards' s2 in rank order).  TWOSD_E_LP if any LP is not optimal. */
+int twosd_evaluate_sampled(twosd_ctx *ctx, const double *x, int64_t N_total, int64_t first, int64_t count,
+                           uint64_t seed, double *s2);
+
 /*
  * solve_problem! (smps_routines.jl:50-62) for scenarios [first, first+count) of epigraph
  * `epi` at first-stage x[n1].  obj[count], status[count] required; pi[count*m2] and

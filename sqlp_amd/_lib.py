@@ -46,6 +46,7 @@ SIGNATURES = [
     ("twosd_set_distributions", I, [P, I, P, P, P, P, P, P]),
     ("twosd_add_sampled_scenarios", I, [P, I, I, C.c_uint64, C.c_uint64, P]),
     ("twosd_get_scenarios", I, [P, I, I, I, P]),
+    ("twosd_evaluate_sampled", I, [P, P, C.c_int64, C.c_int64, C.c_int64, C.c_uint64, P]),
     ("twosd_solve_batch", I, [P, I, P, I, I, P, P, P, P]),
     ("twosd_solve_values", I, [P, P, I, P, P, P, P, P]),
     ("twosd_dvs_push", I, [P, I, P, P, P]),

@@ -743,6 +743,42 @@ extern "C" int twosd_add_sampled_scenarios(twosd_ctx *c, int epi, int N, uint64_
     return TWOSD_OK;
 }
 
+static int copy_lp_outputs(twosd_ctx *c, int N, double *obj, double *pi, double *y, int *status);
+
+// evaluate(sp1, sp2, sto, x; N) stage-2 part (smps_routines.jl:67-82) on device-drawn
+// scenarios: *s2 = sum over scenarios first..first+count-1 of the stream `seed`, in index
+// order, of (1/N_total) * obj (s2_cost += 1/N*obj, :79).  Chunks of <= 1M scenarios:
+// sample into scratch, LP solve (objective only), objectives summed on the host in order.
+extern "C" int twosd_evaluate_sampled(twosd_ctx *c, const double *x, int64_t N_total, int64_t first, int64_t count,
+                                      uint64_t seed, double *s2) {
+    if (!c || !c->has_template) return fail(TWOSD_E_STATE, "evaluate_sampled: no template");
+    if (!c->has_basis) return fail(TWOSD_E_STATE, "evaluate_sampled: no warm-start basis");
+    if (!c->has_dist) return fail(TWOSD_E_STATE, "evaluate_sampled: no distributions (twosd_set_distributions)");
+    if (!s2 || N_total <= 0 || first < 0 || count < 0 || (c->n1 > 0 && !x)) return fail(TWOSD_E_ARG, "evaluate_sampled: bad arguments");
+    HIPCHK(hipSetDevice(c->device));
+    const int k = c->k;
+    const int64_t chunk = 1 << 20;
+    const double invN = 1.0 / (double)N_total;
+    double acc = 0.0;
+    std::vector<double> obj;
+    for (int64_t at = 0; at < count; at += chunk) {
+        const int n = (int)std::min(chunk, count - at);
+        int rc;
+        if ((rc = dgrow(&c->d_dvtmp, &c->dvtmp_cap, (size_t)n * std::max(k, 1), 0, c->stream))) return rc;
+        SampleParams S{};
+        S.N = n; S.k = k; S.seed = seed; S.first_index = (unsigned long long)(first + at);
+        S.kind = c->d_dist_kind; S.off = c->d_dist_off; S.val = c->d_dist_val; S.prob = c->d_dist_prob;
+        S.p0 = c->d_dist_p0; S.p1 = c->d_dist_p1; S.tmpl = c->d_dist_tmpl; S.out = c->d_dvtmp;
+        HIPCHK(launch_sample(S, c->stream));
+        if ((rc = run_lp(c, x, c->d_dvtmp, n, false, false))) return rc;
+        obj.resize(n);
+        if ((rc = copy_lp_outputs(c, n, obj.data(), nullptr, nullptr, nullptr))) return rc;
+        for (int i = 0; i < n; ++i) acc += invN * obj[i];
+    }
+    *s2 = acc;
+    return TWOSD_OK;
+}
+
 extern "C" int twosd_get_scenarios(twosd_ctx *c, int epi, int first, int count, double *values) {
     if (!c || epi < 0 || epi >= (int)c->epis.size()) return fail(TWOSD_E_ARG, "get_scenarios: bad epigraph");
     const EpiDevice &E = c->epis[epi];

@@ -58,6 +58,33 @@ def allgather_rows_ordered(rows: torch.Tensor) -> torch.Tensor:
     return torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
 
 
+def sum_in_rank_order(value: float) -> float:
+    """All-gather one fp64 per rank and sum in rank order (identical on every rank,
+    independent of the reduction tree).  Single rank: the value itself."""
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64)
+    if dist.get_backend() == "nccl":
+        t = t.cuda()
+    parts = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    acc = 0.0
+    for p in parts:
+        acc += float(p.item())
+    return acc
+
+
+def evaluate_sharded(ctx, first_stage_cost, x, N, seed):
+    """evaluate(sp1, sp2, sto, x; N) (smps_routines.jl:67-82) with the N device-drawn
+    scenarios of stream `seed` split over the ranks: c'x + sum of the shards' in-order
+    partial sums, combined in rank order."""
+    from . import twosd
+    rank, G = world()
+    lo, hi = shard_range(N, rank, G)
+    s2 = twosd.evaluate_sampled(ctx, np.zeros(len(x)), x, N, seed, lo, hi - lo)
+    return float(np.dot(first_stage_cost, x)) + sum_in_rank_order(s2)
+
+
 def build_cut_sharded(ctx, epi, x, total_weight, tie_rel, device):
     """build_sasa_cut over the scenarios of every rank: local partial on this GPU,
     all-reduce over RCCL, identical finalize on every rank.  Returns (alpha, beta)."""

@@ -371,6 +371,70 @@ def evaluate(ctx: SDContext, first_stage_cost, x, values):
     return float(np.dot(first_stage_cost, x)) + s2
 
 
+def evaluate_sampled(ctx: SDContext, first_stage_cost, x, N, seed, first=0, count=None):
+    """evaluate(sp1, sp2, sto, x; N) (smps_routines.jl:67-82) with the N scenarios drawn on
+    the device (needs ctx.set_distributions): c'x + sum_w (1/N) obj_w in scenario order.
+    first/count select a shard of the stream (the c'x term is added by every caller of
+    a shard; multi-GPU: sqlp_amd.dist.evaluate_sharded)."""
+    count = N - first if count is None else count
+    s2 = C.c_double()
+    check(ctx.lib.twosd_evaluate_sampled(ctx.h, ptr(_f64(x)), C.c_int64(N), C.c_int64(first), C.c_int64(count),
+                                         C.c_uint64(seed), C.byref(s2)))
+    return float(np.dot(first_stage_cost, x)) + s2.value
+
+
+def evaluate_epigraph(cuts, incumbent_cut, x, total_scenario_weight, lower_bound, sense=MIN_SENSE):
+    """Pointwise max (MIN sense) of the discounted cuts and the incumbent cut at x, floored by
+    the lower bound; no epigraph weight (epigraph.jl:177-203)."""
+    best = lower_bound
+    x = np.asarray(x, dtype=np.float64)
+    for cut in cuts:
+        discount = cut.weight_mark / total_scenario_weight
+        val = discount * (cut.alpha + float(np.dot(cut.beta, x))) + (1 - discount) * lower_bound
+        if (sense == MIN_SENSE and val > best) or (sense != MIN_SENSE and val < best):
+            best = val
+    if incumbent_cut is not None:
+        val = incumbent_cut.alpha + float(np.dot(incumbent_cut.beta, x))
+        if (sense == MIN_SENSE and val > best) or (sense != MIN_SENSE and val < best):
+            best = val
+    return best
+
+
+def evaluate_epigraph_weighted(epi: sdEpigraph, x, sense=MIN_SENSE):
+    """objective_weight * evaluate_epigraph over the epigraph's cuts (epigraph.jl:205-219)."""
+    return epi.objective_weight * evaluate_epigraph(epi.cuts, epi.incumbent_cut, x, epi.total_scenario_weight,
+                                                    epi.lower_bound, sense=sense)
+
+
+def evaluate_multi_epigraph(epis, x, sense=MIN_SENSE):
+    """Sum of the weighted epigraph values (epigraph.jl:221-228)."""
+    return sum(evaluate_epigraph_weighted(e, x, sense=sense) for e in epis)
+
+
+INCUMBENT_SELECTION_Q = 0.2
+
+
+@dataclass
+class sdImprovementInfo:
+    candidate_estimation: float
+    incumbent_estimation: float
+    required_improvement: float
+    is_improved: bool
+
+
+def check_improvement(f_last, f_current, f_cand, f_inc, x_candidate, x_incumbent, sense=MIN_SENSE):
+    """Incumbent selection (improvement.jl:19-49).  f_cand / f_inc are the values of the
+    common (first-stage) expression at the candidate / incumbent (evaluate_expr)."""
+    ce = evaluate_multi_epigraph(f_current, x_candidate, sense) + f_cand
+    ie = evaluate_multi_epigraph(f_current, x_incumbent, sense) + f_inc
+    lce = evaluate_multi_epigraph(f_last, x_candidate, sense) + f_cand
+    lie = evaluate_multi_epigraph(f_last, x_incumbent, sense) + f_inc
+    req_impr = INCUMBENT_SELECTION_Q * (lce - lie)
+    req = ie + req_impr
+    improved = ce < req if sense == MIN_SENSE else ce > req
+    return sdImprovementInfo(ce, ie, req_impr, improved)
+
+
 def argmax_procedure(epi: sdEpigraph, x, dual_vertices: sdDualVertexSet, tie_rel=DEFAULT_TIE_REL):
     """(max_val, max_arg) over every scenario of epi (subprob.jl:141-169); max_arg holds
     0-based vertex indices into dual_vertices (the reference returns Refs to vectors)."""

@@ -67,7 +67,8 @@ def _worker(rank, world, port, out):
     # ordered all-gather of per-rank new vertices (variable counts)
     mine = torch.arange(3 * (rank + 1) * m, dtype=torch.float64).reshape(-1, m) + 1000 * rank
     allrows = sdist.allgather_rows_ordered(mine)
-    out[rank] = (ht.numpy(), st.numpy(), alpha, beta, allrows.numpy())
+    ev = sdist.sum_in_rank_order(0.1 * (rank + 1))   # evaluate(): shards' partials in rank order
+    out[rank] = (ht.numpy(), st.numpy(), alpha, beta, allrows.numpy(), ev)
     dist.destroy_process_group()
 
 
@@ -89,7 +90,8 @@ def test_two_rank_cut_and_gather():
     m, n1, k, rows, cols, r, T, V, dv, w, x = _problem()
     h1, s1 = _partial(0, dv.shape[0], w.sum())
     for rank in (0, 1):
-        h, s, alpha, beta, allrows = res[rank]
+        h, s, alpha, beta, allrows, ev = res[rank]
+        assert ev == 0.0 + 0.1 + 0.2
         assert (h == h1).all()                         # exact: fixed point, order independent
         np.testing.assert_allclose(s, s1, rtol=1e-13, atol=1e-14)
         a1, b1 = sdist.finalize_from_partials(h1, s1, V, r, T, cols)

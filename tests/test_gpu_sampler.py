@@ -48,3 +48,27 @@ def test_device_sampler_sharding_and_solve():
     obj_h, _, _, st_h = ctx.solve_values(x, twosd.get_scenarios(a), want_pi=False)
     assert (st == 0).all() and (st_h == 0).all()
     np.testing.assert_allclose(obj_a, obj_h, rtol=1e-12)
+
+
+@pytest.mark.parametrize("name", ["lands", "storm"])
+def test_evaluate_sampled(name):
+    """evaluate(sp1, sp2, sto, x; N) on device-drawn scenarios == the same scenarios
+    (oracle stream) solved through solve_values and summed in order (smps_routines.jl:79)."""
+    from oracle import cpu
+    from sqlp_amd import smps, twosd
+    inst = I.load(name)
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    ctx.set_distributions(inst["sto"])
+    x = I.x_ev(name)
+    ctx.compute_basis(x, smps.mean_values(inst["sto"]))
+    c1 = np.ones(len(x))
+    N, seed = 30000, 4242
+    val = twosd.evaluate_sampled(ctx, c1, x, N, seed)
+    vals = cpu.sample_deltas(inst["sto"], ctx.positions, ctx.template_values, N, seed) + ctx.template_values
+    ref = twosd.evaluate(ctx, c1, x, vals)
+    assert abs(val - ref) <= 1e-10 * (1 + abs(ref))
+    # two shards of the stream add up to the whole
+    h = N // 3
+    s_a = twosd.evaluate_sampled(ctx, np.zeros(len(x)), x, N, seed, 0, h)
+    s_b = twosd.evaluate_sampled(ctx, np.zeros(len(x)), x, N, seed, h, N - h)
+    assert abs(float(np.dot(c1, x)) + s_a + s_b - val) <= 1e-10 * (1 + abs(val))
