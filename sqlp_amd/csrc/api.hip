@@ -960,7 +960,8 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
         const int kmax = c->kmax_override > 0 ? c->kmax_override : std::min(256, std::max(64, 2 * m + 32));
         const int ecap = std::max(4096, 32 * MP);
         const int CH = c->CH;
-        const int bpc = hyper_max_blocks_per_cu(R, CH, n + m, kmax, c->k);
+        int bpc = hyper_max_blocks_per_cu(R, CH, n + m, kmax, c->k);
+        if (const char *e = getenv("TWOSD_BPC")) bpc = std::min(bpc, std::max(1, atoi(e)));   // diagnostics: occupancy sweep
         if (bpc < 1) return fail(TWOSD_E_UNSUPPORTED, "LP kernel: LDS slice too large (m = %d, k = %d)", m, c->k);
         const int nblocks = std::max(1, std::min((N + kWavesPerBlock - 1) / kWavesPerBlock, bpc * c->num_cus));
         const size_t slots = (size_t)nblocks * kWavesPerBlock;

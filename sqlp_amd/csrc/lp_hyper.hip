@@ -71,12 +71,21 @@ __device__ __forceinline__ double h_infeas(double x, int bt) {
 
 template <int R>
 __device__ __forceinline__ int h_get_row_i(const int (&a)[R], int p) {
+    // one readlane per slot and a scalar select: a select chain over a[t] is folded by the
+    // compiler into a dynamically indexed load, which sends the whole array to scratch
     const int slot = p >> 6;
-    int v = a[0];
+    int v = 0;
 #pragma unroll
-    for (int t = 1; t < R; ++t)
-        if (t == slot) v = a[t];
-    return __builtin_amdgcn_readlane(v, p & 63);
+    for (int t = 0; t < R; ++t) {
+        const int u = __builtin_amdgcn_readlane(a[t], p & 63);
+        v = (t == slot) ? u : v;
+    }
+    return v;
+}
+
+// popcount of the bits of m below this lane (v_mbcnt; no per-lane mask register)
+__device__ __forceinline__ int h_prefix_count(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
 // per-wave LDS slice: a union of {ut, rho} (MP doubles each) and alpha (64C doubles, the
@@ -124,6 +133,16 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
     const uint64_t fixedm = P.fixedmask[lane];
     const uint64_t ubm = P.ubmask[lane];
 
+    // alpha back to zero over the ncol real columns: full slots unconditionally, the one
+    // partial slot by lane (uniform slot predicates: scalar branches, no exec-mask pairs)
+    const int ncol_full = ncol >> 6, ncol_rem = ncol & 63;
+    auto zero_alpha = [&]() {
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            if (c < ncol_full) alpha[64 * c + lane] = 0.0;
+            else if (c == ncol_full && lane < ncol_rem) alpha[64 * c + lane] = 0.0;
+        }
+    };
     for (int j = lane; j < hyper_union_doubles(R, ncol); j += 64) ut[j] = 0.0;
     h_wave_sync();
     STAMP_DECL
@@ -339,8 +358,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             if (thmax == INFINITY) {
                 status = TWOSD_LP_INFEASIBLE;
                 h_wave_sync();
-#pragma unroll
-                for (int c = 0; c < C; ++c) if (64 * c + lane < ncol) alpha[64 * c + lane] = 0.0;
+                zero_alpha();
                 break;
             }
             double bA = 0.0, bD = 0.0, bAs = 0.0;
@@ -357,8 +375,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             if (eq.key == 0.0) {
                 status = TWOSD_LP_NUMERIC;
                 h_wave_sync();
-#pragma unroll
-                for (int c = 0; c < C; ++c) if (64 * c + lane < ncol) alpha[64 * c + lane] = 0.0;
+                zero_alpha();
                 break;
             }
             const double thetaD = eq.p0 / eq.p1;
@@ -367,8 +384,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             for (int c = 0; c < C; ++c)
                 if (nzm & (1ull << c)) d[c] = fma(-thetaD, sg * alpha[64 * c + lane], d[c]);
             h_wave_sync();
-#pragma unroll
-            for (int c = 0; c < C; ++c) if (64 * c + lane < ncol) alpha[64 * c + lane] = 0.0;   // back to all-zero ut / rho
+            zero_alpha();   // back to all-zero ut / rho
             h_wave_sync();
             STAMP(6)
 
@@ -448,7 +464,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 const bool nz = col[t] != 0.0;
                 const uint64_t bal = __ballot(nz);
                 if (nz) {
-                    const int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
+                    const int pos = base + h_prefix_count(bal);
                     const double ratio = col[t] * inv_arq;
                     eidx[pos] = i;
                     evals[pos] = (i == r) ? inv_arq : -ratio;
@@ -489,9 +505,13 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             }
             if (lane == (r & 63)) {
                 const int rs = r >> 6;
+                const int nh = q * 4 + (int)P.btype[q];
 #pragma unroll
-                for (int t = 0; t < R; ++t)
-                    if (t == rs) hb[t] = q * 4 + (int)P.btype[q];
+                for (int t = 0; t < R; ++t) {
+                    int v = (t == rs) ? nh : hb[t];
+                    asm volatile("" : "+v"(v));   // per-slot select kept: no dynamic store into hb
+                    hb[t] = v;
+                }
             }
             ++it;
             h_wave_sync();
@@ -706,6 +726,12 @@ static int ho(size_t lds) {
     return nb > 0 ? nb : 1;
 }
 
+#ifdef HYP_DEV_STORM_ONLY   // development builds: the storm instance (R = 9, C = 32) only
+#define HYPER_C_SWITCH(R, FN, ...)                  \
+    switch (C) {                                    \
+        case 32: if (R == 9) return FN<9, 32>(__VA_ARGS__); \
+    }
+#else
 #define HYPER_C_SWITCH(R, FN, ...)                  \
     switch (C) {                                    \
         case 2: return FN<R, 2>(__VA_ARGS__);       \
@@ -715,6 +741,7 @@ static int ho(size_t lds) {
         case 32: return FN<R, 32>(__VA_ARGS__);     \
         case 64: return FN<R, 64>(__VA_ARGS__);     \
     }
+#endif
 
 hipError_t launch_hyper(int R, int C, const HyperParams &p, int nblocks, size_t lds, hipStream_t s) {
     switch (R) {
