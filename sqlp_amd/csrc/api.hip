@@ -883,6 +883,7 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
     if (P > 1 && c->CH > 0) {
         std::vector<int8_t> bt(c->L.n + m);
         HIPCHK(hipMemcpy(bt.data(), c->d_btype, bt.size(), hipMemcpyDeviceToHost));
+        if (const char *e = getenv("TWOSD_SEL_CW")) c->sel_cw = (float)atof(e);   // selection-key experiments
         std::vector<float> cinf(P, 0.0f);
         std::vector<int> sptr(1, 0), scode;   // interleaved (code, float bits) records
         auto rec = [&](int code, double v) {
@@ -900,7 +901,11 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
                 const int t = bt[B.head[i]];
                 const double xv = xb[(size_t)p * MP + i];
                 const int q0 = B.kptr[i], q1 = B.kptr[i + 1];
-                if (q0 == q1) { cinf[p] += (float)std::fabs(host_infeas(xv, t)); continue; }
+                if (q0 == q1) {
+                    const double f = std::fabs(host_infeas(xv, t));
+                    cinf[p] += (float)f + (f > 0.0 ? c->sel_cw : 0.0f);
+                    continue;
+                }
                 if (box) {
                     // interval of x_i over the training box of the deltas: a row that stays
                     // feasible on the whole box never contributes, so it is left out
@@ -1012,6 +1017,7 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
             S.kcoef = c->d_kcoef;
             S.cinf = c->d_sel_cinf; S.sptr = c->d_sel_ptr; S.rec = reinterpret_cast<const int2 *>(c->d_sel_code);
             S.pick = c->d_pool_pick;
+            S.cw = c->sel_cw;
             HIPCHK(launch_pool_select(S, c->stream));
             size_t tb = 0;
             HIPCHK(sort_by_pool(c->d_pool_pick, nullptr, N, H.npool, nullptr, &tb, c->stream));

@@ -617,10 +617,12 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
 // The selection is a heuristic (any pool basis is a valid start; the choice only changes
 // pivot counts), so it runs in fp32: half the LDS traffic of the staged deltas, 8-byte
 // records (code, value) -- deterministic like everything else.
-__device__ __forceinline__ float h_infeas_f(float x, int bt) {
-    if (bt == BT_Y || bt == BT_L) return x < -1e-9f ? -x : 0.0f;
-    if (bt == BT_G) return x > 1e-9f ? x : 0.0f;
-    return fabsf(x) > 1e-9f ? fabsf(x) : 0.0f;
+__device__ __forceinline__ float h_infeas_f(float x, int bt, float cw) {
+    float v;
+    if (bt == BT_Y || bt == BT_L) v = x < -1e-9f ? -x : 0.0f;
+    else if (bt == BT_G) v = x > 1e-9f ? x : 0.0f;
+    else v = fabsf(x) > 1e-9f ? fabsf(x) : 0.0f;
+    return v > 0.0f ? v + cw : 0.0f;
 }
 
 constexpr int kSelWaves = 16;   // 16 waves share one staged 64-scenario tile (latency hiding)
@@ -649,7 +651,7 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_select_kernel(PoolSelPara
         const int j0 = S.sptr[p], j1 = S.sptr[p + 1];
         auto step = [&](int code, float v, float dl) {
             if (code < 0) {
-                if (bt >= 0) inf += h_infeas_f(x, bt);
+                if (bt >= 0) inf += h_infeas_f(x, bt, S.cw);
                 x = v;
                 bt = -1 - code;
             } else {
@@ -674,7 +676,7 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_select_kernel(PoolSelPara
             const int2 r = S.rec[j];
             step(r.x, __int_as_float(r.y), dvt[(r.x < 0 ? 0 : r.x) * 65 + lane]);
         }
-        if (bt >= 0) inf += h_infeas_f(x, bt);
+        if (bt >= 0) inf += h_infeas_f(x, bt, S.cw);
         if (inf < best) { best = inf; bp = p; }
     }
     bsum[wid][lane] = best;

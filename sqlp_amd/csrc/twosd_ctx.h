@@ -57,6 +57,7 @@ struct twosd_ctx {
     float *d_sel_cinf = nullptr;
     int *d_sel_ptr = nullptr, *d_sel_code = nullptr;   // code: (code, float bits) record pairs
     int64_t sel_nnz = 0, sel_rows = 0;
+    float sel_cw = 0.0f;                 // pool selection key: sum |infeas| + sel_cw * #infeasible rows
     std::vector<double> sel_lo, sel_hi;   // training box of the deltas (empty: no row pruning)
     int *d_bnnz = nullptr;        // npool: nnz of each pool B^{-1} (FMA accounting)
     int *d_head_out = nullptr, *d_pool_pick = nullptr;   // optional LP outputs (pool building)

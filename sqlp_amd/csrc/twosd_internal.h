@@ -95,6 +95,7 @@ struct PoolSelParams {
     const int2 *rec;                                    // (code, float bits): row start (-1 - bound type,
                                                         //   xbase_i); entry (e, B^{-1}[i][row_e])
     int *pick;                                          // N out
+    float cw;                                           // key = sum |infeas| + cw * #infeasible rows
 };
 size_t pool_select_lds_bytes(int k);
 // stable sort of scenarios [0, N) by pool pick -> order (pool_sort.hip); tmp == nullptr: size query
