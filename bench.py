@@ -50,6 +50,33 @@ def chunked_values(sto, positions, lo, hi, seed):
     return out
 
 
+def importance_values(sto, positions, lo, hi, seed, scale):
+    """Scenarios [lo, hi) of an importance-sampled stream (config C5): every NORMAL element
+    drawn from N(mu, (scale sigma)^2), other elements from their own distribution; weight =
+    likelihood ratio target / proposal (per-chunk seeds: sharding-invariant)."""
+    from sqlp_amd import smps
+    k = len(positions)
+    vals = chunked_values(sto, positions, lo, hi, seed)
+    out_w = np.ones(hi - lo)
+    c0, c1 = lo // CHUNK, (hi - 1) // CHUNK
+    for j, pos in enumerate(positions):
+        dist = sto.indep[pos]
+        if dist[0] != "NORMAL":
+            continue
+        mu, sd = dist[1], np.sqrt(dist[2])     # NORMAL(mean, variance), smps_sto.jl:122-125
+        z = np.empty(hi - lo)
+        for c in range(c0, c1 + 1):
+            a, b = c * CHUNK, (c + 1) * CHUNK
+            zz = np.random.default_rng([seed, c, j, 7]).standard_normal(CHUNK)
+            s_, e_ = max(a, lo), min(b, hi)
+            z[s_ - lo:e_ - lo] = zz[s_ - a:e_ - a]
+        v = mu + scale * sd * z
+        vals[:, j] = v
+        out_w *= scale * np.exp(-0.5 * z * z * (scale * scale) + 0.5 * z * z)
+    del k
+    return vals, out_w
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -67,6 +94,12 @@ def main():
     ap.add_argument("--pool-train", type=int, default=16384, help="training scenarios of the pool build")
     ap.add_argument("--sampler", choices=["device", "host"], default="device",
                     help="scenario draws: on-device Philox4x32-10 sampler (twosd_add_sampled_scenarios) or numpy PCG64")
+    ap.add_argument("--epigraphs", type=int, default=1,
+                    help="E > 1: config C5 shape -- E epigraphs (objective weight 1/E), N/E scenarios each, "
+                         "one shared vertex set, one cut per epigraph per step")
+    ap.add_argument("--importance-scale", type=float, default=0.0,
+                    help="s > 0: importance sampling of NORMAL elements from N(mu, (s sigma)^2) with "
+                         "likelihood-ratio weights passed as add_scenario! weights (host draws)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -112,13 +145,32 @@ def main():
     t_pool = time.perf_counter() - t_pool
 
     N = args.scenarios
-    lo, hi = sdist.shard_range(N, rank, world)
-    n_local = hi - lo
+    E = max(1, args.epigraphs)
+    if N % E:
+        raise SystemExit("--scenarios must be a multiple of --epigraphs")
+    NE = N // E                    # scenarios per epigraph (global)
+    lo, hi = sdist.shard_range(NE, rank, world)
+    n_local = hi - lo              # per epigraph on this rank
     t_gen = time.perf_counter()
-    epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
-    scenarios(epi, lo, hi, args.seed)
+    epis, total_weights = [], []
+    for e in range(E):
+        epi_e = twosd.sdEpigraph(ctx, 1.0 / E, 0.0)
+        if args.importance_scale > 0:
+            vals, w = importance_values(sto, positions, lo, hi, args.seed + 101 * (e + 1), args.importance_scale)
+            twosd.add_scenarios(epi_e, vals, w)
+            # global total weight: sum over the ranks' shards (host all-reduce of one number)
+            tw = float(w.sum())
+            if world > 1:
+                t = torch.tensor([tw], dtype=torch.float64, device=device)
+                torch.distributed.all_reduce(t)
+                tw = float(t.item())
+            total_weights.append(tw)
+        else:
+            scenarios(epi_e, lo, hi, args.seed + 101 * e)
+            total_weights.append(float(NE))   # all weights 1.0 (sd_iteration! uses 1.0, algorithm.jl:46)
+        epis.append(epi_e)
+    epi = epis[0]
     t_gen = time.perf_counter() - t_gen
-    total_weight = float(N)        # all weights 1.0 (sd_iteration! uses 1.0, algorithm.jl:46)
 
     # |V| pool: duals of the first scenarios of the global stream seed + 1 (identical on every rank)
     V = twosd.sdDualVertexSet(ctx)
@@ -133,18 +185,22 @@ def main():
         V.truncate(args.vertices)
     nv = len(V)
 
-    def step():
+    def step(rec=None):
         ctx.invalidate_x()     # every pass pays its per-x setup (x_B of the pool, selection data)
-        if args.no_dedup:
-            twosd.solve_batch(epi, x, 0, n_local, want_pi=False)
-        else:
-            twosd.solve_push(epi, x, 0, n_local)
-            V.truncate(nv)
-        if world == 1:
-            cut = twosd.build_sasa_cut(epi, x, V, args.tie_rel)
-            return cut.alpha
-        a, _ = sdist.build_cut_sharded(ctx, epi, x, total_weight, args.tie_rel, device)
-        return a
+        alpha = 0.0
+        for epi_e, tw in zip(epis, total_weights):
+            if args.no_dedup:
+                twosd.solve_batch(epi_e, x, 0, n_local, want_pi=False)
+            else:
+                twosd.solve_push(epi_e, x, 0, n_local)
+                V.truncate(nv)
+            if world == 1:
+                alpha += twosd.build_sasa_cut(epi_e, x, V, args.tie_rel).alpha / E
+            else:
+                alpha += sdist.build_cut_sharded(ctx, epi_e, x, tw, args.tie_rel, device)[0] / E
+            if rec:
+                rec()      # per-epigraph kernel timings (HIP events of the last calls)
+        return alpha
 
     def barrier():
         torch.cuda.synchronize(device)
@@ -155,20 +211,21 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier()
-    t_lp = t_dd = t_cut = t_fin = t_sel = 0.0
-    flops_lp = 0.0
-    piv_sum = 0
-    piv_max = 0
+    acc = {"lp": 0.0, "dd": 0.0, "cut": 0.0, "fin": 0.0, "sel": 0.0, "flops": 0.0, "piv": 0, "pmax": 0}
+
+    def record():
+        tm = ctx.timings_us()
+        acc["lp"] += tm[0]; acc["dd"] += tm[1]; acc["cut"] += tm[2]; acc["fin"] += tm[3]; acc["sel"] += tm[4]
+        acc["flops"] += ctx.lp_flops()
+        ps, pm = ctx.lp_stats()
+        acc["piv"] += ps; acc["pmax"] = max(acc["pmax"], pm)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        alpha = step()
-        tm = ctx.timings_us()
-        t_lp += tm[0]; t_dd += tm[1]; t_cut += tm[2]; t_fin += tm[3]; t_sel += tm[4]
-        flops_lp += ctx.lp_flops()
-        ps, pm = ctx.lp_stats()
-        piv_sum += ps; piv_max = max(piv_max, pm)
+        alpha = step(record)
     barrier()
     elapsed = time.perf_counter() - t0
+    t_lp, t_dd, t_cut, t_fin, t_sel = acc["lp"], acc["dd"], acc["cut"], acc["fin"], acc["sel"]
+    flops_lp, piv_sum, piv_max = acc["flops"], acc["piv"], acc["pmax"]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -179,13 +236,14 @@ def main():
 
     k = len(positions)
     m = sp2.shape[0]
+    passes = K * E                 # LP launches / cut passes in the timed region
     # LP kernel (dominant): counted fp64 FLOPs of the executed pivot path per launch
-    lp_us = t_lp / K
-    lp_tflops = (flops_lp / K) / (lp_us * 1e-6) / 1e12
+    lp_us = t_lp / passes
+    lp_tflops = (flops_lp / passes) / (lp_us * 1e-6) / 1e12
     # cut-gen (argmax + partial sums): algorithmic bytes / flops per pass
     bytes_alg = 8 * n_local * k + 8 * n_local + 12 * n_local + 8 * nv * (m + 1)
     flops_alg = 2 * n_local * nv * k + 2 * nv * m
-    cut_us = t_cut / K
+    cut_us = t_cut / passes
     cut_gbs = bytes_alg / (cut_us * 1e-6) / 1e9
     t_roof = max(bytes_alg / (PEAK_HBM_GBS * 1e9), flops_alg / (PEAK_FP64_TFS * 1e12))
 
@@ -204,14 +262,16 @@ def main():
         "data": (f"synthetic: i.i.d. scenarios of {name}.sto drawn on the device (Philox4x32-10, seed {args.seed}, "
                  f"{t_gen:.2f} s for the shard)" if args.sampler == "device" else
                  f"synthetic: i.i.d. scenarios of {name}.sto (numpy PCG64, seed {args.seed})") + ", x = EV solution",
-        "config": {"workload": f"{name} {N} scenarios sharded over {world} GPU(s), |V|={nv}, "
+        "config": {"workload": f"{name} {N} scenarios" + (f" in {E} epigraphs" if E > 1 else "") +
+                               (f" (importance-sampled, scale {args.importance_scale})" if args.importance_scale > 0 else "") +
+                               f" sharded over {world} GPU(s), |V|={nv}, "
                                f"warm-start pool {pool_size}, LP solve + dual dedup + build_sasa_cut per step",
-                   "instance": name, "scenarios": N, "vertices": nv, "k": k, "m2": m,
+                   "instance": name, "scenarios": N, "epigraphs": E, "vertices": nv, "k": k, "m2": m,
                    "basis_pool": pool_size, "pool_build_s": round(t_pool, 3),
                    "parallelism": f"scenario-dp{world}"},
-        "phases_ms_per_step": {"pool_select": t_sel / K / 1e3, "lp_kernel": lp_us / 1e3, "dedup": t_dd / K / 1e3, "cut_partial": cut_us / 1e3,
-                               "cut_finalize": t_fin / K / 1e3},
-        "lp_pivots_mean": piv_sum / (K * n_local), "lp_pivots_max": piv_max,
+        "phases_ms_per_step": {"pool_select": t_sel / K / 1e3, "lp_kernel": t_lp / K / 1e3, "dedup": t_dd / K / 1e3,
+                               "cut_partial": t_cut / K / 1e3, "cut_finalize": t_fin / K / 1e3},
+        "lp_pivots_mean": piv_sum / (passes * n_local), "lp_pivots_max": piv_max,
         "roofline": {"kernel": "lp_hyper_kernel", "bound": "mfma",
                      "note": "fp64 peak (vector == matrix on gfx950); achieved = counted fp64 FLOPs of the executed pivot path / LP kernel time",
                      "achieved": lp_tflops, "peak": PEAK_FP64_TFS, "unit": "TFLOP/s",

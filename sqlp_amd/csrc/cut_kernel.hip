@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 #include "twosd_ctx.h"
 
@@ -39,8 +40,11 @@ constexpr int kCutTile = 64;       // scenarios per block tile (4 waves x one MF
 constexpr int kLdsStride = 48;     // doubles per k-row in LDS (== 16 mod 32: conflict-free b64 reads)
 constexpr double kFix = 4611686018427387904.0;   // 2^62 fixed-point scale of p_w
 
+constexpr int kHistLds = 256;      // |V| up to this: the block histogram lives in LDS
+
 struct CutParams {
     int N, k, k4, nv, vcap, m;
+    int hist_lds;          // 1: per-block LDS histogram (nv <= kHistLds), flushed once per block
     double tie_rel, inv_total;
     const double *dv;      // N x k
     const double *w;       // N
@@ -50,6 +54,7 @@ struct CutParams {
     const double *base;    // nv
     int *arg; double *val; int *flag;   // N
     unsigned long long *hist;           // nv (fixed point)
+    unsigned long long *hist_part;      // gridDim.x x nv block histograms (hist_lds mode)
     double *partial;       // slots x (k + 1): [sum p*val, S_0..S_{k-1}]
 };
 
@@ -105,8 +110,11 @@ template <int KB>
 __global__ void __launch_bounds__(256, 2) cut_argmax_kernel(CutParams P) {
     __shared__ double Bs[4 * KB * kLdsStride];
     __shared__ double bs[kVT];
+    extern __shared__ unsigned long long hl[];   // nv entries when P.hist_lds
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
+    if (P.hist_lds)
+        for (int v = threadIdx.x; v < P.nv; v += 256) hl[v] = 0ull;   // ordered before use by the chunk barriers
     const int g = lane >> 4, j = lane & 15;
     const int ntiles = (P.N + kCutTile - 1) / kCutTile;
     const int nchunks = (P.nv + kVT - 1) / kVT;
@@ -208,7 +216,10 @@ __global__ void __launch_bounds__(256, 2) cut_argmax_kernel(CutParams P) {
                 P.flag[s] = rb[r].F;
             }
         }
-        // partial sums: loop the 16 rows of this wave (uniform)
+        // partial sums over the 16 rows of this wave, branch-free so every row's loads are in
+        // flight together: an undecided row (flagged, no vertex, past N) gets p = 0 and vertex 0
+        // (adds exact zeros).  The vertex histogram goes to LDS (small |V|: no contention on a
+        // few global addresses) or global atomics; both uint64 fixed point: exact.
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
 #pragma unroll
@@ -217,19 +228,26 @@ __global__ void __launch_bounds__(256, 2) cut_argmax_kernel(CutParams P) {
                 const int ai = __shfl(rb[r].I, gg * 16);
                 const int fl = __shfl(rb[r].F, gg * 16);
                 const double vl = __shfl(rb[r].SV, gg * 16);
-                if (s >= P.N || fl || ai < 0) continue;
-                const double p = P.w[s] * P.inv_total;
-                if (lane == 0) {
+                const bool ok = s < P.N && !fl && ai >= 0;
+                const int au = ok ? ai : 0, su = min(s, P.N - 1);
+                const double p = ok ? P.w[su] * P.inv_total : 0.0;
+                if (lane == 0 && ok) {
                     pv_sum = fma(p, vl, pv_sum);
-                    atomicAdd(&P.hist[ai], (unsigned long long)__double2ull_rn(p * kFix));
+                    const unsigned long long hq = (unsigned long long)__double2ull_rn(p * kFix);
+                    if (P.hist_lds) __hip_atomic_fetch_add(&hl[au], hq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    else atomicAdd(&P.hist[au], hq);
                 }
 #pragma unroll
                 for (int t = 0; t < 2; ++t) {
                     const int e = lane + 64 * t;
-                    if (e < P.k) Sacc[t] = fma(p * P.PK[(size_t)ai * P.k4 + e], P.dv[(size_t)s * P.k + e], Sacc[t]);
+                    if (e < P.k) Sacc[t] = fma(p * P.PK[(size_t)au * P.k4 + e], P.dv[(size_t)su * P.k + e], Sacc[t]);
                 }
             }
         }
+    }
+    if (P.hist_lds) {   // block histogram -> its own slot (summed by cut_hist_reduce_kernel)
+        __syncthreads();
+        for (int v = threadIdx.x; v < P.nv; v += 256) P.hist_part[(size_t)blockIdx.x * P.nv + v] = hl[v];
     }
     const int slot = blockIdx.x * 4 + wid;
     double *out = P.partial + (size_t)slot * (P.k + 1);
@@ -239,6 +257,16 @@ __global__ void __launch_bounds__(256, 2) cut_argmax_kernel(CutParams P) {
         const int e = lane + 64 * t;
         if (e < P.k) out[1 + e] = Sacc[t];
     }
+}
+
+// hist[v] += sum over blocks of the block histograms (integers: exact in any order)
+__global__ void __launch_bounds__(256) cut_hist_reduce_kernel(int nb, int nv, const unsigned long long *__restrict__ part,
+                                                              unsigned long long *__restrict__ hist) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nv) return;
+    unsigned long long s = 0;
+    for (int b = 0; b < nb; ++b) s += part[(size_t)b * nv + v];
+    hist[v] += s;
 }
 
 // exact two-pass rule for flagged scenarios; one wavefront per scenario
@@ -355,7 +383,8 @@ struct CutWs {
     double *gpart = nullptr, *g = nullptr;
     int *arg = nullptr, *flag = nullptr;
     double *val = nullptr;
-    unsigned long long *hist = nullptr;
+    unsigned long long *hist = nullptr, *hist_part = nullptr;
+    size_t hpart_cap = 0;
     double *part2 = nullptr;
     size_t base_cap = 0, part_cap = 0, n_cap = 0, hist_cap = 0, gpart_cap = 0, sums_cap = 0, part2_cap = 0;
     int m = 0, vec_m = 0;
@@ -372,7 +401,7 @@ void cut_free(twosd_ctx *c) {
     CutWs *w = (CutWs *)c->cut_ws;
     hipFree(w->PK); hipFree(w->PKT); hipFree(w->rows); hipFree(w->coef); hipFree(w->bvec); hipFree(w->base);
     hipFree(w->partial); hipFree(w->sums); hipFree(w->gpart); hipFree(w->g); hipFree(w->arg); hipFree(w->flag);
-    hipFree(w->val); hipFree(w->hist); hipFree(w->part2);
+    hipFree(w->val); hipFree(w->hist); hipFree(w->part2); hipFree(w->hist_part);
     delete w;
     c->cut_ws = nullptr;
 }
@@ -409,7 +438,8 @@ static int kb_for(int k4) {
 
 template <int KB>
 static void launch_argmax_t(const CutParams &P, int nblocks, hipStream_t s) {
-    hipLaunchKernelGGL(cut_argmax_kernel<KB>, dim3(nblocks), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(cut_argmax_kernel<KB>, dim3(nblocks), dim3(256), P.hist_lds ? sizeof(unsigned long long) * P.nv : 0,
+                       s, P);
 }
 
 static void launch_argmax(int KB, const CutParams &P, int nblocks, hipStream_t s) {
@@ -505,10 +535,20 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
                        c->dvs.V, w->bvec, w->base);
     CutParams P{};
     P.N = N; P.k = k; P.k4 = k4; P.nv = nv; P.vcap = w->pk_vcap; P.m = m;
+    static const int hist_lds_max = getenv("TWOSD_HIST_LDS") ? atoi(getenv("TWOSD_HIST_LDS")) : kHistLds;
+    P.hist_lds = nv <= hist_lds_max ? 1 : 0;
+    if (P.hist_lds && (size_t)nblocks * nv > w->hpart_cap) {
+        if ((rc = realloc_dev(&w->hist_part, (size_t)nblocks * nv))) return rc;
+        w->hpart_cap = (size_t)nblocks * nv;
+    }
+    P.hist_part = w->hist_part;
     P.tie_rel = tie_rel; P.inv_total = 1.0 / total_weight;
     P.dv = E.d_dv; P.w = E.d_w; P.coef = w->coef; P.PK = w->PK; P.PKT = w->PKT; P.base = w->base;
     P.arg = w->arg; P.val = w->val; P.flag = w->flag; P.hist = d_hist; P.partial = w->partial;
     launch_argmax(KB, P, nblocks, c->stream);
+    if (P.hist_lds)
+        hipLaunchKernelGGL(cut_hist_reduce_kernel, dim3((nv + 255) / 256), dim3(256), 0, c->stream, nblocks, nv, w->hist_part,
+                           d_hist);
     hipLaunchKernelGGL(cut_fixup_kernel, dim3(fix_blocks), dim3(256), 0, c->stream, P, nblocks * 4);
     if ((size_t)(k + 1) * kReduceBlocks > w->part2_cap) {
         if ((rc = realloc_dev(&w->part2, (size_t)(k + 1) * kReduceBlocks))) return rc;
