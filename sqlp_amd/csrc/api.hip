@@ -848,9 +848,40 @@ static double host_infeas(double x, int bt) {
     return std::fabs(x) > tol ? x : 0.0;
 }
 
+// copy n host elements to a device array grown only when n exceeds its capacity
+template <typename T>
+static int upload_cap(T **d, size_t *cap, const T *h, size_t n) {
+    if (!*d || n > *cap) {
+        const size_t nc = std::max<size_t>(n, 1);
+        int rc = dalloc(d, nc);
+        if (rc) return rc;
+        *cap = nc;
+    }
+    if (n) HIPCHK(hipMemcpy(*d, h, sizeof(T) * n, hipMemcpyHostToDevice));
+    return TWOSD_OK;
+}
+
+// run fn(p) for p in [0, P) on up to 16 host threads (every p independent: the result does not
+// depend on the thread count)
+template <typename F>
+static void parallel_over(int P, F fn) {
+    const int nth = (int)std::max(1u, std::min({16u, std::thread::hardware_concurrency(), (unsigned)std::max(P / 8, 1)}));
+    if (nth == 1) {
+        for (int p = 0; p < P; ++p) fn(p);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nth; ++t)
+        th.emplace_back([&, t]() {
+            for (int p = t; p < P; p += nth) fn(p);
+        });
+    for (auto &t : th) t.join();
+}
+
 // per-x shared data: b = r - T x; per pool basis xbase_p = B_p^{-1} b (sparse rows);
 // coef_e(x); dense B0K[e] = coef_e B0^{-1}[:, row_e] for the dense kernel; with a pool, the
-// selection stream (active rows that can turn infeasible on the training box of the deltas)
+// selection stream (active rows that can turn infeasible on the training box of the deltas).
+// Every pool basis is independent, so the per-basis work runs on host threads.
 int twosd::prepare_x(twosd_ctx *c, const double *x) {
     const int m = c->L.m, MP = c->MP, k = c->k, n1 = c->n1;
     if (c->prep_valid && c->prep_x.size() == (size_t)n1 && (n1 == 0 || std::equal(c->prep_x.begin(), c->prep_x.end(), x)))
@@ -862,72 +893,89 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
     const int P = (int)c->pool.size();
     std::vector<double> coef(std::max(k, 1), 1.0);
     for (int e = 0; e < k; ++e) coef[e] = c->pos_col[e] < 0 ? 1.0 : -x[c->pos_col[e]];
-    std::vector<double> xb((size_t)P * MP, 0.0), bk((size_t)std::max(k, 1) * MP, 0.0);
-    for (int p = 0; p < P; ++p) {
+    std::vector<double> xb((size_t)P * MP, 0.0);
+    const bool sel = P > 1 && c->CH > 0;
+    std::vector<int8_t> bt;
+    if (sel) {
+        bt.resize(c->L.n + m);
+        HIPCHK(hipMemcpy(bt.data(), c->d_btype, bt.size(), hipMemcpyDeviceToHost));
+        if (const char *e = getenv("TWOSD_SEL_CW")) c->sel_cw = (float)atof(e);   // selection-key experiments
+    }
+    std::vector<float> cinf(P, 0.0f);
+    std::vector<std::vector<int>> pcode(sel ? P : 0);   // per basis: interleaved (code, float bits) records
+    std::vector<int64_t> prows(P, 0);
+    const bool box = !c->sel_lo.empty();
+    parallel_over(P, [&](int p) {
         const PoolBasis &B = c->pool[p];
+        double *xp = xb.data() + (size_t)p * MP;
         for (int i = 0; i < m; ++i) {
             double s = 0.0;
             for (int q = B.rptr[i]; q < B.rptr[i + 1]; ++q) s += B.rval[q] * b[B.rcol[q]];
-            xb[(size_t)p * MP + i] = s;
+            xp[i] = s;
         }
-    }
-    for (int e = 0; e < k; ++e) {
-        const int rr = c->pos_row[e];
-        for (int i = 0; i < m; ++i) bk[(size_t)e * MP + i] = coef[e] * c->B0inv[(size_t)i * m + rr];
-    }
-    if ((rc = dalloc(&c->d_B0K, (size_t)std::max(k, 1) * MP)) || (rc = dalloc(&c->d_xbase, (size_t)P * MP)) ||
-        (rc = upload(&c->d_kcoef, coef)))
-        return rc;
-    HIPCHK(hipMemcpy(c->d_xbase, xb.data(), sizeof(double) * xb.size(), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->d_B0K, bk.data(), sizeof(double) * std::max(k, 1) * MP, hipMemcpyHostToDevice));
-    if (P > 1 && c->CH > 0) {
-        std::vector<int8_t> bt(c->L.n + m);
-        HIPCHK(hipMemcpy(bt.data(), c->d_btype, bt.size(), hipMemcpyDeviceToHost));
-        if (const char *e = getenv("TWOSD_SEL_CW")) c->sel_cw = (float)atof(e);   // selection-key experiments
-        std::vector<float> cinf(P, 0.0f);
-        std::vector<int> sptr(1, 0), scode;   // interleaved (code, float bits) records
+        if (!sel) return;
+        std::vector<int> &sc = pcode[p];
         auto rec = [&](int code, double v) {
             const float f = (float)v;
             int bits;
             std::memcpy(&bits, &f, 4);
-            scode.push_back(code);
-            scode.push_back(bits);
+            sc.push_back(code);
+            sc.push_back(bits);
         };
-        c->sel_rows = 0;
-        const bool box = !c->sel_lo.empty();
-        for (int p = 0; p < P; ++p) {
-            const PoolBasis &B = c->pool[p];
-            for (int i = 0; i < m; ++i) {
-                const int t = bt[B.head[i]];
-                const double xv = xb[(size_t)p * MP + i];
-                const int q0 = B.kptr[i], q1 = B.kptr[i + 1];
-                if (q0 == q1) {
-                    const double f = std::fabs(host_infeas(xv, t));
-                    cinf[p] += (float)f + (f > 0.0 ? c->sel_cw : 0.0f);
-                    continue;
-                }
-                if (box) {
-                    // interval of x_i over the training box of the deltas: a row that stays
-                    // feasible on the whole box never contributes, so it is left out
-                    double lo = xv, hi = xv, mag = std::fabs(xv);
-                    for (int q = q0; q < q1; ++q) {
-                        const double g = coef[B.ke[q]] * B.kraw[q];
-                        const double a = g * c->sel_lo[B.ke[q]], bb = g * c->sel_hi[B.ke[q]];
-                        lo += std::min(a, bb);
-                        hi += std::max(a, bb);
-                        mag += std::max(std::fabs(a), std::fabs(bb));
-                    }
-                    const double tol = 1e-9 + 1e-12 * mag;
-                    const bool feasible_box = (t == BT_Y || t == BT_L) ? lo > tol : (t == BT_G) ? hi < -tol : false;
-                    if (std::isfinite(lo) && std::isfinite(hi) && feasible_box) continue;
-                }
-                rec(-1 - t, xv);
-                ++c->sel_rows;
-                for (int q = q0; q < q1; ++q) rec(B.ke[q], B.kraw[q]);
+        for (int i = 0; i < m; ++i) {
+            const int t = bt[B.head[i]];
+            const double xv = xp[i];
+            const int q0 = B.kptr[i], q1 = B.kptr[i + 1];
+            if (q0 == q1) {
+                const double f = std::fabs(host_infeas(xv, t));
+                cinf[p] += (float)f + (f > 0.0 ? c->sel_cw : 0.0f);
+                continue;
             }
-            sptr.push_back((int)scode.size() / 2);
+            if (box) {
+                // interval of x_i over the training box of the deltas: a row that stays
+                // feasible on the whole box never contributes, so it is left out
+                double lo = xv, hi = xv, mag = std::fabs(xv);
+                for (int q = q0; q < q1; ++q) {
+                    const double g = coef[B.ke[q]] * B.kraw[q];
+                    const double a = g * c->sel_lo[B.ke[q]], bb = g * c->sel_hi[B.ke[q]];
+                    lo += std::min(a, bb);
+                    hi += std::max(a, bb);
+                    mag += std::max(std::fabs(a), std::fabs(bb));
+                }
+                const double tol = 1e-9 + 1e-12 * mag;
+                const bool feasible_box = (t == BT_Y || t == BT_L) ? lo > tol : (t == BT_G) ? hi < -tol : false;
+                if (std::isfinite(lo) && std::isfinite(hi) && feasible_box) continue;
+            }
+            rec(-1 - t, xv);
+            ++prows[p];
+            for (int q = q0; q < q1; ++q) rec(B.ke[q], B.kraw[q]);
         }
-        if ((rc = upload(&c->d_sel_cinf, cinf)) || (rc = upload(&c->d_sel_ptr, sptr)) || (rc = upload(&c->d_sel_code, scode)))
+    });
+    if ((rc = upload_cap(&c->d_xbase, &c->xbase_cap, xb.data(), xb.size())) ||
+        (rc = upload_cap(&c->d_kcoef, &c->kcoef_cap, coef.data(), coef.size())))
+        return rc;
+    if (!c->use_hyper) {
+        std::vector<double> bk((size_t)std::max(k, 1) * MP, 0.0);
+        for (int e = 0; e < k; ++e) {
+            const int rr = c->pos_row[e];
+            for (int i = 0; i < m; ++i) bk[(size_t)e * MP + i] = coef[e] * c->B0inv[(size_t)i * m + rr];
+        }
+        if ((rc = upload_cap(&c->d_B0K, &c->b0k_cap, bk.data(), bk.size()))) return rc;
+    }
+    if (sel) {
+        std::vector<int> sptr(1, 0), scode;
+        size_t tot = 0;
+        for (int p = 0; p < P; ++p) tot += pcode[p].size();
+        scode.reserve(tot);
+        c->sel_rows = 0;
+        for (int p = 0; p < P; ++p) {
+            scode.insert(scode.end(), pcode[p].begin(), pcode[p].end());
+            sptr.push_back((int)scode.size() / 2);
+            c->sel_rows += prows[p];
+        }
+        if ((rc = upload_cap(&c->d_sel_cinf, &c->cinf_cap, cinf.data(), cinf.size())) ||
+            (rc = upload_cap(&c->d_sel_ptr, &c->sptr_cap, sptr.data(), sptr.size())) ||
+            (rc = upload_cap(&c->d_sel_code, &c->scode_cap, scode.data(), scode.size())))
             return rc;
         c->sel_nnz = (int64_t)scode.size() / 2 - c->sel_rows;
     }

@@ -70,6 +70,8 @@ struct twosd_ctx {
     bool k_valid = false;         // K rows / ELL of the pool (depend on the pool and the positions)
     double *d_kcoef = nullptr;    // k: coef_e(x) = 1 (RHS element) or -x[col] (T element)
     std::vector<double> prep_x;
+    // capacities of the per-x device arrays (prepare_x re-uploads in place, no hipFree/hipMalloc per x)
+    size_t xbase_cap = 0, b0k_cap = 0, kcoef_cap = 0, cinf_cap = 0, sptr_cap = 0, scode_cap = 0;
     // hypersparse kernel data
     int CH = 0;                   // column slots per lane of the hypersparse kernel
     bool use_hyper = true;
