@@ -92,6 +92,10 @@ def main():
     ap.add_argument("--no-dedup", action="store_true")
     ap.add_argument("--pool", type=int, default=512, help="warm-start basis pool size (1 = primary basis only)")
     ap.add_argument("--pool-train", type=int, default=16384, help="training scenarios of the pool build")
+    ap.add_argument("--pool-level1", type=int, default=0,
+                    help="two-level warm-start selection: level 1 over the first L pool bases (0: flat)")
+    ap.add_argument("--pool-cands", type=int, default=16, help="level-2 candidate bases per level-1 basis")
+    ap.add_argument("--cand-train", type=int, default=65536, help="training scenarios of the candidate lists")
     ap.add_argument("--sampler", choices=["device", "host"], default="device",
                     help="scenario draws: on-device Philox4x32-10 sampler (twosd_add_sampled_scenarios) or numpy PCG64")
     ap.add_argument("--epigraphs", type=int, default=1,
@@ -142,6 +146,10 @@ def main():
         scenarios(tr, 0, args.pool_train, args.seed + 2)
         ctx.pool_build(tr, x, 0, args.pool_train, args.pool)
     pool_size = ctx.pool_size()
+    if args.pool_level1 > 0 and pool_size > args.pool_level1:
+        ct = twosd.sdEpigraph(ctx, 1.0, 0.0)
+        scenarios(ct, 0, args.cand_train, args.seed + 3)
+        ctx.pool_build_candidates(ct, x, 0, args.cand_train, args.pool_level1, args.pool_cands)
     t_pool = time.perf_counter() - t_pool
 
     N = args.scenarios
@@ -268,6 +276,8 @@ def main():
                                f"warm-start pool {pool_size}, LP solve + dual dedup + build_sasa_cut per step",
                    "instance": name, "scenarios": N, "epigraphs": E, "vertices": nv, "k": k, "m2": m,
                    "basis_pool": pool_size, "pool_build_s": round(t_pool, 3),
+                   "pool_selection": (f"two-level: {args.pool_level1} + {args.pool_cands} candidates"
+                                      if args.pool_level1 > 0 and pool_size > args.pool_level1 else "flat"),
                    "parallelism": f"scenario-dp{world}"},
         "phases_ms_per_step": {"pool_select": t_sel / K / 1e3, "lp_kernel": t_lp / K / 1e3, "dedup": t_dd / K / 1e3,
                                "cut_partial": t_cut / K / 1e3, "cut_finalize": t_fin / K / 1e3},

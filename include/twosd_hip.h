@@ -98,6 +98,13 @@ int twosd_get_basis(twosd_ctx *ctx, int *head);
 int twosd_pool_add_basis(twosd_ctx *ctx, const int *head, int *added);
 int twosd_pool_build(twosd_ctx *ctx, int epi, const double *x, int first, int count, int max_pool,
                      int *pool_size);
+/* Two-level pool selection: level 1 over pool[0, level1), level 2 over the ncand bases
+ * that a flat selection over the whole pool picks most often for the training scenarios
+ * [first, first+count) of epi at x sharing the level-1 pick.  Cuts the selection cost of a
+ * large pool to about that of its first level1 bases.  level1 = 0: flat selection.  Reset
+ * by any change of the pool. */
+int twosd_pool_build_candidates(twosd_ctx *ctx, int epi, const double *x, int first, int count, int level1,
+                                int ncand);
 int twosd_pool_size(twosd_ctx *ctx, int *size);
 int twosd_pool_get(twosd_ctx *ctx, int p, int *head);
 /* Pool basis each scenario of the last LP batch started from (first N of it; 0 = the

@@ -36,6 +36,7 @@ SIGNATURES = [
     ("twosd_get_basis", I, [P, P]),
     ("twosd_pool_add_basis", I, [P, P, P]),
     ("twosd_pool_build", I, [P, I, P, I, I, I, P]),
+    ("twosd_pool_build_candidates", I, [P, I, P, I, I, I, I]),
     ("twosd_pool_size", I, [P, P]),
     ("twosd_pool_get", I, [P, I, P]),
     ("twosd_last_pool_picks", I, [P, I, P]),

@@ -136,7 +136,7 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_xbase); dfree(c->d_B0K); dfree(c->d_eta); dfree(c->d_queue);
     dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_ops);
     dfree(c->d_dvtmp);
-    dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); dfree(c->d_head_out); dfree(c->d_pool_pick); dfree(c->d_order); dfree(c->d_sort_tmp); c->order_cap = 0; c->sort_tmp_bytes = 0; c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
+    dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); dfree(c->d_head_out); dfree(c->d_pool_pick); dfree(c->d_order); dfree(c->d_sort_tmp); dfree(c->d_cand); dfree(c->d_sel_key); c->key_cap = 0; c->pool_l1 = c->pool_ncand = 0; c->order_cap = 0; c->sort_tmp_bytes = 0; c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
     dfree(c->d_dist_kind); dfree(c->d_dist_off); dfree(c->d_dist_val); dfree(c->d_dist_prob); dfree(c->d_dist_p0);
     dfree(c->d_dist_p1); dfree(c->d_dist_tmpl); c->has_dist = false;
     dfree(c->d_kslot); dfree(c->d_kix); dfree(c->d_kv); dfree(c->d_kcoef); c->k_valid = false;
@@ -411,6 +411,7 @@ static int upload_pool(twosd_ctx *c) {
     }
     c->prep_valid = false;
     c->k_valid = false;
+    c->pool_l1 = c->pool_ncand = 0;   // candidate lists refer to pool indices: rebuild after a change
     return TWOSD_OK;
 }
 
@@ -457,6 +458,7 @@ static int pool_add(twosd_ctx *c, const std::vector<int> &head, bool upload_now)
     PoolBasis pb;
     int rc = make_pool_basis(c, head, pb);
     if (rc) return rc;
+    std::vector<double>().swap(pb.Binv);
     c->pool.push_back(std::move(pb));
     if (upload_now && (rc = upload_pool(c))) return rc;
     return 1;
@@ -592,6 +594,7 @@ extern "C" int twosd_pool_build(twosd_ctx *c, int epi, const double *x, int firs
                     const int s = order[a].second;
                     std::vector<int> head(heads.begin() + (size_t)s * m, heads.begin() + (size_t)(s + 1) * m);
                     ok[a] = compute_pool_basis(c, head, cand[a]) == nullptr;
+                    std::vector<double>().swap(cand[a].Binv);   // sparse forms kept; dense m x m only for the primary
                 }
             });
         for (auto &t : th) t.join();
@@ -611,6 +614,63 @@ extern "C" int twosd_pool_build(twosd_ctx *c, int epi, const double *x, int firs
         }
     }
     if (pool_size) *pool_size = (int)c->pool.size();
+    return TWOSD_OK;
+}
+
+static int select_pool(twosd_ctx *c, const double *d_dv, int N, int *d_pick, int npool_override);
+
+// Two-level selection from training scenarios [first, first + count) of epigraph epi at x:
+// level 1 = pool[0, level1) (the most frequent bases); the candidates of a level-1 basis p are
+// the ncand bases that the flat selection over the whole pool picks most often for training
+// scenarios whose level-1 pick is p (ties: lower index).  level1 = 0 back to flat selection.
+extern "C" int twosd_pool_build_candidates(twosd_ctx *c, int epi, const double *x, int first, int count, int level1,
+                                           int ncand) {
+    if (!c || !c->has_basis) return fail(TWOSD_E_STATE, "pool_build_candidates: no primary basis");
+    if (epi < 0 || epi >= (int)c->epis.size()) return fail(TWOSD_E_ARG, "pool_build_candidates: epigraph %d does not exist", epi);
+    const EpiDevice &E = c->epis[epi];
+    const int P = (int)c->pool.size();
+    if (first < 0 || count < 1 || first + count > E.count || level1 < 0 || ncand < 0 || ncand > 256 || (c->n1 > 0 && !x))
+        return fail(TWOSD_E_ARG, "pool_build_candidates: bad arguments");
+    c->pool_l1 = c->pool_ncand = 0;
+    if (level1 == 0 || ncand == 0 || level1 >= P || P < 2 || c->CH <= 0) return TWOSD_OK;   // flat selection
+    HIPCHK(hipSetDevice(c->device));
+    int rc;
+    if ((rc = prepare_x(c, x))) return rc;
+    int *d_p = nullptr;
+    if ((rc = dalloc(&d_p, (size_t)count))) return rc;
+    const double *dv = E.d_dv + (size_t)first * c->k;
+    std::vector<int> p1(count), pf(count);
+    auto picks = [&](int np, std::vector<int> &out) {   // selection runs on c->stream
+        int r = select_pool(c, dv, count, d_p, np);
+        if (!r && (hipStreamSynchronize(c->stream) != hipSuccess ||
+                   hipMemcpy(out.data(), d_p, sizeof(int) * count, hipMemcpyDeviceToHost) != hipSuccess))
+            r = fail(TWOSD_E_DEVICE, "pool_build_candidates: selection failed");
+        return r;
+    };
+    rc = picks(level1, p1);
+    if (!rc) rc = picks(P, pf);
+    hipFree(d_p);
+    if (rc) return rc;
+    std::vector<std::map<int, int>> freq(level1);
+    for (int s = 0; s < count; ++s)
+        if (pf[s] != p1[s] && p1[s] >= 0 && p1[s] < level1) ++freq[p1[s]][pf[s]];
+    std::vector<int> cand((size_t)level1 * ncand, -1);
+    for (int p = 0; p < level1; ++p) {
+        std::vector<std::pair<int, int>> v;   // (-count, basis)
+        for (auto &kv : freq[p]) v.push_back({-kv.second, kv.first});
+        std::sort(v.begin(), v.end());
+        for (int i = 0; i < (int)v.size() && i < ncand; ++i) cand[(size_t)p * ncand + i] = v[i].second;
+    }
+    if (getenv("TWOSD_DEBUG")) {
+        int diff = 0, filled = 0;
+        for (int s = 0; s < count; ++s) diff += pf[s] != p1[s];
+        for (int v : cand) filled += v >= 0;
+        fprintf(stderr, "pool_build_candidates: P=%d level1=%d: %d of %d training picks change, %d candidate slots filled\n", P,
+                level1, diff, count, filled);
+    }
+    if ((rc = upload(&c->d_cand, cand))) return rc;
+    c->pool_l1 = level1;
+    c->pool_ncand = ncand;
     return TWOSD_OK;
 }
 
@@ -905,6 +965,7 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
     std::vector<std::vector<int>> pcode(sel ? P : 0);   // per basis: interleaved (code, float bits) records
     std::vector<int64_t> prows(P, 0);
     const bool box = !c->sel_lo.empty();
+    static const bool sel_order = !getenv("TWOSD_SEL_ROWORDER") || atoi(getenv("TWOSD_SEL_ROWORDER")) != 0;   // A/B knob
     parallel_over(P, [&](int p) {
         const PoolBasis &B = c->pool[p];
         double *xp = xb.data() + (size_t)p * MP;
@@ -922,6 +983,9 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
             sc.push_back(code);
             sc.push_back(bits);
         };
+        // active rows with the largest possible infeasibility over the training box first:
+        // a losing basis accumulates its key fastest, so the kernel's pruning drops it early
+        std::vector<std::pair<double, int>> act;
         for (int i = 0; i < m; ++i) {
             const int t = bt[B.head[i]];
             const double xv = xp[i];
@@ -931,6 +995,7 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
                 cinf[p] += (float)f + (f > 0.0 ? c->sel_cw : 0.0f);
                 continue;
             }
+            double worst = 0.0;
             if (box) {
                 // interval of x_i over the training box of the deltas: a row that stays
                 // feasible on the whole box never contributes, so it is left out
@@ -945,10 +1010,17 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
                 const double tol = 1e-9 + 1e-12 * mag;
                 const bool feasible_box = (t == BT_Y || t == BT_L) ? lo > tol : (t == BT_G) ? hi < -tol : false;
                 if (std::isfinite(lo) && std::isfinite(hi) && feasible_box) continue;
+                worst = (t == BT_Y || t == BT_L) ? -lo : (t == BT_G) ? hi : std::max(std::fabs(lo), std::fabs(hi));
+                if (!std::isfinite(worst)) worst = HUGE_VAL;
             }
-            rec(-1 - t, xv);
+            act.push_back({-worst, i});
+        }
+        if (sel_order) std::stable_sort(act.begin(), act.end());
+        for (const auto &a : act) {
+            const int i = a.second;
+            rec(-1 - bt[B.head[i]], xp[i]);
             ++prows[p];
-            for (int q = q0; q < q1; ++q) rec(B.ke[q], B.kraw[q]);
+            for (int q = B.kptr[i]; q < B.kptr[i + 1]; ++q) rec(B.ke[q], B.kraw[q]);
         }
     });
     if ((rc = upload_cap(&c->d_xbase, &c->xbase_cap, xb.data(), xb.size())) ||
@@ -981,6 +1053,48 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
     }
     c->prep_x.assign(x, x + n1);
     c->prep_valid = true;
+    return TWOSD_OK;
+}
+
+// Warm-start selection for scenarios [0, N) at the prepared x: pick[s] = pool basis, and
+// c->d_order = the scenarios grouped by pick (stable).  Flat: least key over the whole pool.
+// Two-level (pool_l1 > 0): least key over pool[0, pool_l1), then over the candidates of that
+// pick.  npool_override > 0: flat over pool[0, npool_override) (candidate training).
+static int select_pool(twosd_ctx *c, const double *d_dv, int N, int *d_pick, int npool_override) {
+    const int P = (int)c->pool.size();
+    const bool two = npool_override <= 0 && c->pool_l1 > 0 && c->pool_l1 < P && c->pool_ncand > 0 && c->d_cand;
+    const int np1 = npool_override > 0 ? npool_override : two ? c->pool_l1 : P;
+    int rc;
+    size_t tb = 0, tb2 = 0;
+    HIPCHK(sort_by_pool(d_pick, nullptr, N, P, nullptr, &tb, c->stream));
+    HIPCHK(sort_by_pool(d_pick, nullptr, N, np1, nullptr, &tb2, c->stream));
+    tb = std::max(tb, tb2);
+    if ((size_t)N > c->order_cap || tb > c->sort_tmp_bytes) {
+        if ((rc = dalloc(&c->d_order, (size_t)N)) || (rc = dalloc(&c->d_sort_tmp, tb))) return rc;
+        c->order_cap = N;
+        c->sort_tmp_bytes = tb;
+    }
+    if (two && (size_t)N > c->key_cap) {
+        if ((rc = dalloc(&c->d_sel_key, (size_t)N))) return rc;
+        c->key_cap = N;
+    }
+    PoolSelParams S{};
+    S.N = N; S.k = c->k; S.npool = np1; S.dv = d_dv;
+    S.kcoef = c->d_kcoef;
+    S.cinf = c->d_sel_cinf; S.sptr = c->d_sel_ptr; S.rec = reinterpret_cast<const int2 *>(c->d_sel_code);
+    S.pick = d_pick;
+    S.cw = c->sel_cw;
+    S.key = two ? c->d_sel_key : nullptr;
+    HIPCHK(launch_pool_select(S, c->stream));
+    if (two) {
+        HIPCHK(sort_by_pool(d_pick, c->d_order, N, np1, c->d_sort_tmp, &tb, c->stream));
+        PoolRefineParams Q{};
+        Q.N = N; Q.k = c->k; Q.ncand = c->pool_ncand; Q.dv = d_dv; Q.kcoef = c->d_kcoef;
+        Q.cinf = c->d_sel_cinf; Q.sptr = c->d_sel_ptr; Q.rec = S.rec;
+        Q.order = c->d_order; Q.cand = c->d_cand; Q.pick = d_pick; Q.key = c->d_sel_key; Q.cw = c->sel_cw;
+        HIPCHK(launch_pool_refine(Q, c->stream));
+    }
+    HIPCHK(sort_by_pool(d_pick, c->d_order, N, P, c->d_sort_tmp, &tb, c->stream));
     return TWOSD_OK;
 }
 
@@ -1060,21 +1174,7 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
         }
         HIPCHK(hipEventRecord(c->ev[0], c->stream));
         if (H.npool > 1) {
-            PoolSelParams S{};
-            S.N = N; S.k = c->k; S.npool = H.npool; S.dv = d_dv;
-            S.kcoef = c->d_kcoef;
-            S.cinf = c->d_sel_cinf; S.sptr = c->d_sel_ptr; S.rec = reinterpret_cast<const int2 *>(c->d_sel_code);
-            S.pick = c->d_pool_pick;
-            S.cw = c->sel_cw;
-            HIPCHK(launch_pool_select(S, c->stream));
-            size_t tb = 0;
-            HIPCHK(sort_by_pool(c->d_pool_pick, nullptr, N, H.npool, nullptr, &tb, c->stream));
-            if ((size_t)N > c->order_cap || tb > c->sort_tmp_bytes) {
-                if ((rc = dalloc(&c->d_order, (size_t)N)) || (rc = dalloc(&c->d_sort_tmp, tb))) return rc;
-                c->order_cap = N;
-                c->sort_tmp_bytes = tb;
-            }
-            HIPCHK(sort_by_pool(c->d_pool_pick, c->d_order, N, H.npool, c->d_sort_tmp, &tb, c->stream));
+            if ((rc = select_pool(c, d_dv, N, c->d_pool_pick, 0))) return rc;
             H.order = c->d_order;
         }
         HIPCHK(hipEventRecord(c->ev[2], c->stream));

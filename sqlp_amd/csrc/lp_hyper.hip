@@ -630,6 +630,10 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_select_kernel(PoolSelPara
     extern __shared__ float dvt[];   // k x 65 (padded)
     __shared__ float bsum[kSelWaves][64];
     __shared__ int bidx[kSelWaves][64];
+    // best key found so far by any wave, per scenario (keys are >= 0, so the uint order of
+    // the fp32 bits is the float order): a wave stops a basis once it is strictly worse than
+    // another wave's best for every lane
+    __shared__ unsigned sbest[64];
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar stream loads
     const int s0 = blockIdx.x * 64;
@@ -639,9 +643,15 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_select_kernel(PoolSelPara
         const int sl = idx / k, e = idx - sl * k;
         dvt[e * 65 + sl] = sl < ns ? (float)(S.kcoef[e] * S.dv[(size_t)s0 * k + idx]) : 0.0f;
     }
+    if (threadIdx.x < 64) sbest[threadIdx.x] = 0x7f800000u;   // +inf
     __syncthreads();
     float best = INFINITY;
     int bp = 0;
+    // a lane can still win with key `inf` only if inf < its own best (lower p wins ties within
+    // the wave) and inf <= every other wave's best (ties with other waves are settled at the end)
+    auto alive = [&](float inf) {
+        return inf < best && inf <= __uint_as_float(__hip_atomic_load(&sbest[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    };
     for (int p = wid; p < S.npool; p += kSelWaves) {
         // one flat, wave-uniform stream per basis: a row-start record (code -1 - bound type,
         // value xbase_i) followed by the row's entries (code e, value B^{-1}[i][row_e]);
@@ -658,7 +668,7 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_select_kernel(PoolSelPara
                 x = fmaf(v, dl, x);
             }
         };
-        int j = (__ballot(inf < best) == 0) ? j1 : j0;   // constant rows alone already lose
+        int j = (__ballot(alive(inf)) == 0) ? j1 : j0;   // constant rows alone already lose
         for (; j + 8 <= j1; j += 8) {   // batches of 8 records: scalar loads and LDS reads in flight together
             int2 rc[8];
             float dl[8];
@@ -670,14 +680,18 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_select_kernel(PoolSelPara
             for (int u = 0; u < 8; ++u) step(rc[u].x, __int_as_float(rc[u].y), dl[u]);
             // exact pruning: inf only grows (sum of nonnegative terms), so once no lane can
             // still beat its best, this basis cannot win for any of the 64 scenarios
-            if (__ballot(inf < best) == 0) { bt = -1; inf = INFINITY; j = j1; break; }
+            if (__ballot(alive(inf)) == 0) { bt = -1; inf = INFINITY; j = j1; break; }
         }
         for (; j < j1; ++j) {
             const int2 r = S.rec[j];
             step(r.x, __int_as_float(r.y), dvt[(r.x < 0 ? 0 : r.x) * 65 + lane]);
         }
         if (bt >= 0) inf += h_infeas_f(x, bt, S.cw);
-        if (inf < best) { best = inf; bp = p; }
+        if (inf < best) {
+            best = inf;
+            bp = p;
+            atomicMin(&sbest[lane], __float_as_uint(inf));
+        }
     }
     bsum[wid][lane] = best;
     bidx[wid][lane] = bp;
@@ -689,7 +703,93 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_select_kernel(PoolSelPara
             if (v < best || (v == best && pw < bp)) { best = v; bp = pw; }
         }
         S.pick[s0 + lane] = bp;
+        if (S.key) S.key[s0 + lane] = best;
     }
+}
+
+// ---- level 2: 64 consecutive entries of `order` (scenarios sorted by their level-1 pick, so a
+// tile holds one or two pick groups) per block; the block's 16 waves share the staged deltas
+// and split each group's candidate list (candidate ci on wave ci % 16).  Each candidate streams
+// its records wave-uniformly, as in level 1.  Result per scenario: least (key, ci) with the
+// level-1 pick as ci = -1, i.e. a candidate replaces the pick only with a strictly smaller key,
+// and among equal keys the earlier candidate wins (deterministic).
+__global__ void __launch_bounds__(64 * kSelWaves) pool_refine_kernel(PoolRefineParams S) {
+    extern __shared__ float dvt[];   // k x 65
+    __shared__ float rkey[kSelWaves][64];
+    __shared__ int rci[kSelWaves][64];
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int t0 = blockIdx.x * 64;
+    const int k = S.k;
+    const int nv = min(64, S.N - t0);
+    for (int idx = threadIdx.x; idx < 64 * k; idx += 64 * kSelWaves) {
+        const int r = idx / k, e = idx - r * k;
+        dvt[e * 65 + r] = r < nv ? (float)(S.kcoef[e] * S.dv[(size_t)S.order[t0 + r] * k + e]) : 0.0f;
+    }
+    __syncthreads();
+    const bool valid = lane < nv;
+    const int s = valid ? S.order[t0 + lane] : 0;
+    const int p1 = valid ? S.pick[s] : -1;
+    const float key1 = valid ? S.key[s] : 0.0f;
+    float best = key1;
+    int bci = -1;
+    uint64_t todo = __ballot(valid);
+    while (todo) {
+        const int g = __builtin_amdgcn_readlane(p1, __builtin_ctzll(todo));
+        const bool mine = valid && p1 == g;
+        todo &= ~__ballot(mine);
+        for (int ci = wid; ci < S.ncand; ci += kSelWaves) {
+            const int cb = S.cand[(size_t)g * S.ncand + ci];
+            if (cb < 0) break;
+            float inf = S.cinf[cb], x = 0.0f;
+            int bt = -1;
+            auto step = [&](int code, float v, float dl) {
+                if (code < 0) {
+                    if (bt >= 0) inf += h_infeas_f(x, bt, S.cw);
+                    x = v;
+                    bt = -1 - code;
+                } else {
+                    x = fmaf(v, dl, x);
+                }
+            };
+            const int j0 = S.sptr[cb], j1 = S.sptr[cb + 1];
+            int j = (__ballot(mine && inf < best) == 0) ? j1 : j0;
+            for (; j + 8 <= j1; j += 8) {
+                int2 rc[8];
+                float dl[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) rc[u] = S.rec[j + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) dl[u] = dvt[(rc[u].x < 0 ? 0 : rc[u].x) * 65 + lane];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) step(rc[u].x, __int_as_float(rc[u].y), dl[u]);
+                if (__ballot(mine && inf < best) == 0) { bt = -1; inf = INFINITY; j = j1; break; }
+            }
+            for (; j < j1; ++j) {
+                const int2 r = S.rec[j];
+                step(r.x, __int_as_float(r.y), dvt[(r.x < 0 ? 0 : r.x) * 65 + lane]);
+            }
+            if (bt >= 0) inf += h_infeas_f(x, bt, S.cw);
+            if (mine && inf < best) { best = inf; bci = ci; }
+        }
+    }
+    rkey[wid][lane] = best;
+    rci[wid][lane] = bci;
+    __syncthreads();
+    if (wid == 0 && valid) {
+        for (int w = 1; w < kSelWaves; ++w) {
+            const float v = rkey[w][lane];
+            const int cw = rci[w][lane];
+            if (v < best || (v == best && cw >= 0 && (bci < 0 ? false : cw < bci))) { best = v; bci = cw; }
+        }
+        if (bci >= 0) S.pick[s] = S.cand[(size_t)p1 * S.ncand + bci];
+    }
+}
+
+hipError_t launch_pool_refine(const PoolRefineParams &p, hipStream_t s) {
+    if (p.N <= 0 || p.ncand <= 0) return hipSuccess;
+    hipLaunchKernelGGL(pool_refine_kernel, dim3((p.N + 63) / 64), dim3(64 * kSelWaves), pool_select_lds_bytes(p.k), s, p);
+    return hipGetLastError();
 }
 
 size_t pool_select_lds_bytes(int k) { return (size_t)4 * 65 * (size_t)std::max(k, 1); }

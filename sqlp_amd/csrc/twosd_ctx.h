@@ -62,6 +62,12 @@ struct twosd_ctx {
     int *d_bnnz = nullptr;        // npool: nnz of each pool B^{-1} (FMA accounting)
     int *d_head_out = nullptr, *d_pool_pick = nullptr;   // optional LP outputs (pool building)
     size_t head_cap = 0, pick_cap = 0;
+    // two-level pool selection (twosd_pool_build_candidates): level 1 over pool[0, pool_l1),
+    // level 2 over the candidate bases of the level-1 pick (d_cand: pool_l1 x pool_ncand)
+    int pool_l1 = 0, pool_ncand = 0;
+    int *d_cand = nullptr;
+    float *d_sel_key = nullptr;
+    size_t key_cap = 0;
     int *d_order = nullptr;       // LP visiting order grouped by pool basis
     char *d_sort_tmp = nullptr;
     size_t order_cap = 0, sort_tmp_bytes = 0;

@@ -96,7 +96,22 @@ struct PoolSelParams {
                                                         //   xbase_i); entry (e, B^{-1}[i][row_e])
     int *pick;                                          // N out
     float cw;                                           // key = sum |infeas| + cw * #infeasible rows
+    float *key;                                         // N out (nullable): key of the pick
 };
+// second level of the two-level pool selection: scenarios in `order` (grouped by their
+// level-1 pick) try the candidate bases of their level-1 pick (cand: nl1 x ncand, -1 pad)
+struct PoolRefineParams {
+    int N, k, ncand;
+    const double *dv, *kcoef;
+    const float *cinf;
+    const int *sptr;
+    const int2 *rec;
+    const int *order, *cand;
+    int *pick;                                          // N in (level 1) / out
+    const float *key;                                   // N: level-1 key
+    float cw;
+};
+hipError_t launch_pool_refine(const PoolRefineParams &p, hipStream_t s);
 size_t pool_select_lds_bytes(int k);
 // stable sort of scenarios [0, N) by pool pick -> order (pool_sort.hip); tmp == nullptr: size query
 hipError_t sort_by_pool(const int *pick, int *order, int N, int npool, void *tmp, size_t *tmp_bytes, hipStream_t s);

@@ -129,6 +129,13 @@ class SDContext:
                                         C.byref(n)))
         return n.value
 
+    def pool_build_candidates(self, epi, x, first, count, level1, ncand):
+        """Two-level warm-start selection: level 1 over the first `level1` pool bases, level 2
+        over the `ncand` bases a flat selection picks most often for the training scenarios
+        [first, first+count) of `epi` that share the level-1 pick.  level1 = 0: flat."""
+        check(self.lib.twosd_pool_build_candidates(self.h, epi.index, ptr(_f64(x)), int(first), int(count),
+                                                   int(level1), int(ncand)))
+
     def last_pool_picks(self, N):
         """Pool basis every scenario of the last LP batch started from."""
         picks = np.zeros(N, dtype=np.int32)
