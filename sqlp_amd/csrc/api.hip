@@ -15,6 +15,7 @@
 #include <vector>
 #include <map>
 #include <thread>
+#include <chrono>
 #include "twosd_internal.h"
 #include "twosd_ctx.h"
 
@@ -136,7 +137,9 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_xbase); dfree(c->d_B0K); dfree(c->d_eta); dfree(c->d_queue);
     dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_ops);
     dfree(c->d_dvtmp);
-    dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); dfree(c->d_head_out); dfree(c->d_pool_pick); dfree(c->d_order); dfree(c->d_sort_tmp); dfree(c->d_cand); dfree(c->d_sel_key); c->key_cap = 0; c->pool_l1 = c->pool_ncand = 0; c->order_cap = 0; c->sort_tmp_bytes = 0; c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
+    dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); dfree(c->d_head_out); dfree(c->d_pool_pick); dfree(c->d_order); dfree(c->d_sort_tmp); dfree(c->d_bvec); c->bvec_cap = 0;
+    if (c->h_scode) hipHostFree(c->h_scode);
+    c->h_scode = nullptr; c->h_scode_cap = 0; dfree(c->d_cand); dfree(c->d_sel_key); c->key_cap = 0; c->pool_l1 = c->pool_ncand = 0; c->order_cap = 0; c->sort_tmp_bytes = 0; c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
     dfree(c->d_dist_kind); dfree(c->d_dist_off); dfree(c->d_dist_val); dfree(c->d_dist_prob); dfree(c->d_dist_p0);
     dfree(c->d_dist_p1); dfree(c->d_dist_tmpl); c->has_dist = false;
     dfree(c->d_kslot); dfree(c->d_kix); dfree(c->d_kv); dfree(c->d_kcoef); c->k_valid = false;
@@ -908,6 +911,19 @@ static double host_infeas(double x, int bt) {
     return std::fabs(x) > tol ? x : 0.0;
 }
 
+// x_B of every pool basis at b: xbase[p][i] = sum_q B_p^{-1}[i][col_q] b[col_q] over the CSR
+// rows (pool-strided brptr, MP + 1 per basis; rows >= m are empty), q ascending
+__global__ void pool_xbase_kernel(int P, int MP, const int *__restrict__ brptr, const int *__restrict__ brcol,
+                                  const double *__restrict__ brval, const double *__restrict__ b, double *__restrict__ xbase) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (size_t)P * MP) return;
+    const size_t p = t / MP, i = t - p * MP;
+    const int *rp = brptr + p * (MP + 1);
+    double s = 0.0;
+    for (int q = rp[i]; q < rp[i + 1]; ++q) s = fma(brval[q], b[brcol[q]], s);
+    xbase[t] = s;
+}
+
 // copy n host elements to a device array grown only when n exceeds its capacity
 template <typename T>
 static int upload_cap(T **d, size_t *cap, const T *h, size_t n) {
@@ -947,13 +963,15 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
     if (c->prep_valid && c->prep_x.size() == (size_t)n1 && (n1 == 0 || std::equal(c->prep_x.begin(), c->prep_x.end(), x)))
         return TWOSD_OK;
     int rc;
+    const auto t_start = std::chrono::steady_clock::now();
     if (!c->k_valid && (rc = prepare_elements(c))) return rc;
     std::vector<double> b;
     rhs_at(c, x, nullptr, b);
     const int P = (int)c->pool.size();
     std::vector<double> coef(std::max(k, 1), 1.0);
     for (int e = 0; e < k; ++e) coef[e] = c->pos_col[e] < 0 ? 1.0 : -x[c->pos_col[e]];
-    std::vector<double> xb((size_t)P * MP, 0.0);
+    std::vector<double> &xb = c->h_xb;
+    xb.resize((size_t)P * MP);
     const bool sel = P > 1 && c->CH > 0;
     std::vector<int8_t> bt;
     if (sel) {
@@ -962,7 +980,8 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
         if (const char *e = getenv("TWOSD_SEL_CW")) c->sel_cw = (float)atof(e);   // selection-key experiments
     }
     std::vector<float> cinf(P, 0.0f);
-    std::vector<std::vector<int>> pcode(sel ? P : 0);   // per basis: interleaved (code, float bits) records
+    std::vector<std::vector<int>> &pcode = c->h_pcode;   // per basis: interleaved (code, float bits) records
+    pcode.resize(sel ? P : 0);
     std::vector<int64_t> prows(P, 0);
     const bool box = !c->sel_lo.empty();
     static const bool sel_order = !getenv("TWOSD_SEL_ROWORDER") || atoi(getenv("TWOSD_SEL_ROWORDER")) != 0;   // A/B knob
@@ -976,6 +995,7 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
         }
         if (!sel) return;
         std::vector<int> &sc = pcode[p];
+        sc.clear();
         auto rec = [&](int code, double v) {
             const float f = (float)v;
             int bits;
@@ -1023,9 +1043,23 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
             for (int q = B.kptr[i]; q < B.kptr[i + 1]; ++q) rec(B.ke[q], B.kraw[q]);
         }
     });
-    if ((rc = upload_cap(&c->d_xbase, &c->xbase_cap, xb.data(), xb.size())) ||
+    // device x_B from the device copy of the pool's B^{-1} rows (no P x MP upload)
+    if ((rc = upload_cap(&c->d_bvec, &c->bvec_cap, b.data(), b.size())) ||
         (rc = upload_cap(&c->d_kcoef, &c->kcoef_cap, coef.data(), coef.size())))
         return rc;
+    if (!c->d_xbase || (size_t)P * MP > c->xbase_cap) {
+        if ((rc = dalloc(&c->d_xbase, (size_t)P * MP))) return rc;
+        c->xbase_cap = (size_t)P * MP;
+    }
+    if (c->CH > 0) {
+        const size_t tot = (size_t)P * MP;
+        hipLaunchKernelGGL(pool_xbase_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, P, MP, c->d_brptr,
+                           c->d_brcol, c->d_brval, c->d_bvec, c->d_xbase);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(c->stream));
+    } else {
+        HIPCHK(hipMemcpy(c->d_xbase, xb.data(), sizeof(double) * xb.size(), hipMemcpyHostToDevice));
+    }
     if (!c->use_hyper) {
         std::vector<double> bk((size_t)std::max(k, 1) * MP, 0.0);
         for (int e = 0; e < k; ++e) {
@@ -1035,24 +1069,36 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
         if ((rc = upload_cap(&c->d_B0K, &c->b0k_cap, bk.data(), bk.size()))) return rc;
     }
     if (sel) {
-        std::vector<int> sptr(1, 0), scode;
-        size_t tot = 0;
-        for (int p = 0; p < P; ++p) tot += pcode[p].size();
-        scode.reserve(tot);
+        // concatenate the per-basis streams into pinned staging (fast upload), in pool order
+        std::vector<int> sptr(1, 0);
+        std::vector<size_t> off(P + 1, 0);
+        for (int p = 0; p < P; ++p) off[p + 1] = off[p] + pcode[p].size();
+        const size_t tot = off[P];
+        if (tot > c->h_scode_cap || !c->h_scode) {
+            if (c->h_scode) hipHostFree(c->h_scode);
+            c->h_scode = nullptr;
+            const size_t cap = std::max<size_t>(tot + tot / 4, 1024);
+            HIPCHK(hipHostMalloc((void **)&c->h_scode, sizeof(int) * cap, hipHostMallocDefault));
+            c->h_scode_cap = cap;
+        }
+        parallel_over(P, [&](int p) { std::copy(pcode[p].begin(), pcode[p].end(), c->h_scode + off[p]); });
         c->sel_rows = 0;
         for (int p = 0; p < P; ++p) {
-            scode.insert(scode.end(), pcode[p].begin(), pcode[p].end());
-            sptr.push_back((int)scode.size() / 2);
+            sptr.push_back((int)(off[p + 1] / 2));
             c->sel_rows += prows[p];
         }
         if ((rc = upload_cap(&c->d_sel_cinf, &c->cinf_cap, cinf.data(), cinf.size())) ||
             (rc = upload_cap(&c->d_sel_ptr, &c->sptr_cap, sptr.data(), sptr.size())) ||
-            (rc = upload_cap(&c->d_sel_code, &c->scode_cap, scode.data(), scode.size())))
+            (rc = upload_cap(&c->d_sel_code, &c->scode_cap, (const int *)c->h_scode, tot)))
             return rc;
-        c->sel_nnz = (int64_t)scode.size() / 2 - c->sel_rows;
+        c->sel_nnz = (int64_t)tot / 2 - c->sel_rows;
     }
     c->prep_x.assign(x, x + n1);
     c->prep_valid = true;
+    if (getenv("TWOSD_DEBUG"))
+        fprintf(stderr, "prepare_x: P=%d %.3f ms (%lld selection records)\n", P,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count(),
+                (long long)(c->sel_nnz + c->sel_rows));
     return TWOSD_OK;
 }
 

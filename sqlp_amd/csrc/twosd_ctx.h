@@ -78,6 +78,12 @@ struct twosd_ctx {
     std::vector<double> prep_x;
     // capacities of the per-x device arrays (prepare_x re-uploads in place, no hipFree/hipMalloc per x)
     size_t xbase_cap = 0, b0k_cap = 0, kcoef_cap = 0, cinf_cap = 0, sptr_cap = 0, scode_cap = 0;
+    double *d_bvec = nullptr;     // m: r - T x at the prepared x (x_B of the pool computed on the device)
+    size_t bvec_cap = 0;
+    std::vector<double> h_xb;     // host x_B of the pool (selection stream values), kept across x
+    std::vector<std::vector<int>> h_pcode;   // per-basis selection records, kept across x
+    int *h_scode = nullptr;       // pinned staging of the selection stream
+    size_t h_scode_cap = 0;
     // hypersparse kernel data
     int CH = 0;                   // column slots per lane of the hypersparse kernel
     bool use_hyper = true;
