@@ -1167,7 +1167,7 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
         if ((rc = dalloc(&c->d_y, (size_t)c->out_cap * n))) return rc;
         c->y_cap = c->out_cap;
     }
-    if (!c->d_queue && (rc = dalloc(&c->d_queue, 4))) return rc;
+    if (!c->d_queue && (rc = dalloc(&c->d_queue, (size_t)kMaxQueueGroups * kQueueStride))) return rc;
     if (c->use_hyper) {
         // eta capacity (pivots per scenario): 256 keeps two 4-wave blocks per CU within the LDS
         const int kmax = c->kmax_override > 0 ? c->kmax_override : std::min(256, std::max(64, 2 * m + 32));
@@ -1183,7 +1183,7 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
             c->earena_slots = slots;
             c->earena_cap = ecap;
         }
-        HIPCHK(hipMemsetAsync(c->d_queue, 0, sizeof(int) * 4, c->stream));
+        HIPCHK(hipMemsetAsync(c->d_queue, 0, sizeof(int) * kMaxQueueGroups * kQueueStride, c->stream));
         HyperParams H{};
         H.m = m; H.n = n; H.k = c->k; H.N = N; H.kmax = kmax; H.ecap = ecap;
         H.colptr = c->d_colptr; H.rowidx = c->d_rowidx; H.val = c->d_val; H.q = c->d_q; H.btype = c->d_btype;
@@ -1195,6 +1195,8 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
         H.xbase = c->d_xbase; H.d0 = c->d_d0; H.hb0 = c->d_hb0;
         H.basic0 = c->d_basic0; H.fixedmask = c->d_fixedmask; H.ubmask = c->d_ubmask;
         H.dv = d_dv; H.eidx = c->d_eidx; H.evals = c->d_evals; H.queue = c->d_queue;
+        H.qgroups = std::max(1, std::min(kMaxQueueGroups, nblocks));
+        if (const char *e = getenv("TWOSD_QGROUPS")) H.qgroups = std::max(1, std::min(H.qgroups, atoi(e)));   // A/B knob
         H.obj = c->d_obj; H.pi = want_pi ? c->d_pi : nullptr; H.y = want_y ? c->d_y : nullptr;
         H.status = c->d_status; H.iters = c->d_iters; H.ops = c->d_ops;
         if (!c->d_stamps) {
@@ -1247,7 +1249,7 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
         c->eta_slots = slots;
         c->eta_kmax = kmax;
     }
-    if (!c->d_queue && (rc = dalloc(&c->d_queue, 4))) return rc;
+    if (!c->d_queue && (rc = dalloc(&c->d_queue, (size_t)kMaxQueueGroups * kQueueStride))) return rc;
     HIPCHK(hipMemsetAsync(c->d_queue, 0, sizeof(int) * 4, c->stream));
     LpParams P{};
     P.m = m; P.n = n; P.MP = MP; P.k = c->k; P.N = N; P.kmax = kmax; P.C = c->C;

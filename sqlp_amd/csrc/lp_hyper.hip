@@ -147,11 +147,27 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
     h_wave_sync();
     STAMP_DECL
 
+    // XCD-aware work queues: the visiting order is cut into qgroups contiguous ranges, range g
+    // served first by the blocks with blockIdx % qgroups == g (one XCD under the round-robin
+    // block placement, speed only), so the waves that share a pool basis share one L2.  A wave
+    // whose range is exhausted moves on to the next range (never back: exhausted stays exhausted).
+    const int G = P.qgroups;
+    const int g0 = blockIdx.x % G;
+    int gt = 0;
     for (;;) {
-        int s = 0;
-        if (lane == 0) s = atomicAdd(P.queue, 1);
-        s = __builtin_amdgcn_readfirstlane(__shfl(s, 0));
-        if (s >= P.N) break;
+        int s = -1;
+        for (; gt < G; ++gt) {
+            const int g = g0 + gt < G ? g0 + gt : g0 + gt - G;
+            const int lo = (int)(((long long)P.N * g) / G), hi = (int)(((long long)P.N * (g + 1)) / G);
+            int t = 0;
+            if (lane == 0) t = atomicAdd(P.queue + g * kQueueStride, 1);
+            t = __builtin_amdgcn_readfirstlane(__shfl(t, 0));
+            if (lo + t < hi) {
+                s = lo + t;
+                break;
+            }
+        }
+        if (s < 0) break;
         if (P.order) s = __builtin_amdgcn_readfirstlane(P.order[s]);   // grouped by pool basis
 
         const double *dvs = P.dv + (size_t)s * P.k;

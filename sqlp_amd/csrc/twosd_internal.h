@@ -51,6 +51,8 @@ struct LpParams {
 };
 
 // hypersparse kernel (lp_hyper.hip)
+constexpr int kQueueStride = 32;   // queue heads one 128-B line apart
+constexpr int kMaxQueueGroups = 8;
 struct HyperParams {
     int m, n, k, N, kmax, ecap;
     const int *colptr, *rowidx; const double *val;      // W CSC
@@ -71,7 +73,8 @@ struct HyperParams {
     const uint64_t *basic0, *fixedmask, *ubmask;        // 64
     const double *dv;                                   // N x k
     int *eidx; double *evals;                           // nslots x ecap sparse eta arena
-    int *queue;
+    int *queue;                                         // qgroups heads, kQueueStride ints apart
+    int qgroups;                                        // XCD-group work queues (>= 1)
     double *obj, *pi, *y;
     int *status, *iters;
     long long *ops;                                     // executed FMAs
