@@ -137,12 +137,12 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_xbase); dfree(c->d_B0K); dfree(c->d_eta); dfree(c->d_queue);
     dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_ops);
     dfree(c->d_dvtmp);
-    dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); dfree(c->d_head_out); dfree(c->d_pool_pick); dfree(c->d_order); dfree(c->d_sort_tmp); dfree(c->d_bvec); c->bvec_cap = 0;
-    if (c->h_scode) hipHostFree(c->h_scode);
-    c->h_scode = nullptr; c->h_scode_cap = 0; dfree(c->d_cand); dfree(c->d_sel_key); c->key_cap = 0; c->pool_l1 = c->pool_ncand = 0; c->order_cap = 0; c->sort_tmp_bytes = 0; c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
+    dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); dfree(c->d_head_out); dfree(c->d_pool_pick); dfree(c->d_order); dfree(c->d_sort_tmp);
+    dfree(c->d_cand); dfree(c->d_sel_key); c->key_cap = 0; c->pool_l1 = c->pool_ncand = 0; c->order_cap = 0; c->sort_tmp_bytes = 0; c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
     dfree(c->d_dist_kind); dfree(c->d_dist_off); dfree(c->d_dist_val); dfree(c->d_dist_prob); dfree(c->d_dist_p0);
     dfree(c->d_dist_p1); dfree(c->d_dist_tmpl); c->has_dist = false;
     dfree(c->d_kslot); dfree(c->d_kix); dfree(c->d_kv); dfree(c->d_kcoef); c->k_valid = false;
+    dfree(c->d_sel_end); dfree(c->d_kp); dfree(c->d_ke); dfree(c->d_kraw); dfree(c->d_xaux); c->xaux_cap = 0; c->sel_cap_total = 0;
     dfree(c->d_d0); dfree(c->d_eidx); dfree(c->d_evals); dfree(c->d_stamps);
     dfree(c->d_wr_col); dfree(c->d_wr_val); dfree(c->d_wr_ocol); dfree(c->d_wr_oval); dfree(c->d_bslot); dfree(c->d_bix); dfree(c->d_bv);
     dfree(c->d_brptr); dfree(c->d_brcol); dfree(c->d_brval);
@@ -899,16 +899,35 @@ static int prepare_elements(twosd_ctx *c) {
     }
     int rc;
     if (c->CH > 0 && ((rc = upload(&c->d_kslot, ks)) || (rc = upload(&c->d_kix, ki)) || (rc = upload(&c->d_kv, kv)))) return rc;
+    if (c->CH > 0 && c->pool.size() > 1) {
+        // device selection-stream inputs: CSR rows of every basis, and a static record capacity
+        // per basis (every row active: m row starts + all its entries)
+        const int P = (int)c->pool.size();
+        std::vector<int> kp, ke, cap(P + 1, 0);
+        std::vector<double> kr;
+        kp.reserve((size_t)P * (m + 1));
+        for (int p = 0; p < P; ++p) {
+            const PoolBasis &B = c->pool[p];
+            const int base = (int)ke.size();
+            for (int i = 0; i <= m; ++i) kp.push_back(base + B.kptr[i]);
+            ke.insert(ke.end(), B.ke.begin(), B.ke.end());
+            kr.insert(kr.end(), B.kraw.begin(), B.kraw.end());
+            cap[p + 1] = cap[p] + m + (int)B.ke.size();
+        }
+        if (ke.empty()) { ke.push_back(0); kr.push_back(0.0); }
+        if ((rc = upload(&c->d_kp, kp)) || (rc = upload(&c->d_ke, ke)) || (rc = upload(&c->d_kraw, kr)) ||
+            (rc = upload(&c->d_sel_ptr, cap)))
+            return rc;
+        dfree(c->d_sel_code);
+        dfree(c->d_sel_end);
+        dfree(c->d_sel_cinf);
+        if ((rc = dalloc(&c->d_sel_code, 2 * (size_t)std::max(cap[P], 1))) || (rc = dalloc(&c->d_sel_end, (size_t)P)) ||
+            (rc = dalloc(&c->d_sel_cinf, (size_t)P)))
+            return rc;
+        c->sel_cap_total = cap[P];
+    }
     c->k_valid = true;
     return TWOSD_OK;
-}
-
-// primal infeasibility of a basic variable at value x (h_infeas of lp_hyper.hip, tolerance 1e-9)
-static double host_infeas(double x, int bt) {
-    const double tol = 1e-9;
-    if (bt == BT_Y || bt == BT_L) return x < -tol ? x : 0.0;
-    if (bt == BT_G) return x > tol ? x : 0.0;
-    return std::fabs(x) > tol ? x : 0.0;
 }
 
 // x_B of every pool basis at b: xbase[p][i] = sum_q B_p^{-1}[i][col_q] b[col_q] over the CSR
@@ -924,6 +943,133 @@ __global__ void pool_xbase_kernel(int P, int MP, const int *__restrict__ brptr, 
     xbase[t] = s;
 }
 
+// primal infeasibility of a basic variable at value x (h_infeas of lp_hyper.hip, tolerance 1e-9)
+__device__ __forceinline__ double dev_infeas(double x, int bt) {
+    const double tol = 1e-9;
+    if (bt == BT_Y || bt == BT_L) return x < -tol ? x : 0.0;
+    if (bt == BT_G) return x > tol ? x : 0.0;
+    return fabs(x) > tol ? x : 0.0;
+}
+
+// Selection stream of one pool basis per block (prepare_x, per x; hb0 = head * 4 + bound type): the rows of basis p that can
+// turn infeasible on the training box of the deltas, ordered by their worst box infeasibility
+// (largest first, row index on ties), each written as a row-start record (-1 - bound type,
+// x_B,i) followed by its element entries (e, B_p^{-1}[i][row_e]) at the basis's static capacity
+// offset; rows without entries add their constant infeasibility to cinf[p] (fixed-order sum).
+constexpr int kSelStreamThreads = 256;
+constexpr int kSelStreamRows = 1024;   // MP <= 1024 (R <= 16)
+__global__ void __launch_bounds__(kSelStreamThreads) pool_selstream_kernel(
+    int m, int MP, int k, const double *__restrict__ xbase, const int *__restrict__ hb0,
+    const int *__restrict__ kp, const int *__restrict__ ke, const double *__restrict__ kraw, const double *__restrict__ xaux,
+    int box, int order_rows, float cw, const int *__restrict__ scap, int2 *__restrict__ rec, int *__restrict__ send,
+    float *__restrict__ cinf) {
+    __shared__ double skey[kSelStreamRows];
+    __shared__ int sidx[kSelStreamRows];
+    __shared__ int soff[kSelStreamRows];
+    __shared__ float cpart[kSelStreamThreads];
+    __shared__ int tsum[kSelStreamThreads];
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const double *coef = xaux + m, *lo_e = xaux + m + k, *hi_e = xaux + m + 2 * k;
+    const int *kpp = kp + (size_t)p * (m + 1);
+    float cf = 0.0f;
+    for (int i = tid; i < kSelStreamRows; i += kSelStreamThreads) {
+        double key = INFINITY;   // inactive rows sort last
+        if (i < m) {
+            const int t = (hb0[(size_t)p * MP + i] & 3);
+            const double xv = xbase[(size_t)p * MP + i];
+            const int q0 = kpp[i], q1 = kpp[i + 1];
+            if (q0 == q1) {
+                const double f = fabs(dev_infeas(xv, t));
+                cf += (float)f + (f > 0.0 ? cw : 0.0f);
+            } else {
+                double worst = 0.0;
+                bool active = true;
+                if (box) {
+                    double lo = xv, hi = xv, mag = fabs(xv);
+                    for (int q = q0; q < q1; ++q) {
+                        const int e = ke[q];
+                        const double g = coef[e] * kraw[q];
+                        const double a = g * lo_e[e], bb = g * hi_e[e];
+                        lo += fmin(a, bb);
+                        hi += fmax(a, bb);
+                        mag += fmax(fabs(a), fabs(bb));
+                    }
+                    const double tol = 1e-9 + 1e-12 * mag;
+                    const bool feasible_box = (t == BT_Y || t == BT_L) ? lo > tol : (t == BT_G) ? hi < -tol : false;
+                    if (isfinite(lo) && isfinite(hi) && feasible_box) active = false;
+                    worst = (t == BT_Y || t == BT_L) ? -lo : (t == BT_G) ? hi : fmax(fabs(lo), fabs(hi));
+                    if (!isfinite(worst)) worst = HUGE_VAL;
+                }
+                if (active) key = order_rows ? -worst : 0.0;
+            }
+        }
+        skey[i] = key;
+        sidx[i] = i;
+    }
+    cpart[tid] = cf;
+    __syncthreads();
+    // bitonic sort of (key, row) ascending: (-worst, i) lexicographic = the host's stable sort
+    for (int kk = 2; kk <= kSelStreamRows; kk <<= 1) {
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            for (int t2 = tid; t2 < kSelStreamRows / 2; t2 += kSelStreamThreads) {
+                const int a = 2 * j * (t2 / j) + (t2 % j), b2 = a + j;
+                const bool up = (a & kk) == 0;
+                const double ka = skey[a], kb = skey[b2];
+                const int ia = sidx[a], ib = sidx[b2];
+                const bool gt = ka > kb || (ka == kb && ia > ib);
+                if (gt == up) {
+                    skey[a] = kb; skey[b2] = ka;
+                    sidx[a] = ib; sidx[b2] = ia;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // records per sorted position, exclusive scan (4 consecutive positions per thread)
+    constexpr int PER = kSelStreamRows / kSelStreamThreads;
+    int loc[PER], run = 0;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int sp = tid * PER + u;
+        const int i = sidx[sp];
+        const int c = skey[sp] != INFINITY ? 1 + kpp[i + 1] - kpp[i] : 0;
+        loc[u] = run;
+        run += c;
+    }
+    tsum[tid] = run;
+    __syncthreads();
+    if (tid == 0) {   // fixed-order sums: 256 partials (records, constant-row infeasibility)
+        int acc = 0;
+        float cacc = 0.0f;
+        for (int t = 0; t < kSelStreamThreads; ++t) {
+            const int v = tsum[t];
+            tsum[t] = acc;
+            acc += v;
+            cacc += cpart[t];
+        }
+        send[p] = scap[p] + acc;
+        cinf[p] = cacc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < PER; ++u) soff[tid * PER + u] = tsum[tid] + loc[u];
+    __syncthreads();
+    // emit: one wave per sorted row at a time, the row's entries written by consecutive lanes
+    const int lane = tid & 63, wv = tid >> 6;
+    const size_t base = (size_t)scap[p];
+    for (int sp = wv; sp < kSelStreamRows; sp += kSelStreamThreads / 64) {
+        if (skey[sp] == INFINITY) break;   // sorted: the inactive rows are all at the end
+        const int i = sidx[sp];
+        const int q0 = kpp[i], q1 = kpp[i + 1];
+        int2 *out = rec + base + soff[sp];
+        if (lane == 0) {
+            const int t = (hb0[(size_t)p * MP + i] & 3);
+            out[0] = make_int2(-1 - t, __float_as_int((float)xbase[(size_t)p * MP + i]));
+        }
+        for (int q = q0 + lane; q < q1; q += 64) out[1 + q - q0] = make_int2(ke[q], __float_as_int((float)kraw[q]));
+    }
+}
+
 // copy n host elements to a device array grown only when n exceeds its capacity
 template <typename T>
 static int upload_cap(T **d, size_t *cap, const T *h, size_t n) {
@@ -935,23 +1081,6 @@ static int upload_cap(T **d, size_t *cap, const T *h, size_t n) {
     }
     if (n) HIPCHK(hipMemcpy(*d, h, sizeof(T) * n, hipMemcpyHostToDevice));
     return TWOSD_OK;
-}
-
-// run fn(p) for p in [0, P) on up to 16 host threads (every p independent: the result does not
-// depend on the thread count)
-template <typename F>
-static void parallel_over(int P, F fn) {
-    const int nth = (int)std::max(1u, std::min({16u, std::thread::hardware_concurrency(), (unsigned)std::max(P / 8, 1)}));
-    if (nth == 1) {
-        for (int p = 0; p < P; ++p) fn(p);
-        return;
-    }
-    std::vector<std::thread> th;
-    for (int t = 0; t < nth; ++t)
-        th.emplace_back([&, t]() {
-            for (int p = t; p < P; p += nth) fn(p);
-        });
-    for (auto &t : th) t.join();
 }
 
 // per-x shared data: b = r - T x; per pool basis xbase_p = B_p^{-1} b (sparse rows);
@@ -970,95 +1099,60 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
     const int P = (int)c->pool.size();
     std::vector<double> coef(std::max(k, 1), 1.0);
     for (int e = 0; e < k; ++e) coef[e] = c->pos_col[e] < 0 ? 1.0 : -x[c->pos_col[e]];
-    std::vector<double> &xb = c->h_xb;
-    xb.resize((size_t)P * MP);
-    const bool sel = P > 1 && c->CH > 0;
-    std::vector<int8_t> bt;
-    if (sel) {
-        bt.resize(c->L.n + m);
-        HIPCHK(hipMemcpy(bt.data(), c->d_btype, bt.size(), hipMemcpyDeviceToHost));
-        if (const char *e = getenv("TWOSD_SEL_CW")) c->sel_cw = (float)atof(e);   // selection-key experiments
-    }
-    std::vector<float> cinf(P, 0.0f);
-    std::vector<std::vector<int>> &pcode = c->h_pcode;   // per basis: interleaved (code, float bits) records
-    pcode.resize(sel ? P : 0);
-    std::vector<int64_t> prows(P, 0);
-    const bool box = !c->sel_lo.empty();
-    static const bool sel_order = !getenv("TWOSD_SEL_ROWORDER") || atoi(getenv("TWOSD_SEL_ROWORDER")) != 0;   // A/B knob
-    parallel_over(P, [&](int p) {
-        const PoolBasis &B = c->pool[p];
-        double *xp = xb.data() + (size_t)p * MP;
-        for (int i = 0; i < m; ++i) {
-            double s = 0.0;
-            for (int q = B.rptr[i]; q < B.rptr[i + 1]; ++q) s += B.rval[q] * b[B.rcol[q]];
-            xp[i] = s;
-        }
-        if (!sel) return;
-        std::vector<int> &sc = pcode[p];
-        sc.clear();
-        auto rec = [&](int code, double v) {
-            const float f = (float)v;
-            int bits;
-            std::memcpy(&bits, &f, 4);
-            sc.push_back(code);
-            sc.push_back(bits);
-        };
-        // active rows with the largest possible infeasibility over the training box first:
-        // a losing basis accumulates its key fastest, so the kernel's pruning drops it early
-        std::vector<std::pair<double, int>> act;
-        for (int i = 0; i < m; ++i) {
-            const int t = bt[B.head[i]];
-            const double xv = xp[i];
-            const int q0 = B.kptr[i], q1 = B.kptr[i + 1];
-            if (q0 == q1) {
-                const double f = std::fabs(host_infeas(xv, t));
-                cinf[p] += (float)f + (f > 0.0 ? c->sel_cw : 0.0f);
-                continue;
-            }
-            double worst = 0.0;
-            if (box) {
-                // interval of x_i over the training box of the deltas: a row that stays
-                // feasible on the whole box never contributes, so it is left out
-                double lo = xv, hi = xv, mag = std::fabs(xv);
-                for (int q = q0; q < q1; ++q) {
-                    const double g = coef[B.ke[q]] * B.kraw[q];
-                    const double a = g * c->sel_lo[B.ke[q]], bb = g * c->sel_hi[B.ke[q]];
-                    lo += std::min(a, bb);
-                    hi += std::max(a, bb);
-                    mag += std::max(std::fabs(a), std::fabs(bb));
-                }
-                const double tol = 1e-9 + 1e-12 * mag;
-                const bool feasible_box = (t == BT_Y || t == BT_L) ? lo > tol : (t == BT_G) ? hi < -tol : false;
-                if (std::isfinite(lo) && std::isfinite(hi) && feasible_box) continue;
-                worst = (t == BT_Y || t == BT_L) ? -lo : (t == BT_G) ? hi : std::max(std::fabs(lo), std::fabs(hi));
-                if (!std::isfinite(worst)) worst = HUGE_VAL;
-            }
-            act.push_back({-worst, i});
-        }
-        if (sel_order) std::stable_sort(act.begin(), act.end());
-        for (const auto &a : act) {
-            const int i = a.second;
-            rec(-1 - bt[B.head[i]], xp[i]);
-            ++prows[p];
-            for (int q = B.kptr[i]; q < B.kptr[i + 1]; ++q) rec(B.ke[q], B.kraw[q]);
-        }
-    });
-    // device x_B from the device copy of the pool's B^{-1} rows (no P x MP upload)
-    if ((rc = upload_cap(&c->d_bvec, &c->bvec_cap, b.data(), b.size())) ||
-        (rc = upload_cap(&c->d_kcoef, &c->kcoef_cap, coef.data(), coef.size())))
-        return rc;
     if (!c->d_xbase || (size_t)P * MP > c->xbase_cap) {
         if ((rc = dalloc(&c->d_xbase, (size_t)P * MP))) return rc;
         c->xbase_cap = (size_t)P * MP;
     }
     if (c->CH > 0) {
+        // everything per x on the device: one upload of [b, coef, box lo, box hi], x_B of every
+        // pool basis, then the selection stream (pool_selstream_kernel)
+        const bool sel = P > 1;
+        const bool box = !c->sel_lo.empty();
+        std::vector<double> aux((size_t)m + 3 * (size_t)k, 0.0);
+        std::copy(b.begin(), b.end(), aux.begin());
+        std::copy(coef.begin(), coef.begin() + k, aux.begin() + m);
+        if (box) {
+            std::copy(c->sel_lo.begin(), c->sel_lo.end(), aux.begin() + m + k);
+            std::copy(c->sel_hi.begin(), c->sel_hi.end(), aux.begin() + m + 2 * k);
+        }
+        if ((rc = upload_cap(&c->d_xaux, &c->xaux_cap, aux.data(), aux.size())) ||
+            (rc = upload_cap(&c->d_kcoef, &c->kcoef_cap, coef.data(), coef.size())))
+            return rc;
         const size_t tot = (size_t)P * MP;
         hipLaunchKernelGGL(pool_xbase_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, P, MP, c->d_brptr,
-                           c->d_brcol, c->d_brval, c->d_bvec, c->d_xbase);
+                           c->d_brcol, c->d_brval, c->d_xaux, c->d_xbase);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipStreamSynchronize(c->stream));
+        if (sel) {
+            if (MP > kSelStreamRows) return fail(TWOSD_E_UNSUPPORTED, "pool selection: m = %d rows > %d", m, kSelStreamRows);
+            if (const char *e = getenv("TWOSD_SEL_CW")) c->sel_cw = (float)atof(e);   // selection-key experiments
+            static const bool sel_order = !getenv("TWOSD_SEL_ROWORDER") || atoi(getenv("TWOSD_SEL_ROWORDER")) != 0;   // A/B knob
+            hipLaunchKernelGGL(pool_selstream_kernel, dim3(P), dim3(kSelStreamThreads), 0, c->stream, m, MP, k, c->d_xbase,
+                               c->d_hb0, c->d_kp, c->d_ke, c->d_kraw, c->d_xaux, box ? 1 : 0, sel_order ? 1 : 0,
+                               c->sel_cw, c->d_sel_ptr, reinterpret_cast<int2 *>(c->d_sel_code), c->d_sel_end, c->d_sel_cinf);
+            HIPCHK(hipGetLastError());
+        }
+        if (getenv("TWOSD_DEBUG") && sel) {
+            HIPCHK(hipStreamSynchronize(c->stream));
+            std::vector<int> beg(P + 1), end(P);
+            HIPCHK(hipMemcpy(beg.data(), c->d_sel_ptr, sizeof(int) * (P + 1), hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(end.data(), c->d_sel_end, sizeof(int) * P, hipMemcpyDeviceToHost));
+            c->sel_nnz = 0;
+            for (int p = 0; p < P; ++p) c->sel_nnz += end[p] - beg[p];
+            c->sel_rows = 0;
+        }
     } else {
+        // dense kernel: x_B of the primary basis and dense B0K on the host
+        std::vector<double> xb((size_t)P * MP, 0.0);
+        for (int p = 0; p < P; ++p) {
+            const PoolBasis &B = c->pool[p];
+            for (int i = 0; i < m; ++i) {
+                double s = 0.0;
+                for (int q = B.rptr[i]; q < B.rptr[i + 1]; ++q) s += B.rval[q] * b[B.rcol[q]];
+                xb[(size_t)p * MP + i] = s;
+            }
+        }
         HIPCHK(hipMemcpy(c->d_xbase, xb.data(), sizeof(double) * xb.size(), hipMemcpyHostToDevice));
+        if ((rc = upload_cap(&c->d_kcoef, &c->kcoef_cap, coef.data(), coef.size()))) return rc;
     }
     if (!c->use_hyper) {
         std::vector<double> bk((size_t)std::max(k, 1) * MP, 0.0);
@@ -1068,37 +1162,14 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
         }
         if ((rc = upload_cap(&c->d_B0K, &c->b0k_cap, bk.data(), bk.size()))) return rc;
     }
-    if (sel) {
-        // concatenate the per-basis streams into pinned staging (fast upload), in pool order
-        std::vector<int> sptr(1, 0);
-        std::vector<size_t> off(P + 1, 0);
-        for (int p = 0; p < P; ++p) off[p + 1] = off[p] + pcode[p].size();
-        const size_t tot = off[P];
-        if (tot > c->h_scode_cap || !c->h_scode) {
-            if (c->h_scode) hipHostFree(c->h_scode);
-            c->h_scode = nullptr;
-            const size_t cap = std::max<size_t>(tot + tot / 4, 1024);
-            HIPCHK(hipHostMalloc((void **)&c->h_scode, sizeof(int) * cap, hipHostMallocDefault));
-            c->h_scode_cap = cap;
-        }
-        parallel_over(P, [&](int p) { std::copy(pcode[p].begin(), pcode[p].end(), c->h_scode + off[p]); });
-        c->sel_rows = 0;
-        for (int p = 0; p < P; ++p) {
-            sptr.push_back((int)(off[p + 1] / 2));
-            c->sel_rows += prows[p];
-        }
-        if ((rc = upload_cap(&c->d_sel_cinf, &c->cinf_cap, cinf.data(), cinf.size())) ||
-            (rc = upload_cap(&c->d_sel_ptr, &c->sptr_cap, sptr.data(), sptr.size())) ||
-            (rc = upload_cap(&c->d_sel_code, &c->scode_cap, (const int *)c->h_scode, tot)))
-            return rc;
-        c->sel_nnz = (int64_t)tot / 2 - c->sel_rows;
-    }
     c->prep_x.assign(x, x + n1);
     c->prep_valid = true;
-    if (getenv("TWOSD_DEBUG"))
+    if (getenv("TWOSD_DEBUG")) {
+        HIPCHK(hipStreamSynchronize(c->stream));
         fprintf(stderr, "prepare_x: P=%d %.3f ms (%lld selection records)\n", P,
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count(),
                 (long long)(c->sel_nnz + c->sel_rows));
+    }
     return TWOSD_OK;
 }
 
@@ -1127,7 +1198,7 @@ static int select_pool(twosd_ctx *c, const double *d_dv, int N, int *d_pick, int
     PoolSelParams S{};
     S.N = N; S.k = c->k; S.npool = np1; S.dv = d_dv;
     S.kcoef = c->d_kcoef;
-    S.cinf = c->d_sel_cinf; S.sptr = c->d_sel_ptr; S.rec = reinterpret_cast<const int2 *>(c->d_sel_code);
+    S.cinf = c->d_sel_cinf; S.sptr = c->d_sel_ptr; S.send = c->d_sel_end; S.rec = reinterpret_cast<const int2 *>(c->d_sel_code);
     S.pick = d_pick;
     S.cw = c->sel_cw;
     S.key = two ? c->d_sel_key : nullptr;
@@ -1136,7 +1207,7 @@ static int select_pool(twosd_ctx *c, const double *d_dv, int N, int *d_pick, int
         HIPCHK(sort_by_pool(d_pick, c->d_order, N, np1, c->d_sort_tmp, &tb, c->stream));
         PoolRefineParams Q{};
         Q.N = N; Q.k = c->k; Q.ncand = c->pool_ncand; Q.dv = d_dv; Q.kcoef = c->d_kcoef;
-        Q.cinf = c->d_sel_cinf; Q.sptr = c->d_sel_ptr; Q.rec = S.rec;
+        Q.cinf = c->d_sel_cinf; Q.sptr = c->d_sel_ptr; Q.send = c->d_sel_end; Q.rec = S.rec;
         Q.order = c->d_order; Q.cand = c->d_cand; Q.pick = d_pick; Q.key = c->d_sel_key; Q.cw = c->sel_cw;
         HIPCHK(launch_pool_refine(Q, c->stream));
     }

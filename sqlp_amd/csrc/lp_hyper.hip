@@ -674,7 +674,7 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_select_kernel(PoolSelPara
         // no load depends on the loop state, so the stream pipelines through the scalar cache
         float inf = S.cinf[p], x = 0.0f;
         int bt = -1;
-        const int j0 = S.sptr[p], j1 = S.sptr[p + 1];
+        const int j0 = S.sptr[p], j1 = S.send[p];
         auto step = [&](int code, float v, float dl) {
             if (code < 0) {
                 if (bt >= 0) inf += h_infeas_f(x, bt, S.cw);
@@ -735,7 +735,12 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_refine_kernel(PoolRefineP
     __shared__ int rci[kSelWaves][64];
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int t0 = blockIdx.x * 64;
+    // XCD-aware tile remap: consecutive tiles (the same level-1 pick group, the same candidate
+    // record streams) go to blocks b, b + 8, ... which share one XCD's L2 under round-robin
+    // placement (speed only; any bijection is correct)
+    const int nb = gridDim.x, b = blockIdx.x, xq = nb >> 3, xr = nb & 7, xc = b & 7;
+    const int tile = xc * xq + min(xc, xr) + (b >> 3);
+    const int t0 = tile * 64;
     const int k = S.k;
     const int nv = min(64, S.N - t0);
     for (int idx = threadIdx.x; idx < 64 * k; idx += 64 * kSelWaves) {
@@ -768,7 +773,7 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_refine_kernel(PoolRefineP
                     x = fmaf(v, dl, x);
                 }
             };
-            const int j0 = S.sptr[cb], j1 = S.sptr[cb + 1];
+            const int j0 = S.sptr[cb], j1 = S.send[cb];
             int j = (__ballot(mine && inf < best) == 0) ? j1 : j0;
             for (; j + 8 <= j1; j += 8) {
                 int2 rc[8];

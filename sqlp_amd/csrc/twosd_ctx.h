@@ -56,6 +56,14 @@ struct twosd_ctx {
     // pool selection data (per x, prepare_x): constant-row infeasibility, active rows, entries
     float *d_sel_cinf = nullptr;
     int *d_sel_ptr = nullptr, *d_sel_code = nullptr;   // code: (code, float bits) record pairs
+    int *d_sel_end = nullptr;            // npool: end of each basis's records (begin = d_sel_ptr, static capacity)
+    // x-independent element rows of the pool on the device (CSR, pool-strided kp: npool x (m+1)
+    // absolute offsets into ke / kraw), inputs of the device selection-stream build
+    int *d_kp = nullptr, *d_ke = nullptr;
+    double *d_kraw = nullptr;
+    double *d_xaux = nullptr;            // per x: b (m), coef (k), box lo (k), box hi (k)
+    size_t xaux_cap = 0;
+    int64_t sel_cap_total = 0;           // records the static capacity layout holds
     int64_t sel_nnz = 0, sel_rows = 0;
     float sel_cw = 0.0f;                 // pool selection key: sum |infeas| + sel_cw * #infeasible rows
     std::vector<double> sel_lo, sel_hi;   // training box of the deltas (empty: no row pruning)
@@ -77,13 +85,7 @@ struct twosd_ctx {
     double *d_kcoef = nullptr;    // k: coef_e(x) = 1 (RHS element) or -x[col] (T element)
     std::vector<double> prep_x;
     // capacities of the per-x device arrays (prepare_x re-uploads in place, no hipFree/hipMalloc per x)
-    size_t xbase_cap = 0, b0k_cap = 0, kcoef_cap = 0, cinf_cap = 0, sptr_cap = 0, scode_cap = 0;
-    double *d_bvec = nullptr;     // m: r - T x at the prepared x (x_B of the pool computed on the device)
-    size_t bvec_cap = 0;
-    std::vector<double> h_xb;     // host x_B of the pool (selection stream values), kept across x
-    std::vector<std::vector<int>> h_pcode;   // per-basis selection records, kept across x
-    int *h_scode = nullptr;       // pinned staging of the selection stream
-    size_t h_scode_cap = 0;
+    size_t xbase_cap = 0, b0k_cap = 0, kcoef_cap = 0;
     // hypersparse kernel data
     int CH = 0;                   // column slots per lane of the hypersparse kernel
     bool use_hyper = true;

@@ -94,7 +94,7 @@ struct PoolSelParams {
     const double *dv;                                   // N x k
     const double *kcoef;                                // k: coef_e(x)
     const float *cinf;                                  // npool: infeasibility of the constant rows
-    const int *sptr;                                    // npool + 1 -> flat stream of active rows
+    const int *sptr, *send;                             // npool: [sptr[p], send[p]) = records of basis p
     const int2 *rec;                                    // (code, float bits): row start (-1 - bound type,
                                                         //   xbase_i); entry (e, B^{-1}[i][row_e])
     int *pick;                                          // N out
@@ -107,7 +107,7 @@ struct PoolRefineParams {
     int N, k, ncand;
     const double *dv, *kcoef;
     const float *cinf;
-    const int *sptr;
+    const int *sptr, *send;
     const int2 *rec;
     const int *order, *cand;
     int *pick;                                          // N in (level 1) / out
