@@ -90,11 +90,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-dedup", action="store_true")
-    ap.add_argument("--pool", type=int, default=512, help="warm-start basis pool size (1 = primary basis only)")
+    ap.add_argument("--pool", type=int, default=4096, help="warm-start basis pool size (1 = primary basis only)")
     ap.add_argument("--pool-train", type=int, default=16384, help="training scenarios of the pool build")
-    ap.add_argument("--pool-level1", type=int, default=0,
+    ap.add_argument("--pool-level1", type=int, default=128,
                     help="two-level warm-start selection: level 1 over the first L pool bases (0: flat)")
-    ap.add_argument("--pool-cands", type=int, default=16, help="level-2 candidate bases per level-1 basis")
+    ap.add_argument("--pool-cands", type=int, default=128, help="level-2 candidate bases per level-1 basis")
     ap.add_argument("--cand-train", type=int, default=65536, help="training scenarios of the candidate lists")
     ap.add_argument("--sampler", choices=["device", "host"], default="device",
                     help="scenario draws: on-device Philox4x32-10 sampler (twosd_add_sampled_scenarios) or numpy PCG64")
@@ -110,11 +110,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
-    device = torch.device("cuda", local_rank)
+    # TWOSD_BENCH_SHARED_GPU=1 (rehearsal only): every rank on cuda:0 with gloo collectives,
+    # so the N > 1 path can be exercised on a one-GPU box; the real run is one rank per GPU
+    # over RCCL
+    shared = os.environ.get("TWOSD_BENCH_SHARED_GPU") == "1"
+    device = torch.device("cuda", 0 if shared else local_rank)
     torch.cuda.set_device(device)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
     from sqlp_amd import smps, twosd
     from sqlp_amd import dist as sdist
 
@@ -125,7 +132,7 @@ def main():
     with open(os.path.join(ROOT, "tests", "golden", "ev_x.json")) as f:
         x = np.array(json.load(f)[name]["x"])
     positions = list(sto.indep.keys())
-    ctx = twosd.SDContext(sp2, sto, device=local_rank)
+    ctx = twosd.SDContext(sp2, sto, device=device.index)
     ctx.compute_basis(x, smps.mean_values(sto, positions))
 
     if args.sampler == "device":
