@@ -824,7 +824,7 @@ hipError_t launch_pool_select(const PoolSelParams &p, hipStream_t s) {
 
 // ---- dispatch: R in {1,2,4,9,16}, C in {2,4,8,16,32,64}
 static const int kHR[] = {1, 2, 4, 9, 16};
-static const int kHC[] = {2, 4, 8, 16, 32, 64};
+static const int kHC[] = {2, 4, 8, 14, 16, 28, 32, 64};   // 14 / 28: ssn / storm exactly (fewer d[] registers)
 
 int hyper_rows_per_lane(int m) {
     for (int R : kHR)
@@ -852,6 +852,7 @@ static int ho(size_t lds) {
 #ifdef HYP_DEV_STORM_ONLY   // development builds: the storm instance (R = 9, C = 32) only
 #define HYPER_C_SWITCH(R, FN, ...)                  \
     switch (C) {                                    \
+        case 28: if (R == 9) return FN<9, 28>(__VA_ARGS__); \
         case 32: if (R == 9) return FN<9, 32>(__VA_ARGS__); \
     }
 #else
@@ -860,7 +861,9 @@ static int ho(size_t lds) {
         case 2: return FN<R, 2>(__VA_ARGS__);       \
         case 4: return FN<R, 4>(__VA_ARGS__);       \
         case 8: return FN<R, 8>(__VA_ARGS__);       \
+        case 14: return FN<R, 14>(__VA_ARGS__);     \
         case 16: return FN<R, 16>(__VA_ARGS__);     \
+        case 28: return FN<R, 28>(__VA_ARGS__);     \
         case 32: return FN<R, 32>(__VA_ARGS__);     \
         case 64: return FN<R, 64>(__VA_ARGS__);     \
     }

@@ -18,7 +18,7 @@ import shutil
 import sys
 from collections import defaultdict
 
-KERNELS = ["lp_hyper_kernel", "pool_select_kernel", "cut_argmax_kernel", "cut_fixup_kernel", "cut_vbase_kernel",
+KERNELS = ["lp_hyper_kernel", "pool_select_kernel", "pool_refine_kernel", "pool_selstream_kernel", "pool_xbase_kernel", "cut_argmax_kernel", "cut_fixup_kernel", "cut_vbase_kernel",
            "cut_pk_kernel", "dvs_batch_kernel", "dvs_lookup_kernel", "dvs_assign_kernel"]
 
 
