@@ -106,6 +106,15 @@ size_t hyper_lds_bytes(int R, int ncol, int kmax, int k) { return (size_t)kWaves
 
 // min waves per SIMD (VGPR budget 256 / 168): measured on MI355X, storm (R=9) is fastest
 // at 2 waves/SIMD, ssn (R=4) at 3 (tools/lp_speed.py)
+// loads in flight per memory round trip: etas per group (BTRAN / rho / FTRAN), W rows per
+// pricing group (A/B knobs of the development builds)
+#ifndef TWOSD_ETA_G
+#define TWOSD_ETA_G 4
+#endif
+#ifndef TWOSD_PRICE_G
+#define TWOSD_PRICE_G 8
+#endif
+constexpr int EG = TWOSD_ETA_G;
 #ifndef TWOSD_HYPER_WPE
 #define TWOSD_HYPER_WPE(R) ((R) >= 9 ? 2 : 3)
 #endif
@@ -238,11 +247,11 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             h_wave_sync();
             // etas in groups of 4: the group's entries (first 64 of each) are loaded together,
             // so one memory round trip serves four sequential steps
-            for (int tg = K - 1; tg >= 0; tg -= 4) {
-                int gi[4], gn[4], go[4];
+            for (int tg = K - 1; tg >= 0; tg -= EG) {
+                int gi[EG], gn[EG], go[EG];
                 double gv[4];
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
+                for (int g = 0; g < EG; ++g) {
                     const int tt = tg - g;
                     gi[g] = 0; gv[g] = 0.0; gn[g] = 0; go[g] = 0;
                     if (tt >= 0) {
@@ -252,7 +261,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                     }
                 }
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
+                for (int g = 0; g < EG; ++g) {
                     const int tt = tg - g;
                     if (tt < 0) break;
                     double acc = gv[g] != 0.0 ? ut[gi[g]] * gv[g] : 0.0;
@@ -267,11 +276,11 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             // rho = u' B0^{-1} as a row scatter over the nonzeros of u, which sit at r and at
             // the eta pivot rows; each row is consumed once (then zeroed), in the fixed order
             // r, etap[K-1], ..., etap[0], so the accumulation order is deterministic.
-            for (int tg = K; tg >= 0; tg -= 4) {
-                int gi[4], gn[4], gp[4], go[4];
+            for (int tg = K; tg >= 0; tg -= EG) {
+                int gi[EG], gn[EG], gp[EG], go[EG];
                 double gv[4];
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
+                for (int g = 0; g < EG; ++g) {
                     const int tt = tg - g;
                     gi[g] = 0; gv[g] = 0.0; gn[g] = 0; go[g] = 0; gp[g] = 0;
                     if (tt >= 0) {
@@ -282,7 +291,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                     }
                 }
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
+                for (int g = 0; g < EG; ++g) {
                     const int tt = tg - g;
                     if (tt < 0) break;
                     const double up = ut[gp[g]];
@@ -319,7 +328,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             for (int t = 0; t < R; ++t) {
                 uint64_t msk = __ballot(rv[t] != 0.0);
                 while (msk) {
-                    constexpr int G = 8;
+                    constexpr int G = TWOSD_PRICE_G;
                     int gi[G], gc[G];
                     double gr[G], gw[G];
 #pragma unroll
@@ -424,11 +433,11 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                     h_wave_sync();
                 }
             }
-            for (int tg = 0; tg < K; tg += 4) {
-                int gi[4], gn[4], go[4];
+            for (int tg = 0; tg < K; tg += EG) {
+                int gi[EG], gn[EG], go[EG];
                 double gv[4];
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
+                for (int g = 0; g < EG; ++g) {
                     const int tt = tg + g;
                     gi[g] = 0; gv[g] = 0.0; gn[g] = 0; go[g] = 0;
                     if (tt < K) {
@@ -438,7 +447,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                     }
                 }
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
+                for (int g = 0; g < EG; ++g) {
                     const int tt = tg + g;
                     if (tt >= K) break;
                     const int p = etap[tt];

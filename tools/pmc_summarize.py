@@ -43,6 +43,23 @@ def main():
             if k:
                 d = (float(r["End_Timestamp"]) - float(r["Start_Timestamp"])) / 1e6
                 dur[k] = max(dur.get(k, 0.0), d)
+    # timed-region stats: the trace run is bench.py --steps 2 --warmup 1, and every step starts
+    # with pool_xbase_kernel (invalidate_x), so the last two of those open the timed steps;
+    # per kernel: launches, average and total duration inside that region (the numbers the
+    # bench's HIP events time)
+    if traces:
+        rows = sorted(csv.DictReader(open(traces[0])), key=lambda r: int(r["Start_Timestamp"]))
+        starts = [i for i, r in enumerate(rows) if "pool_xbase_kernel" in r["Kernel_Name"]]
+        if len(starts) >= 2:
+            agg = defaultdict(list)
+            for r in rows[starts[-2]:]:
+                agg[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+            with open(os.path.join(dst, "timed_kernel_stats.csv"), "w", newline="") as fh:
+                wr = csv.writer(fh)
+                wr.writerow(["Name", "Calls", "AverageMs", "TotalMs", "MinMs", "MaxMs"])
+                for name, ds in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
+                    wr.writerow([name, len(ds), round(sum(ds) / len(ds), 6), round(sum(ds), 6), round(min(ds), 6),
+                                 round(max(ds), 6)])
     pmc = defaultdict(lambda: defaultdict(list))
     scratch = {}
     for tag in ("pmc_fetch", "pmc_write"):
