@@ -742,6 +742,7 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_refine_kernel(PoolRefineP
     extern __shared__ float dvt[];   // k x 65
     __shared__ float rkey[kSelWaves][64];
     __shared__ int rci[kSelWaves][64];
+    __shared__ unsigned sbest[64];   // best key so far over all waves, per scenario (as in level 1)
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // XCD-aware tile remap: consecutive tiles (the same level-1 pick group, the same candidate
@@ -763,6 +764,15 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_refine_kernel(PoolRefineP
     const float key1 = valid ? S.key[s] : 0.0f;
     float best = key1;
     int bci = -1;
+    if (wid == 0) sbest[lane] = __float_as_uint(key1);
+    __syncthreads();
+    // a candidate can still win for a lane only below the lane's own best (strict: the level-1
+    // pick and earlier candidates of this wave win ties) and not above any other wave's best
+    // (ties with other waves are settled by candidate index at the end)
+    auto alive = [&](bool mine, float inf) {
+        return mine && inf < best &&
+               inf <= __uint_as_float(__hip_atomic_load(&sbest[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    };
     uint64_t todo = __ballot(valid);
     while (todo) {
         const int g = __builtin_amdgcn_readlane(p1, __builtin_ctzll(todo));
@@ -783,7 +793,7 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_refine_kernel(PoolRefineP
                 }
             };
             const int j0 = S.sptr[cb], j1 = S.send[cb];
-            int j = (__ballot(mine && inf < best) == 0) ? j1 : j0;
+            int j = (__ballot(alive(mine, inf)) == 0) ? j1 : j0;
             for (; j + 8 <= j1; j += 8) {
                 int2 rc[8];
                 float dl[8];
@@ -793,14 +803,18 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_refine_kernel(PoolRefineP
                 for (int u = 0; u < 8; ++u) dl[u] = dvt[(rc[u].x < 0 ? 0 : rc[u].x) * 65 + lane];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) step(rc[u].x, __int_as_float(rc[u].y), dl[u]);
-                if (__ballot(mine && inf < best) == 0) { bt = -1; inf = INFINITY; j = j1; break; }
+                if (__ballot(alive(mine, inf)) == 0) { bt = -1; inf = INFINITY; j = j1; break; }
             }
             for (; j < j1; ++j) {
                 const int2 r = S.rec[j];
                 step(r.x, __int_as_float(r.y), dvt[(r.x < 0 ? 0 : r.x) * 65 + lane]);
             }
             if (bt >= 0) inf += h_infeas_f(x, bt, S.cw);
-            if (mine && inf < best) { best = inf; bci = ci; }
+            if (mine && inf < best) {
+                best = inf;
+                bci = ci;
+                atomicMin(&sbest[lane], __float_as_uint(inf));
+            }
         }
     }
     rkey[wid][lane] = best;
