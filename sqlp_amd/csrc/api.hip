@@ -134,7 +134,7 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_colptr); dfree(c->d_rowidx); dfree(c->d_val); dfree(c->d_q); dfree(c->d_btype);
     dfree(c->d_fixedmask); dfree(c->d_ubmask);
     dfree(c->d_hb0); dfree(c->d_basic0); dfree(c->d_B0inv); dfree(c->d_B0invT); dfree(c->d_pi0);
-    dfree(c->d_xbase); dfree(c->d_B0K); dfree(c->d_eta); dfree(c->d_queue);
+    dfree(c->d_xbase); dfree(c->d_B0K); dfree(c->d_eta); dfree(c->d_queue); dfree(c->d_lpstats);
     dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_ops);
     dfree(c->d_dvtmp);
     dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); dfree(c->d_head_out); dfree(c->d_pool_pick); dfree(c->d_order); dfree(c->d_sort_tmp);
@@ -1343,20 +1343,52 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
     return TWOSD_OK;
 }
 
+// batch statistics on the device (integer sums: exact, order independent): [0] pivots,
+// [1] executed FMAs, [2] max pivots, [3] non-optimal scenarios
+__global__ void lp_stats_kernel(int N, const int *__restrict__ its, const long long *__restrict__ ops,
+                                const int *__restrict__ st, unsigned long long *out) {
+    unsigned long long a = 0, b = 0, d = 0;
+    unsigned long long mx = 0;
+    for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < N; s += gridDim.x * blockDim.x) {
+        a += (unsigned long long)its[s];
+        b += (unsigned long long)ops[s];
+        mx = its[s] > (int)mx ? (unsigned long long)its[s] : mx;
+        d += st[s] != TWOSD_LP_OPTIMAL;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_down(a, o);
+        b += __shfl_down(b, o);
+        d += __shfl_down(d, o);
+        const unsigned long long m2 = __shfl_down(mx, o);
+        mx = m2 > mx ? m2 : mx;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&out[0], a);
+        atomicAdd(&out[1], b);
+        atomicMax(&out[2], mx);
+        atomicAdd(&out[3], d);
+    }
+}
+
 static int copy_lp_outputs(twosd_ctx *c, int N, double *obj, double *pi, double *y, int *status) {
+    if (!c->d_lpstats) {
+        int rc = dalloc(&c->d_lpstats, 4);
+        if (rc) return rc;
+    }
+    HIPCHK(hipMemsetAsync(c->d_lpstats, 0, 4 * sizeof(unsigned long long), c->stream));
+    hipLaunchKernelGGL(lp_stats_kernel, dim3((unsigned)std::min(1024, (N + 255) / 256)), dim3(256), 0, c->stream, N,
+                       c->d_iters, c->d_ops, c->d_status, c->d_lpstats);
+    HIPCHK(hipGetLastError());
+    unsigned long long stv[4];
+    HIPCHK(hipMemcpyAsync(stv, c->d_lpstats, sizeof(stv), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     if (obj) HIPCHK(hipMemcpy(obj, c->d_obj, sizeof(double) * N, hipMemcpyDeviceToHost));
     if (pi) HIPCHK(hipMemcpy(pi, c->d_pi, sizeof(double) * N * c->L.m, hipMemcpyDeviceToHost));
     if (y) HIPCHK(hipMemcpy(y, c->d_y, sizeof(double) * N * c->L.n, hipMemcpyDeviceToHost));
-    std::vector<int> st(N), its(N);
-    HIPCHK(hipMemcpy(st.data(), c->d_status, sizeof(int) * N, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(its.data(), c->d_iters, sizeof(int) * N, hipMemcpyDeviceToHost));
-    std::vector<long long> ops(N);
-    HIPCHK(hipMemcpy(ops.data(), c->d_ops, sizeof(long long) * N, hipMemcpyDeviceToHost));
-    int64_t sum = 0, osum = 0; int mx = 0, bad = 0;
-    for (int s = 0; s < N; ++s) { sum += its[s]; osum += ops[s]; mx = std::max(mx, its[s]); bad += st[s] != TWOSD_LP_OPTIMAL; }
-    c->last_pivots_sum = sum; c->last_pivots_max = mx; c->last_ops_sum = osum;
-    if (status) std::copy(st.begin(), st.end(), status);
-    if (bad) return fail(TWOSD_E_LP, "%d of %d scenario LPs not optimal (see status[])", bad, N);
+    if (status) HIPCHK(hipMemcpy(status, c->d_status, sizeof(int) * N, hipMemcpyDeviceToHost));
+    c->last_pivots_sum = (int64_t)stv[0]; c->last_ops_sum = (int64_t)stv[1]; c->last_pivots_max = (int)stv[2];
+    const long long bad = (long long)stv[3];
+    if (bad) return fail(TWOSD_E_LP, "%lld of %d scenario LPs not optimal (see status[])", bad, N);
     return TWOSD_OK;
 }
 

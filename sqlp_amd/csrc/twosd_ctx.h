@@ -111,6 +111,7 @@ struct twosd_ctx {
     size_t eta_slots = 0;
     int eta_kmax = 0;
     int *d_queue = nullptr;
+    unsigned long long *d_lpstats = nullptr;   // lp_stats_kernel output (4 words)
     double *d_obj = nullptr, *d_pi = nullptr, *d_y = nullptr;
     int *d_status = nullptr, *d_iters = nullptr;
     long long *d_ops = nullptr;

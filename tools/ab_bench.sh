@@ -5,7 +5,8 @@ NS=${2:-1000000}
 mkdir -p gpurun_out
 : > gpurun_out/abb.jsonl
 for v in $VARS; do
-  TWOSD_LIB=$v timeout -k 10 300 python bench.py --no-cpu --steps 3 --warmup 1 --scenarios $NS 2>>gpurun_out/abb.err | tail -1 | sed "s/^{/{\"lib\": \"$v\", /" >> gpurun_out/abb.jsonl || exit 1
+  if [ "$v" = default ]; then unset TWOSD_LIB; else export TWOSD_LIB=$v; fi
+  timeout -k 10 300 python bench.py --no-cpu --steps 3 --warmup 1 --scenarios $NS 2>>gpurun_out/abb.err | tail -1 | sed "s/^{/{\"lib\": \"$v\", /" >> gpurun_out/abb.jsonl || exit 1
 done
 python3 -c "
 import json
