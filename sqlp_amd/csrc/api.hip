@@ -905,6 +905,8 @@ static int prepare_elements(twosd_ctx *c) {
         const int P = (int)c->pool.size();
         std::vector<int> kp, ke, cap(P + 1, 0);
         std::vector<double> kr;
+        std::vector<int8_t> bt(c->L.n + m);
+        HIPCHK(hipMemcpy(bt.data(), c->d_btype, bt.size(), hipMemcpyDeviceToHost));
         kp.reserve((size_t)P * (m + 1));
         for (int p = 0; p < P; ++p) {
             const PoolBasis &B = c->pool[p];
@@ -912,7 +914,10 @@ static int prepare_elements(twosd_ctx *c) {
             for (int i = 0; i <= m; ++i) kp.push_back(base + B.kptr[i]);
             ke.insert(ke.end(), B.ke.begin(), B.ke.end());
             kr.insert(kr.end(), B.kraw.begin(), B.kraw.end());
-            cap[p + 1] = cap[p] + m + (int)B.ke.size();
+            int64_t cp = 0;   // every row active; rows of fixed (E) basics are emitted twice
+            for (int i = 0; i < m; ++i) cp += (int64_t)(1 + B.kptr[i + 1] - B.kptr[i]) * (bt[B.head[i]] == BT_E ? 2 : 1);
+            if (cap[p] + cp > INT32_MAX) return fail(TWOSD_E_UNSUPPORTED, "pool selection stream: > 2^31 records");
+            cap[p + 1] = cap[p] + (int)cp;
         }
         if (ke.empty()) { ke.push_back(0); kr.push_back(0.0); }
         if ((rc = upload(&c->d_kp, kp)) || (rc = upload(&c->d_ke, ke)) || (rc = upload(&c->d_kraw, kr)) ||
@@ -1032,7 +1037,7 @@ __global__ void __launch_bounds__(kSelStreamThreads) pool_selstream_kernel(
     for (int u = 0; u < PER; ++u) {
         const int sp = tid * PER + u;
         const int i = sidx[sp];
-        const int c = skey[sp] != INFINITY ? 1 + kpp[i + 1] - kpp[i] : 0;
+        const int c = skey[sp] != INFINITY ? (1 + kpp[i + 1] - kpp[i]) * ((hb0[(size_t)p * MP + i] & 3) == BT_E ? 2 : 1) : 0;
         loc[u] = run;
         run += c;
     }
@@ -1062,11 +1067,17 @@ __global__ void __launch_bounds__(kSelStreamThreads) pool_selstream_kernel(
         const int i = sidx[sp];
         const int q0 = kpp[i], q1 = kpp[i + 1];
         int2 *out = rec + base + soff[sp];
-        if (lane == 0) {
-            const int t = (hb0[(size_t)p * MP + i] & 3);
-            out[0] = make_int2(-1 - t, __float_as_int((float)xbase[(size_t)p * MP + i]));
+        // records are sign-folded so that the kernels' test is always "x' > tol": x' = -x for
+        // Y / L basics (infeasible below 0), x for G (above 0); a fixed (E) basic is written
+        // twice, with +x and -x (|x| > tol <=> one of them > tol)
+        const int t = hb0[(size_t)p * MP + i] & 3;
+        const int ncopy = t == BT_E ? 2 : 1;
+        for (int cpy = 0; cpy < ncopy; ++cpy) {
+            const float sg = (t == BT_Y || t == BT_L || cpy == 1) ? -1.0f : 1.0f;
+            int2 *o = out + cpy * (1 + q1 - q0);
+            if (lane == 0) o[0] = make_int2(-1, __float_as_int(sg * (float)xbase[(size_t)p * MP + i]));
+            for (int q = q0 + lane; q < q1; q += 64) o[1 + q - q0] = make_int2(ke[q], __float_as_int(sg * (float)kraw[q]));
         }
-        for (int q = q0 + lane; q < q1; q += 64) out[1 + q - q0] = make_int2(ke[q], __float_as_int((float)kraw[q]));
     }
 }
 

@@ -642,13 +642,9 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
 // The selection is a heuristic (any pool basis is a valid start; the choice only changes
 // pivot counts), so it runs in fp32: half the LDS traffic of the staged deltas, 8-byte
 // records (code, value) -- deterministic like everything else.
-__device__ __forceinline__ float h_infeas_f(float x, int bt, float cw) {
-    float v;
-    if (bt == BT_Y || bt == BT_L) v = x < -1e-9f ? -x : 0.0f;
-    else if (bt == BT_G) v = x > 1e-9f ? x : 0.0f;
-    else v = fabsf(x) > 1e-9f ? fabsf(x) : 0.0f;
-    return v > 0.0f ? v + cw : 0.0f;
-}
+// records are sign-folded by pool_selstream_kernel (x' = -x for Y / L basics, x for G, both
+// signs for E), so a row's infeasibility is x' when x' > tol
+__device__ __forceinline__ float h_viol_f(float x, float cw) { return x > 1e-9f ? x + cw : 0.0f; }
 
 constexpr int kSelWaves = 16;   // 16 waves share one staged 64-scenario tile (latency hiding)
 __global__ void __launch_bounds__(64 * kSelWaves) pool_select_kernel(PoolSelParams S) {
@@ -682,13 +678,11 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_select_kernel(PoolSelPara
         // value xbase_i) followed by the row's entries (code e, value B^{-1}[i][row_e]);
         // no load depends on the loop state, so the stream pipelines through the scalar cache
         float inf = S.cinf[p], x = 0.0f;
-        int bt = -1;
         const int j0 = S.sptr[p], j1 = S.send[p];
         auto step = [&](int code, float v, float dl) {
-            if (code < 0) {
-                if (bt >= 0) inf += h_infeas_f(x, bt, S.cw);
+            if (code < 0) {   // next row: close the previous one
+                inf += h_viol_f(x, S.cw);
                 x = v;
-                bt = -1 - code;
             } else {
                 x = fmaf(v, dl, x);
             }
@@ -705,13 +699,13 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_select_kernel(PoolSelPara
             for (int u = 0; u < 8; ++u) step(rc[u].x, __int_as_float(rc[u].y), dl[u]);
             // exact pruning: inf only grows (sum of nonnegative terms), so once no lane can
             // still beat its best, this basis cannot win for any of the 64 scenarios
-            if (__ballot(alive(inf)) == 0) { bt = -1; inf = INFINITY; j = j1; break; }
+            if (__ballot(alive(inf)) == 0) { x = 0.0f; inf = INFINITY; j = j1; break; }
         }
         for (; j < j1; ++j) {
             const int2 r = S.rec[j];
             step(r.x, __int_as_float(r.y), dvt[(r.x < 0 ? 0 : r.x) * 65 + lane]);
         }
-        if (bt >= 0) inf += h_infeas_f(x, bt, S.cw);
+        inf += h_viol_f(x, S.cw);
         if (inf < best) {
             best = inf;
             bp = p;
@@ -782,12 +776,10 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_refine_kernel(PoolRefineP
             const int cb = S.cand[(size_t)g * S.ncand + ci];
             if (cb < 0) break;
             float inf = S.cinf[cb], x = 0.0f;
-            int bt = -1;
             auto step = [&](int code, float v, float dl) {
-                if (code < 0) {
-                    if (bt >= 0) inf += h_infeas_f(x, bt, S.cw);
+                if (code < 0) {   // next row: close the previous one
+                    inf += h_viol_f(x, S.cw);
                     x = v;
-                    bt = -1 - code;
                 } else {
                     x = fmaf(v, dl, x);
                 }
@@ -803,13 +795,13 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_refine_kernel(PoolRefineP
                 for (int u = 0; u < 8; ++u) dl[u] = dvt[(rc[u].x < 0 ? 0 : rc[u].x) * 65 + lane];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) step(rc[u].x, __int_as_float(rc[u].y), dl[u]);
-                if (__ballot(alive(mine, inf)) == 0) { bt = -1; inf = INFINITY; j = j1; break; }
+                if (__ballot(alive(mine, inf)) == 0) { x = 0.0f; inf = INFINITY; j = j1; break; }
             }
             for (; j < j1; ++j) {
                 const int2 r = S.rec[j];
                 step(r.x, __int_as_float(r.y), dvt[(r.x < 0 ? 0 : r.x) * 65 + lane]);
             }
-            if (bt >= 0) inf += h_infeas_f(x, bt, S.cw);
+            inf += h_viol_f(x, S.cw);
             if (mine && inf < best) {
                 best = inf;
                 bci = ci;

@@ -95,8 +95,8 @@ struct PoolSelParams {
     const double *kcoef;                                // k: coef_e(x)
     const float *cinf;                                  // npool: infeasibility of the constant rows
     const int *sptr, *send;                             // npool: [sptr[p], send[p]) = records of basis p
-    const int2 *rec;                                    // (code, float bits): row start (-1 - bound type,
-                                                        //   xbase_i); entry (e, B^{-1}[i][row_e])
+    const int2 *rec;                                    // (code, float bits): row start (-1, sign-folded
+                                                        //   xbase_i); entry (e, sign * B^{-1}[i][row_e])
     int *pick;                                          // N out
     float cw;                                           // key = sum |infeas| + cw * #infeasible rows
     float *key;                                         // N out (nullable): key of the pick
