@@ -135,3 +135,29 @@ def test_lp_basis_pool(name):
     # set_basis resets the pool
     ctx.set_basis(head0)
     assert ctx.pool_size() == 1
+
+
+@pytest.mark.parametrize("groups", ["1", "3"])
+def test_lp_queue_groups(groups, monkeypatch):
+    """The XCD-grouped work queues (visiting order cut into qgroups contiguous ranges, idle
+    waves stealing from the next range) solve every scenario exactly once: objectives and
+    statuses equal the default 8-group run for 1 and 3 groups, with N not a multiple of
+    either, with and without a pool-grouped visiting order."""
+    from sqlp_amd import twosd
+    ctx, x = _ctx("storm")
+    N = 1237
+    vals = I.sample("storm", N, seed=5)
+    base, _, _, st0 = ctx.solve_values(x, vals)
+    tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(tr, I.sample("storm", 2048, seed=11))
+    ctx.pool_build(tr, x, 0, 2048, 16)
+    pooled, _, _, st1 = ctx.solve_values(x, vals)
+    monkeypatch.setenv("TWOSD_QGROUPS", groups)
+    for ref, st_ref in ((pooled, st1),):
+        obj, _, _, st = ctx.solve_values(x, vals)
+        assert (st == st_ref).all()
+        np.testing.assert_array_equal(obj, ref)
+    ctx.set_basis(ctx.get_basis())
+    obj, _, _, st = ctx.solve_values(x, vals)
+    assert (st == st0).all()
+    np.testing.assert_array_equal(obj, base)
