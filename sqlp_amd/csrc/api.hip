@@ -1277,8 +1277,8 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
         H.xbase = c->d_xbase; H.d0 = c->d_d0; H.hb0 = c->d_hb0;
         H.basic0 = c->d_basic0; H.fixedmask = c->d_fixedmask; H.ubmask = c->d_ubmask;
         H.dv = d_dv; H.eidx = c->d_eidx; H.evals = c->d_evals; H.queue = c->d_queue;
-        H.qgroups = std::max(1, std::min(kMaxQueueGroups, nblocks));
-        if (const char *e = getenv("TWOSD_QGROUPS")) H.qgroups = std::max(1, std::min(H.qgroups, atoi(e)));   // A/B knob
+        H.qgroups = std::max(1, std::min(16, nblocks));   // two ranges per XCD (8 / 16 / 32 / 64: 143.6 / 142.7 / 142.8 / 146.3 ms, storm 1M)
+        if (const char *e = getenv("TWOSD_QGROUPS")) H.qgroups = std::max(1, std::min({kMaxQueueGroups, nblocks, atoi(e)}));   // A/B knob
         H.obj = c->d_obj; H.pi = want_pi ? c->d_pi : nullptr; H.y = want_y ? c->d_y : nullptr;
         H.status = c->d_status; H.iters = c->d_iters; H.ops = c->d_ops;
         if (!c->d_stamps) {

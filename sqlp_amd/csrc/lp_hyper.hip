@@ -115,6 +115,13 @@ size_t hyper_lds_bytes(int R, int ncol, int kmax, int k) { return (size_t)kWaves
 #define TWOSD_PRICE_G 8
 #endif
 constexpr int EG = TWOSD_ETA_G;
+// unroll of the per-scenario gathers (x_B warm start, vertex recovery): loads in flight
+#ifndef TWOSD_XB_UNROLL
+#define TWOSD_XB_UNROLL 2
+#endif
+#ifndef TWOSD_REC_UNROLL
+#define TWOSD_REC_UNROLL 1
+#endif
 #ifndef TWOSD_HYPER_WPE
 #define TWOSD_HYPER_WPE(R) ((R) >= 9 ? 2 : 3)
 #endif
@@ -188,7 +195,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             const int i = 64 * t + lane;
             double x = P.xbase[(size_t)p * MP + i];
             const int e0 = P.kslot[p * (R + 1) + t], e1 = P.kslot[p * (R + 1) + t + 1];
-#pragma unroll 2
+#pragma unroll TWOSD_XB_UNROLL
             for (int e = e0; e < e1; ++e) x = fma(P.kv[(size_t)e * 64 + lane], dvl[P.kix[(size_t)e * 64 + lane]], x);
             return x;
         };
@@ -570,7 +577,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             for (int t = 0; t < R; ++t) {
                 const int e0 = bslot[t], e1 = bslot[t + 1];
                 double a = 0.0;
-#pragma unroll 1
+#pragma unroll TWOSD_REC_UNROLL
                 for (int e = e0; e < e1; ++e) {
                     const double v = P.bv[e * 64 + lane];
                     a = fma(ut[P.bix[e * 64 + lane]], v, a);

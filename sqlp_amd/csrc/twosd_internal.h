@@ -52,7 +52,7 @@ struct LpParams {
 
 // hypersparse kernel (lp_hyper.hip)
 constexpr int kQueueStride = 32;   // queue heads one 128-B line apart
-constexpr int kMaxQueueGroups = 8;
+constexpr int kMaxQueueGroups = 64;
 struct HyperParams {
     int m, n, k, N, kmax, ecap;
     const int *colptr, *rowidx; const double *val;      // W CSC
