@@ -115,6 +115,10 @@ size_t hyper_lds_bytes(int R, int ncol, int kmax, int k) { return (size_t)kWaves
 #define TWOSD_PRICE_G 8
 #endif
 constexpr int EG = TWOSD_ETA_G;
+// alpha~ slots read together in the Harris passes
+#ifndef TWOSD_HARRIS_B
+#define TWOSD_HARRIS_B 1
+#endif
 // unroll of the per-scenario gathers (x_B warm start, vertex recovery): loads in flight
 #ifndef TWOSD_XB_UNROLL
 #define TWOSD_XB_UNROLL 2
@@ -370,20 +374,31 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             }
             STAMP(4)
 
-            // Harris ratio test over the nonbasic columns (d in registers, alpha~ from LDS)
+            // Harris ratio test over the nonbasic columns (d in registers, alpha~ from LDS).  The
+            // alpha~ of HB slots are read together (unconditionally: masked slots are ignored), so
+            // HB LDS reads are in flight per wait instead of one
+            constexpr int HB = TWOSD_HARRIS_B;
             const double sg = delta > 0 ? 1.0 : -1.0;
             double thmax = INFINITY;
             uint64_t nzm = 0, elm = 0;
 #pragma unroll
-            for (int c = 0; c < C; ++c) {
-                const uint64_t bit = 1ull << c;
-                if ((bmask | fixedm) & bit) continue;
-                const double a = sg * alpha[64 * c + lane];
-                if (a != 0.0) nzm |= bit;
-                const bool atlb = !(ubm & bit);
-                if (atlb ? a > HTOL_PIV : a < -HTOL_PIV) {
-                    elm |= bit;
-                    thmax = fmin(thmax, ((atlb ? d[c] + HTOL_D : d[c] - HTOL_D)) / a);
+            for (int c0 = 0; c0 < C; c0 += HB) {
+                double av[HB];
+#pragma unroll
+                for (int u = 0; u < HB; ++u) av[u] = (HB == 1 || c0 + u < C) ? alpha[64 * (c0 + u) + lane] : 0.0;
+#pragma unroll
+                for (int u = 0; u < HB; ++u) {
+                    const int c = c0 + u;
+                    if (c >= C) break;
+                    const uint64_t bit = 1ull << c;
+                    if ((bmask | fixedm) & bit) continue;
+                    const double a = sg * av[u];
+                    if (a != 0.0) nzm |= bit;
+                    const bool atlb = !(ubm & bit);
+                    if (atlb ? a > HTOL_PIV : a < -HTOL_PIV) {
+                        elm |= bit;
+                        thmax = fmin(thmax, ((atlb ? d[c] + HTOL_D : d[c] - HTOL_D)) / a);
+                    }
                 }
             }
             thmax = wmin(thmax);
@@ -396,10 +411,19 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             double bA = 0.0, bD = 0.0, bAs = 0.0;
             int bq = 0x7fffffff;
 #pragma unroll
-            for (int c = 0; c < C; ++c) {
-                if (!(elm & (1ull << c))) continue;
-                const double a = sg * alpha[64 * c + lane];
-                if (d[c] / a <= thmax && fabs(a) > bA) { bA = fabs(a); bq = 64 * c + lane; bD = d[c]; bAs = a; }
+            for (int c0 = 0; c0 < C; c0 += HB) {
+                if (HB > 1 && !((elm >> c0) & ((1ull << HB) - 1))) continue;
+                double av[HB];
+#pragma unroll
+                for (int u = 0; u < HB; ++u) av[u] = (HB == 1 || c0 + u < C) ? alpha[64 * (c0 + u) + lane] : 0.0;
+#pragma unroll
+                for (int u = 0; u < HB; ++u) {
+                    const int c = c0 + u;
+                    if (c >= C) break;
+                    if (!(elm & (1ull << c))) continue;
+                    const double a = sg * av[u];
+                    if (d[c] / a <= thmax && fabs(a) > bA) { bA = fabs(a); bq = 64 * c + lane; bD = d[c]; bAs = a; }
+                }
             }
             const ArgBest eq = warg_max(bA, bq, bD, bAs);
             const int q = eq.idx;
@@ -413,8 +437,18 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             const double thetaD = eq.p0 / eq.p1;
             // d_j -= thetaD * alpha~_j for every nonbasic column with alpha_j != 0
 #pragma unroll
-            for (int c = 0; c < C; ++c)
-                if (nzm & (1ull << c)) d[c] = fma(-thetaD, sg * alpha[64 * c + lane], d[c]);
+            for (int c0 = 0; c0 < C; c0 += HB) {
+                if (HB > 1 && !((nzm >> c0) & ((1ull << HB) - 1))) continue;
+                double av[HB];
+#pragma unroll
+                for (int u = 0; u < HB; ++u) av[u] = (HB == 1 || c0 + u < C) ? alpha[64 * (c0 + u) + lane] : 0.0;
+#pragma unroll
+                for (int u = 0; u < HB; ++u) {
+                    const int c = c0 + u;
+                    if (c >= C) break;
+                    if (nzm & (1ull << c)) d[c] = fma(-thetaD, sg * av[u], d[c]);
+                }
+            }
             h_wave_sync();
             zero_alpha();   // back to all-zero ut / rho
             h_wave_sync();

@@ -13,7 +13,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-PHASES = ["init", "leaving_row", "btran_etas", "rho_pass", "ratio_pass1", "ratio_pass2", "dual_update_pass3",
+PHASES = ["init_xB", "leaving_row", "btran_etas", "rho_scatter", "pricing", "harris_ratio", "dual_update",
           "ftran", "updates", "final_recovery"]
 
 
