@@ -161,3 +161,53 @@ def test_lp_queue_groups(groups, monkeypatch):
     obj, _, _, st = ctx.solve_values(x, vals)
     assert (st == st0).all()
     np.testing.assert_array_equal(obj, base)
+
+
+def test_pool_selection_picks_least_infeasible():
+    """Flat warm-start selection (pool_select_kernel over the device-built selection stream,
+    pool_selstream_kernel): every scenario's pick minimises the total primal infeasibility
+    sum_i viol(x_B,i) of x_B = B_p^{-1} b_w over the pool, restated here in fp64 from the pool
+    heads (the kernels work in fp32 and drop rows that stay feasible on the training box, which
+    holds every test scenario of storm's DISCRETE distribution), up to fp32 rounding."""
+    from sqlp_amd import twosd
+    ctx, x = _ctx("storm")
+    inst = I.load("storm")
+    sp = inst["osp2"]
+    tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(tr, I.sample("storm", 2048, seed=11))
+    P = ctx.pool_build(tr, x, 0, 2048, 16)
+    assert P > 1
+    N = 256
+    vals = I.sample("storm", N, seed=9)
+    _, _, _, st = ctx.solve_values(x, vals)
+    assert (st == 0).all()
+    picks = ctx.last_pool_picks(N)
+    b = I.rhs_of("storm", x, vals)                    # N x m
+    m, n = sp.W.shape
+    tol = 1e-9
+    keys = np.zeros((N, P))
+    for p in range(P):
+        head = ctx.pool_get(p)
+        B = np.zeros((m, m))
+        for i, j in enumerate(head):
+            if j < n:
+                B[:, i] = sp.W[:, j]
+            else:
+                B[j - n, i] = 1.0
+        xb = np.linalg.solve(B, b.T).T                # N x m
+        for i, j in enumerate(head):
+            sense = None if j < n else sp.senses[j - n]
+            v = xb[:, i]
+            if sense == 'G':
+                keys[:, p] += np.where(v > tol, v, 0.0)
+            elif sense == 'E':
+                keys[:, p] += np.where(np.abs(v) > tol, np.abs(v), 0.0)
+            else:                                     # y_j >= 0 or slack of an L row >= 0
+                keys[:, p] += np.where(v < -tol, -v, 0.0)
+    best = keys.min(axis=1)
+    got = keys[np.arange(N), picks]
+    # fp32 evaluation: x_B entries carry ~1e-7 relative error of the rhs magnitude
+    slack = 1e-4 * best + 1e-5 * (1.0 + np.abs(b).max(axis=1))
+    assert (got <= best + slack).all(), np.max(got - best - slack)
+    assert np.mean(got == best) > 0.9
+    assert len(np.unique(picks)) > 1
