@@ -90,12 +90,12 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-dedup", action="store_true")
-    ap.add_argument("--pool", type=int, default=16384, help="warm-start basis pool size (1 = primary basis only)")
-    ap.add_argument("--pool-train", type=int, default=65536, help="training scenarios of the pool build")
+    ap.add_argument("--pool", type=int, default=32768, help="warm-start basis pool size (1 = primary basis only)")
+    ap.add_argument("--pool-train", type=int, default=131072, help="training scenarios of the pool build")
     ap.add_argument("--pool-level1", type=int, default=128,
                     help="two-level warm-start selection: level 1 over the first L pool bases (0: flat)")
     ap.add_argument("--pool-cands", type=int, default=128, help="level-2 candidate bases per level-1 basis")
-    ap.add_argument("--cand-train", type=int, default=131072, help="training scenarios of the candidate lists")
+    ap.add_argument("--cand-train", type=int, default=262144, help="training scenarios of the candidate lists")
     ap.add_argument("--sampler", choices=["device", "host"], default="device",
                     help="scenario draws: on-device Philox4x32-10 sampler (twosd_add_sampled_scenarios) or numpy PCG64")
     ap.add_argument("--epigraphs", type=int, default=1,
