@@ -90,8 +90,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-dedup", action="store_true")
-    ap.add_argument("--pool", type=int, default=32768, help="warm-start basis pool size (1 = primary basis only)")
-    ap.add_argument("--pool-train", type=int, default=131072, help="training scenarios of the pool build")
+    ap.add_argument("--pool", type=int, default=0,
+                    help="warm-start basis pool size (1 = primary basis only; 0 = by the per-rank shard: "
+                         "32768 from 500k scenarios per GPU, else 16384)")
+    ap.add_argument("--pool-train", type=int, default=0, help="training scenarios of the pool build (0 = 4 x pool)")
     ap.add_argument("--pool-level1", type=int, default=128,
                     help="two-level warm-start selection: level 1 over the first L pool bases (0: flat)")
     ap.add_argument("--pool-cands", type=int, default=128, help="level-2 candidate bases per level-1 basis")
@@ -147,6 +149,13 @@ def main():
 
     # warm-start basis pool (setup, untimed like compute_basis): optimal bases of independent
     # training scenarios of the same distribution (seed + 2, identical on every rank)
+    # pool size by the per-rank shard (profiles/r01/configs/pool_sweep7.jsonl): a larger pool
+    # saves pivots but its per-x preparation (x_B, selection stream) is a fixed cost per step
+    # and its B^-1 data competes for L2, so small shards (the N > 1 steps) prefer 16384
+    if args.pool <= 0:
+        args.pool = 32768 if args.scenarios // max(1, args.epigraphs) // world >= 500_000 else 16384
+    if args.pool_train <= 0:
+        args.pool_train = 4 * args.pool
     t_pool = time.perf_counter()
     if args.pool > 1:
         tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
