@@ -442,6 +442,32 @@ static void launch_argmax_t(const CutParams &P, int nblocks, hipStream_t s) {
                        s, P);
 }
 
+// resident blocks per CU of one instantiation (registers and LDS): the persistent grid is
+// sized to exactly what is resident, so no block starts after the first ones drain (a grid
+// of 3 blocks per CU at 2 resident ran its last third with half of every CU idle)
+template <int KB>
+static int argmax_occupancy_t(size_t dyn_lds) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cut_argmax_kernel<KB>, 256, dyn_lds) != hipSuccess) nb = 0;
+    return nb;
+}
+
+static int argmax_occupancy(int KB, size_t dyn_lds) {
+    switch (KB) {
+        case 1: return argmax_occupancy_t<1>(dyn_lds);
+        case 2: return argmax_occupancy_t<2>(dyn_lds);
+        case 4: return argmax_occupancy_t<4>(dyn_lds);
+        case 6: return argmax_occupancy_t<6>(dyn_lds);
+        case 8: return argmax_occupancy_t<8>(dyn_lds);
+        case 12: return argmax_occupancy_t<12>(dyn_lds);
+        case 16: return argmax_occupancy_t<16>(dyn_lds);
+        case 24: return argmax_occupancy_t<24>(dyn_lds);
+        case 30: return argmax_occupancy_t<30>(dyn_lds);
+        case 32: return argmax_occupancy_t<32>(dyn_lds);
+    }
+    return 0;
+}
+
 static void launch_argmax(int KB, const CutParams &P, int nblocks, hipStream_t s) {
     switch (KB) {
         case 1: launch_argmax_t<1>(P, nblocks, s); break;
@@ -523,7 +549,13 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     HIPCHK(hipMemcpyAsync(w->coef, coef.data(), sizeof(double) * k4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(w->bvec, bvec.data(), sizeof(double) * m, hipMemcpyHostToDevice, c->stream));
     const int ntiles = (N + kCutTile - 1) / kCutTile;
-    const int nblocks = std::max(1, std::min(ntiles, 3 * c->num_cus));
+    // blocks per CU: resident occupancy of this instantiation (TWOSD_CUT_BPC overrides; the
+    // |V| <= kHistLds case adds the LDS histogram, at most 2 KB)
+    static const int bpc_env = getenv("TWOSD_CUT_BPC") ? atoi(getenv("TWOSD_CUT_BPC")) : 0;
+    int bpc = bpc_env;
+    if (bpc <= 0) bpc = argmax_occupancy(KB, sizeof(unsigned long long) * kHistLds);
+    if (bpc <= 0) bpc = 2;
+    const int nblocks = std::max(1, std::min(ntiles, bpc * c->num_cus));
     const int fix_blocks = std::max(1, std::min((N + 3) / 4, c->num_cus));
     const size_t slots = (size_t)nblocks * 4 + (size_t)fix_blocks * 4;
     if (slots * (k + 1) > w->part_cap) {
