@@ -96,7 +96,7 @@ def main():
     ap.add_argument("--pool-train", type=int, default=0, help="training scenarios of the pool build (0 = 4 x pool)")
     ap.add_argument("--pool-level1", type=int, default=128,
                     help="two-level warm-start selection: level 1 over the first L pool bases (0: flat)")
-    ap.add_argument("--pool-cands", type=int, default=128, help="level-2 candidate bases per level-1 basis")
+    ap.add_argument("--pool-cands", type=int, default=160, help="level-2 candidate bases per level-1 basis")
     ap.add_argument("--cand-train", type=int, default=262144, help="training scenarios of the candidate lists")
     ap.add_argument("--sampler", choices=["device", "host"], default="device",
                     help="scenario draws: on-device Philox4x32-10 sampler (twosd_add_sampled_scenarios) or numpy PCG64")
