@@ -172,6 +172,11 @@ int twosd_dvs_get(twosd_ctx *ctx, int first, int count, double *out /* count*m2 
 int twosd_dvs_clear(twosd_ctx *ctx);
 /* Truncate the set to its first `size` vertices (rollback of a speculative push). */
 int twosd_dvs_truncate(twosd_ctx *ctx, int size);
+/* Order-dependent 64-bit digest of the set (size and the per-vertex dedup fingerprints in
+ * insertion order).  No reference counterpart: ranks compare it so that a cut all-reduce
+ * over vertex indices only runs on identical ordered sets (the reference is single-process,
+ * cell.jl:25 shares one set). */
+int twosd_dvs_fingerprint(twosd_ctx *ctx, uint64_t *digest);
 
 /*
  * sd_iteration! hot segment for one epigraph (algorithm.jl:45-55): solve scenarios

@@ -92,3 +92,28 @@ def solve_ev(sp1, sp2, r2):
                   method="highs")
     assert res.status == 0, res.message
     return float(res.fun), res.x[:n1]
+
+
+def extensive_form(sp1, sp2, scenario_rhs, probs=None):
+    """all_in_one (src/crash.jl:18-72) via HiGHS: min c'x + sum_s p_s q'y_s, stage-1 rows,
+    per scenario T x + W y_s (senses) r_s.  Returns the optimal objective."""
+    S = len(scenario_rhs)
+    probs = [1.0 / S] * S if probs is None else list(probs)
+    n1, n2 = sp1.W.shape[1], sp2.W.shape[1]
+    m1, m2 = sp1.W.shape[0], sp2.W.shape[0]
+    A = np.zeros((m1 + S * m2, n1 + S * n2))
+    A[:m1, :n1] = sp1.W
+    for s in range(S):
+        A[m1 + s * m2:m1 + (s + 1) * m2, :n1] = sp2.T
+        A[m1 + s * m2:m1 + (s + 1) * m2, n1 + s * n2:n1 + (s + 1) * n2] = sp2.W
+    b = np.concatenate([sp1.r] + [np.asarray(r, dtype=np.float64) for r in scenario_rhs])
+    senses = list(sp1.senses) + list(sp2.senses) * S
+    G, L, E, A_ub, b_ub, A_eq, b_eq = _split(senses, A, b)
+    lb = np.concatenate([sp1.cur_lb] + [sp2.cur_lb] * S)
+    ub = np.concatenate([sp1.cur_ub] + [sp2.cur_ub] * S)
+    bounds = list(zip([None if np.isinf(l) else l for l in lb],
+                      [None if np.isinf(u) else u for u in ub]))
+    c = np.concatenate([sp1.q] + [p * sp2.q for p in probs])
+    res = linprog(c, A_ub=A_ub, b_ub=b_ub, A_eq=A_eq, b_eq=b_eq, bounds=bounds, method="highs")
+    assert res.status == 0, res.message
+    return float(res.fun)

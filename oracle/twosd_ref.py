@@ -12,6 +12,7 @@ Pure-numpy restatement of the reference's Julia, in the reference's loop order:
   * ``argmax_procedure``    <- subprob.jl:141-169
   * ``build_sasa_cut``      <- epigraph.jl:125-146
   * ``add_cut_discount`` / ``evaluate_epigraph`` <- epigraph.jl:101-117, 177-203
+  * ``evaluate_multi_epigraph`` / ``check_improvement`` <- epigraph.jl:221-228, improvement.jl:19-49
 """
 from __future__ import annotations
 
@@ -194,3 +195,23 @@ def evaluate_epigraph(cuts, incumbent_cut, x, total_scenario_weight, lower_bound
         if v > best:
             best = v
     return best
+
+
+INCUMBENT_SELECTION_Q = 0.2        # improvement.jl:1
+
+
+def evaluate_multi_epigraph(infos, x):
+    """epigraph.jl:221-228 over (objective_weight, cuts, incumbent_cut, total_weight,
+    lower_bound) tuples; cuts = [(alpha, beta, weight_mark)]."""
+    return sum(w * evaluate_epigraph(cuts, inc, x, tw, lb) for w, cuts, inc, tw, lb in infos)
+
+
+def check_improvement(f_last, f_current, x_candidate, x_incumbent, f_cand, f_inc):
+    """improvement.jl:19-49 (MIN_SENSE): returns (candidate_estimation, incumbent_estimation,
+    required_improvement, is_improved)."""
+    ce = evaluate_multi_epigraph(f_current, x_candidate) + f_cand
+    ie = evaluate_multi_epigraph(f_current, x_incumbent) + f_inc
+    lce = evaluate_multi_epigraph(f_last, x_candidate) + f_cand
+    lie = evaluate_multi_epigraph(f_last, x_incumbent) + f_inc
+    req_impr = INCUMBENT_SELECTION_Q * (lce - lie)
+    return ce, ie, req_impr, ce < ie + req_impr

@@ -55,6 +55,7 @@ SIGNATURES = [
     ("twosd_dvs_get", I, [P, I, I, P]),
     ("twosd_dvs_clear", I, [P]),
     ("twosd_dvs_truncate", I, [P, I]),
+    ("twosd_dvs_fingerprint", I, [P, P]),
     ("twosd_solve_push", I, [P, I, P, I, I, P, P, P]),
     ("twosd_build_cut", I, [P, I, P, D, P, P, P, P, P]),
     ("twosd_cut_partial_len", I, [P, P, P]),

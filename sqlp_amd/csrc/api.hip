@@ -133,8 +133,8 @@ static int upload(T **d, const std::vector<T> &h) {
 static void free_template(twosd_ctx *c) {
     dfree(c->d_colptr); dfree(c->d_rowidx); dfree(c->d_val); dfree(c->d_q); dfree(c->d_btype);
     dfree(c->d_fixedmask); dfree(c->d_ubmask);
-    dfree(c->d_hb0); dfree(c->d_basic0); dfree(c->d_B0inv); dfree(c->d_B0invT); dfree(c->d_pi0);
-    dfree(c->d_xbase); dfree(c->d_B0K); dfree(c->d_eta); dfree(c->d_queue); dfree(c->d_lpstats);
+    dfree(c->d_hb0); dfree(c->d_basic0);
+    dfree(c->d_xbase); dfree(c->d_queue); dfree(c->d_lpstats);
     dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_ops);
     dfree(c->d_dvtmp);
     dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); dfree(c->d_head_out); dfree(c->d_pool_pick); dfree(c->d_order); dfree(c->d_sort_tmp);
@@ -149,7 +149,7 @@ static void free_template(twosd_ctx *c) {
     c->earena_slots = 0; c->earena_cap = 0;
     for (auto &e : c->epis) { dfree(e.d_dv); dfree(e.d_w); }
     c->epis.clear();
-    c->out_cap = 0; c->eta_slots = 0; c->dvtmp_cap = 0;
+    c->out_cap = 0; c->dvtmp_cap = 0;
     dvs_free(c);
     cut_free(c);
     c->has_template = c->has_basis = false;
@@ -213,8 +213,7 @@ extern "C" int twosd_set_template(twosd_ctx *c, int m2, int n1, int n2, const in
     if (C > kMaxColsPerLane) return fail(TWOSD_E_UNSUPPORTED, "n2 + m2 = %d exceeds %d columns", n2 + m2, 64 * kMaxColsPerLane);
     c->R = R; c->MP = 64 * R; c->C = C;
     c->CH = hyper_cols_per_lane(n2 + m2);
-    const char *kern = getenv("TWOSD_LP_KERNEL");
-    c->use_hyper = c->CH > 0 && !(kern && std::string(kern) == "dense");
+    if (c->CH <= 0) return fail(TWOSD_E_UNSUPPORTED, "n2 + m2 = %d exceeds the LP kernel's column slots", n2 + m2);
     // device template
     int rc;
     if ((rc = dalloc(&c->d_colptr, n2 + 1)) || (rc = dalloc(&c->d_rowidx, nnzW)) || (rc = dalloc(&c->d_val, nnzW)) ||
@@ -419,25 +418,10 @@ static int upload_pool(twosd_ctx *c) {
 }
 
 static int install_basis(twosd_ctx *c, const std::vector<int> &head) {
-    const int m = c->L.m, MP = c->MP;
     PoolBasis pb;
     int rc = make_pool_basis(c, head, pb);
     if (rc) return rc;
     c->head0 = head;
-    c->B0inv = pb.Binv;
-    // dense-kernel form of the primary basis
-    std::vector<double> Bp((size_t)m * MP, 0.0), BTp((size_t)m * MP, 0.0), pip(MP, 0.0);
-    for (int i = 0; i < m; ++i)
-        for (int j = 0; j < m; ++j) {
-            Bp[(size_t)i * MP + j] = pb.Binv[(size_t)i * m + j];
-            BTp[(size_t)j * MP + i] = pb.Binv[(size_t)i * m + j];
-        }
-    for (int i = 0; i < m; ++i) pip[i] = pb.pi0[i];
-    if ((rc = dalloc(&c->d_B0inv, (size_t)m * MP)) || (rc = dalloc(&c->d_B0invT, (size_t)m * MP)) || (rc = dalloc(&c->d_pi0, MP)))
-        return rc;
-    HIPCHK(hipMemcpy(c->d_B0inv, Bp.data(), sizeof(double) * m * MP, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->d_B0invT, BTp.data(), sizeof(double) * m * MP, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->d_pi0, pip.data(), sizeof(double) * MP, hipMemcpyHostToDevice));
     c->pool.clear();
     c->sel_lo.clear();
     c->sel_hi.clear();
@@ -536,7 +520,6 @@ extern "C" int twosd_pool_build(twosd_ctx *c, int epi, const double *x, int firs
     const EpiDevice &E = c->epis[epi];
     if (first < 0 || count < 0 || first + count > E.count || max_pool < 1 || (c->n1 > 0 && !x))
         return fail(TWOSD_E_ARG, "pool_build: bad arguments");
-    if (!c->use_hyper) return fail(TWOSD_E_UNSUPPORTED, "pool_build: basis pool needs the hypersparse LP kernel");
     if (pool_select_lds_bytes(c->k) > 160 * 1024) return fail(TWOSD_E_UNSUPPORTED, "pool_build: k = %d random elements too many for pool selection", c->k);
     HIPCHK(hipSetDevice(c->device));
     const int m = c->L.m;
@@ -1095,7 +1078,7 @@ static int upload_cap(T **d, size_t *cap, const T *h, size_t n) {
 }
 
 // per-x shared data: b = r - T x; per pool basis xbase_p = B_p^{-1} b (sparse rows);
-// coef_e(x); dense B0K[e] = coef_e B0^{-1}[:, row_e] for the dense kernel; with a pool, the
+// coef_e(x); with a pool, the
 // selection stream (active rows that can turn infeasible on the training box of the deltas).
 // Every pool basis is independent, so the per-basis work runs on host threads.
 int twosd::prepare_x(twosd_ctx *c, const double *x) {
@@ -1151,27 +1134,6 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
             for (int p = 0; p < P; ++p) c->sel_nnz += end[p] - beg[p];
             c->sel_rows = 0;
         }
-    } else {
-        // dense kernel: x_B of the primary basis and dense B0K on the host
-        std::vector<double> xb((size_t)P * MP, 0.0);
-        for (int p = 0; p < P; ++p) {
-            const PoolBasis &B = c->pool[p];
-            for (int i = 0; i < m; ++i) {
-                double s = 0.0;
-                for (int q = B.rptr[i]; q < B.rptr[i + 1]; ++q) s += B.rval[q] * b[B.rcol[q]];
-                xb[(size_t)p * MP + i] = s;
-            }
-        }
-        HIPCHK(hipMemcpy(c->d_xbase, xb.data(), sizeof(double) * xb.size(), hipMemcpyHostToDevice));
-        if ((rc = upload_cap(&c->d_kcoef, &c->kcoef_cap, coef.data(), coef.size()))) return rc;
-    }
-    if (!c->use_hyper) {
-        std::vector<double> bk((size_t)std::max(k, 1) * MP, 0.0);
-        for (int e = 0; e < k; ++e) {
-            const int rr = c->pos_row[e];
-            for (int i = 0; i < m; ++i) bk[(size_t)e * MP + i] = coef[e] * c->B0inv[(size_t)i * m + rr];
-        }
-        if ((rc = upload_cap(&c->d_B0K, &c->b0k_cap, bk.data(), bk.size()))) return rc;
     }
     c->prep_x.assign(x, x + n1);
     c->prep_valid = true;
@@ -1250,7 +1212,7 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
         c->y_cap = c->out_cap;
     }
     if (!c->d_queue && (rc = dalloc(&c->d_queue, (size_t)kMaxQueueGroups * kQueueStride))) return rc;
-    if (c->use_hyper) {
+    {
         // eta capacity (pivots per scenario): 256 keeps two 4-wave blocks per CU within the LDS
         const int kmax = c->kmax_override > 0 ? c->kmax_override : std::min(256, std::max(64, 2 * m + 32));
         const int ecap = std::max(4096, 32 * MP);
@@ -1321,37 +1283,6 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
         c->last_ops_width = 1;
         return TWOSD_OK;
     }
-    c->last_ops_width = MP;
-    const int kmax = c->kmax_override > 0 ? c->kmax_override : std::min(1024, std::max(64, 2 * m + 32));
-    const int bpc = lp_max_blocks_per_cu(R, kmax);
-    const int nblocks = std::max(1, std::min((N + kWavesPerBlock - 1) / kWavesPerBlock, bpc * c->num_cus));
-    const size_t slots = (size_t)nblocks * kWavesPerBlock;
-    if (slots > c->eta_slots || kmax != c->eta_kmax) {
-        if ((rc = dalloc(&c->d_eta, slots * kmax * MP))) return rc;
-        c->eta_slots = slots;
-        c->eta_kmax = kmax;
-    }
-    if (!c->d_queue && (rc = dalloc(&c->d_queue, (size_t)kMaxQueueGroups * kQueueStride))) return rc;
-    HIPCHK(hipMemsetAsync(c->d_queue, 0, sizeof(int) * 4, c->stream));
-    LpParams P{};
-    P.m = m; P.n = n; P.MP = MP; P.k = c->k; P.N = N; P.kmax = kmax; P.C = c->C;
-    P.colptr = c->d_colptr; P.rowidx = c->d_rowidx; P.val = c->d_val; P.q = c->d_q;
-    P.hb0 = c->d_hb0; P.basic0 = c->d_basic0; P.fixedmask = c->d_fixedmask; P.ubmask = c->d_ubmask; P.btype = c->d_btype;
-    P.B0inv = c->d_B0inv; P.B0invT = c->d_B0invT; P.B0K = c->d_B0K; P.pi0 = c->d_pi0; P.xbase = c->d_xbase;
-    P.dv = d_dv; P.eta = c->d_eta; P.queue = c->d_queue;
-    P.obj = c->d_obj; P.pi = want_pi ? c->d_pi : nullptr; P.y = want_y ? c->d_y : nullptr;
-    P.status = c->d_status; P.iters = c->d_iters; P.ops = c->d_ops;
-    HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    HIPCHK(launch_lp(R, P, nblocks, lp_lds_bytes(R, kmax), c->stream));
-    HIPCHK(hipEventRecord(c->ev[1], c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    float ms = 0;
-    hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
-    c->t_us[0] = 1e3 * ms;
-    c->t_us[4] = 0.0;
-    c->last_lp_N = N;
-    c->last_lp_blocks = nblocks;
-    return TWOSD_OK;
 }
 
 // batch statistics on the device (integer sums: exact, order independent): [0] pivots,

@@ -391,6 +391,23 @@ extern "C" int twosd_dvs_get(twosd_ctx *c, int first, int count, double *out) {
 
 extern "C" int twosd_dvs_clear(twosd_ctx *c) { return twosd_dvs_truncate(c, 0); }
 
+// Order-dependent digest of the set: size + sum_i fp_i (2i + 1) mod 2^64 over the per-vertex
+// 64-bit fingerprints of the rounded components (the dedup keys).  Ranks compare it before an
+// all-reduce over vertex indices (sqlp_amd/dist.py).
+extern "C" int twosd_dvs_fingerprint(twosd_ctx *c, uint64_t *out) {
+    if (!c || !out) return fail(TWOSD_E_ARG, "dvs_fingerprint: NULL");
+    const int n = c->dvs.size;
+    uint64_t acc = (uint64_t)n * 0x9E3779B97F4A7C15ull;
+    if (n > 0) {
+        HIPCHK(hipSetDevice(c->device));
+        std::vector<uint64_t> fp(n);
+        HIPCHK(hipMemcpy(fp.data(), c->dvs.fp, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
+        for (int i = 0; i < n; ++i) acc += fp[i] * (2 * (uint64_t)i + 1);
+    }
+    *out = acc;
+    return TWOSD_OK;
+}
+
 extern "C" int twosd_dvs_truncate(twosd_ctx *c, int size) {
     if (!c) return fail(TWOSD_E_ARG, "dvs_truncate: NULL");
     if (size < 0 || size > c->dvs.size) return fail(TWOSD_E_ARG, "dvs_truncate: size %d outside [0, %d]", size, c->dvs.size);

@@ -1,10 +1,10 @@
 // lp_hyper.hip -- hypersparse batched dual simplex for the stage-2 LPs (gfx950).
 //
-// Same problem, pivot rules and outputs as lp_kernel.hip (solve_problem!,
-// src/smps/smps_routines.jl:50-62), restructured for what the SMPS recourse matrices
-// look like: B0^{-1} of storm is 1.2 % dense (about 6 nonzeros per row/column) and
-// the FTRAN columns B^{-1} a_q about 1 %, so every 64R-wide dense row operation of the
-// dense kernel is ~99 % zeros.  Here:
+// Bounded dual simplex for solve_problem! (src/smps/smps_routines.jl:50-62), one
+// 64-lane wavefront per scenario, built for what the SMPS recourse matrices look like:
+// B0^{-1} of storm is 1.2 % dense (about 6 nonzeros per row/column) and the FTRAN
+// columns B^{-1} a_q about 1 %, so dense 64R-wide row operations would be ~99 % zeros.
+// Here:
 //   * B0^{-1} is stored CSC (column c -> (row i, B0^{-1}[i][c])), shared by all waves;
 //   * the eta file of a wave is a sparse arena (row index, value) in HBM (L1/L2 hits in
 //     practice), its pivot rows and offsets in the wave's LDS slice;
@@ -14,8 +14,9 @@
 //     C slots, template parameter) and are updated in place (no dual vector, no pi);
 //   * FTRAN: scatter of the sparse B0^{-1} columns of a_q, then the sparse etas;
 //   * x_B and dual Devex weights stay in registers (row i: lane i%64, slot i/64).
-// The leaving-row choice, Harris two-pass ratio test and tie breaks are those of
-// lp_kernel.hip, so both kernels follow the same pivot path up to rounding.
+// Pivot rules (dual Devex leaving row, Harris two-pass ratio test, lowest index on ties)
+// are those of the C oracle (oracle/cpu_lp.c), so both follow the same pivot path up to
+// rounding.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include "twosd_internal.h"
@@ -234,7 +235,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         STAMP(0)
 
         for (;;) {
-            // ---- 1. leaving row (same rule as lp_kernel.hip)
+            // ---- 1. leaving row (dual Devex: max infeas^2 / w, lowest row on ties)
             double best = 0.0, bdel = 0.0;
             int br = 0x7fffffff;
 #pragma unroll
@@ -260,7 +261,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             // so one memory round trip serves four sequential steps
             for (int tg = K - 1; tg >= 0; tg -= EG) {
                 int gi[EG], gn[EG], go[EG];
-                double gv[4];
+                double gv[EG];
 #pragma unroll
                 for (int g = 0; g < EG; ++g) {
                     const int tt = tg - g;
@@ -289,7 +290,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             // r, etap[K-1], ..., etap[0], so the accumulation order is deterministic.
             for (int tg = K; tg >= 0; tg -= EG) {
                 int gi[EG], gn[EG], gp[EG], go[EG];
-                double gv[4];
+                double gv[EG];
 #pragma unroll
                 for (int g = 0; g < EG; ++g) {
                     const int tt = tg - g;
@@ -476,7 +477,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             }
             for (int tg = 0; tg < K; tg += EG) {
                 int gi[EG], gn[EG], go[EG];
-                double gv[4];
+                double gv[EG];
 #pragma unroll
                 for (int g = 0; g < EG; ++g) {
                     const int tt = tg + g;

@@ -16,7 +16,7 @@ struct EpiDevice {
     std::vector<double> w_host;
 };
 
-// one warm-start basis of the pool (pool[0] is the primary basis head0 / B0inv)
+// one warm-start basis of the pool (pool[0] is the primary basis head0)
 struct PoolBasis {
     std::vector<int> head;        // m basic columns (0-based over [y; slacks])
     std::vector<double> Binv;     // m x m row-major
@@ -48,10 +48,9 @@ struct twosd_ctx {
     uint64_t *d_fixedmask = nullptr, *d_ubmask = nullptr;
     // basis
     std::vector<int> head0;
-    std::vector<double> B0inv;    // m x m host copy
     int *d_hb0 = nullptr;
     uint64_t *d_basic0 = nullptr;
-    double *d_B0inv = nullptr, *d_B0invT = nullptr, *d_pi0 = nullptr, *d_xbase = nullptr, *d_B0K = nullptr;
+    double *d_xbase = nullptr;
     std::vector<twosd::PoolBasis> pool;   // warm-start basis pool, pool[0] = head0
     // pool selection data (per x, prepare_x): constant-row infeasibility, active rows, entries
     float *d_sel_cinf = nullptr;
@@ -85,10 +84,9 @@ struct twosd_ctx {
     double *d_kcoef = nullptr;    // k: coef_e(x) = 1 (RHS element) or -x[col] (T element)
     std::vector<double> prep_x;
     // capacities of the per-x device arrays (prepare_x re-uploads in place, no hipFree/hipMalloc per x)
-    size_t xbase_cap = 0, b0k_cap = 0, kcoef_cap = 0;
+    size_t xbase_cap = 0, kcoef_cap = 0;
     // hypersparse kernel data
     int CH = 0;                   // column slots per lane of the hypersparse kernel
-    bool use_hyper = true;
     int *d_kslot = nullptr, *d_kix = nullptr;
     double *d_kv = nullptr, *d_d0 = nullptr;
     int wr_width = 1;             // W row-ELL width (max row length)
@@ -107,9 +105,6 @@ struct twosd_ctx {
     unsigned long long *d_stamps = nullptr;
     int last_ops_width = 1;
     // LP workspace + outputs
-    double *d_eta = nullptr;
-    size_t eta_slots = 0;
-    int eta_kmax = 0;
     int *d_queue = nullptr;
     unsigned long long *d_lpstats = nullptr;   // lp_stats_kernel output (4 words)
     double *d_obj = nullptr, *d_pi = nullptr, *d_y = nullptr;

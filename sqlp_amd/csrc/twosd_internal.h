@@ -19,36 +19,6 @@ constexpr int kMaxColsPerLane = 64;
 // variable bound types (all nonbasic variables sit at 0)
 enum : int { BT_Y = 0, BT_G = 1, BT_L = 2, BT_E = 3 };
 
-struct LpParams {
-    int m, n, MP;          // rows, structural columns, padded rows (= 64 * R)
-    int k;                 // random elements per scenario
-    int N;                 // scenarios in this launch
-    int kmax;              // eta capacity per wavefront
-    int C;                 // column slots per lane
-    // template
-    const int *colptr, *rowidx; const double *val;   // W CSC (0-based, int32)
-    const double *q;                                 // n
-    const int *hb0;        // MP: head0 * 4 + bound type, -1 for padded rows
-    const uint64_t *basic0;    // 64: per-lane bit c set <=> column 64c+lane basic in B0
-    const uint64_t *fixedmask; // 64: E slacks and padding columns (never enter)
-    const uint64_t *ubmask;    // 64: G slacks (nonbasic at upper bound 0)
-    const int8_t *btype;       // n + m: bound type of every column
-    // shared basis data (L2 / MALL resident)
-    const double *B0inv;   // m rows x MP (row-major, zero-padded)
-    const double *B0invT;  // m rows x MP: row i = column i of B0inv
-    const double *B0K;     // k rows x MP: coef_e * column row_e of B0inv
-    const double *pi0;     // MP
-    const double *xbase;   // MP: B0inv (r - T x)
-    // scenarios
-    const double *dv;      // N x k deltas (value - template)
-    // workspace
-    double *eta;           // nslots x kmax x MP
-    int *queue;            // [0] work counter
-    // outputs
-    double *obj, *pi, *y;  // N, N x m (nullable), N x n (nullable)
-    int *status, *iters;   // N, N
-    long long *ops;        // N (nullable): executed 64R-wide fp64 row operations (FMA rows)
-};
 
 // hypersparse kernel (lp_hyper.hip)
 constexpr int kQueueStride = 32;   // queue heads one 128-B line apart
@@ -125,10 +95,6 @@ int hyper_cols_per_lane(int ncols);
 hipError_t launch_hyper(int R, int C, const HyperParams &p, int nblocks, size_t lds, hipStream_t s);
 int hyper_max_blocks_per_cu(int R, int C, int ncol, int kmax, int k);
 
-int lp_rows_per_lane(int m);   // supported R for m, or -1
-hipError_t launch_lp(int R, const LpParams &p, int nblocks, size_t lds_bytes, hipStream_t s);
-size_t lp_lds_bytes(int R, int kmax);
-int lp_max_blocks_per_cu(int R, int kmax);
 
 // ---- on-device scenario sampler (sampler.hip)
 struct SampleParams {

@@ -8,9 +8,10 @@ hot path shards naturally by scenario:
   * build_sasa_cut needs ONE exchange: the vertex-weight histogram (uint64 fixed point,
     summed exactly, so every rank count gives bit-identical h) and k+1 fp64 sums,
     all-reduced over RCCL (backend "nccl") -- a few KB per cut.
-  * vertex-set growth: every rank dedups its new duals locally, then the locally-new rows
-    are all-gathered and pushed in (rank, local index) order, so every rank holds the same
-    ordered set (the order decides argmax ties).
+  * vertex-set growth (push_sharded): every rank dedups its new duals locally, then the
+    locally-new rows are all-gathered and pushed in (rank, local index) order, so every rank
+    holds the same ordered set (the order decides argmax ties); check_vertex_sets_agree
+    compares size + fingerprint across ranks before every cut all-reduce.
 The collectives are plain torch.distributed calls on tensors, so the same code runs on
 CPU tensors with gloo (tests) and on HIP tensors with RCCL (bench).
 """
@@ -85,17 +86,92 @@ def evaluate_sharded(ctx, first_stage_cost, x, N, seed):
     return float(np.dot(first_stage_cost, x)) + sum_in_rank_order(s2)
 
 
-def build_cut_sharded(ctx, epi, x, total_weight, tie_rel, device):
-    """build_sasa_cut over the scenarios of every rank: local partial on this GPU,
-    all-reduce over RCCL, identical finalize on every rank.  Returns (alpha, beta)."""
-    n_u64, n_f64 = ctx.cut_partial_len()
-    hist = torch.zeros(n_u64, dtype=torch.int64, device=device)
-    sums = torch.zeros(n_f64, dtype=torch.float64, device=device)
-    torch.cuda.synchronize(device)
-    ctx.cut_partial(epi, x, tie_rel, total_weight, hist.data_ptr(), sums.data_ptr())
-    allreduce_cut_partials(hist, sums)
-    torch.cuda.synchronize(device)
-    return ctx.cut_finalize(x, hist.data_ptr(), sums.data_ptr())
+class CutExchange:
+    """Device buffers of the per-cut exchange of one context, allocated once and regrown only
+    when the vertex set grows (no per-cut allocation)."""
+
+    def __init__(self, ctx, device):
+        self.ctx = ctx
+        self.device = device
+        self.hist = None
+        self.sums = None
+
+    def _buffers(self):
+        n_u64, n_f64 = self.ctx.cut_partial_len()
+        if self.hist is None or self.hist.numel() < n_u64:
+            self.hist = torch.zeros(max(n_u64, 1024), dtype=torch.int64, device=self.device)
+            self._sync()
+        if self.sums is None or self.sums.numel() < n_f64:
+            self.sums = torch.zeros(max(n_f64, 256), dtype=torch.float64, device=self.device)
+            self._sync()     # torch's fill must land before the library's stream touches the buffer
+        return self.hist[:n_u64], self.sums[:n_f64]
+
+    def _sync(self):
+        if self.hist is not None and self.hist.is_cuda:
+            torch.cuda.synchronize(self.device)
+
+    def build_cut(self, epi, x, total_weight, tie_rel, verify=True):
+        """build_sasa_cut over the scenarios of every rank: local partial on this GPU (the
+        library zero-fills and writes the buffers on its stream, synchronously), all-reduce,
+        identical finalize on every rank.  Returns (alpha, beta)."""
+        if verify:
+            check_vertex_sets_agree(self.ctx)
+        hist, sums = self._buffers()
+        self.ctx.cut_partial(epi, x, tie_rel, total_weight, hist.data_ptr(), sums.data_ptr())
+        allreduce_cut_partials(hist, sums)
+        self._sync()         # the collective runs on torch / RCCL streams, finalize on the library's
+        return self.ctx.cut_finalize(x, hist.data_ptr(), sums.data_ptr())
+
+
+def build_cut_sharded(ctx, epi, x, total_weight, tie_rel, device, verify=True):
+    """build_sasa_cut over the scenarios of every rank (one CutExchange per context)."""
+    ex = getattr(ctx, "_cut_exchange", None)
+    if ex is None:
+        ex = ctx._cut_exchange = CutExchange(ctx, device)
+    return ex.build_cut(epi, x, total_weight, tie_rel, verify=verify)
+
+
+def check_vertex_sets_agree(ctx):
+    """Raise unless every rank holds the same ordered vertex set (size + order-dependent
+    fingerprint, twosd_dvs_fingerprint): the histogram all-reduce sums by vertex index, so
+    ranks with different sets would hang (different lengths) or add unrelated vertices."""
+    rank, G = world()
+    if G == 1:
+        return
+    from .twosd import sdDualVertexSet
+    V = sdDualVertexSet(ctx)
+    fp = V.fingerprint()
+    mine = torch.tensor([len(V), fp - (1 << 64) if fp >= (1 << 63) else fp], dtype=torch.int64)
+    if dist.get_backend() == "nccl":
+        mine = mine.cuda()
+    parts = [torch.zeros_like(mine) for _ in range(G)]
+    dist.all_gather(parts, mine)
+    rows = [tuple(int(v) for v in p.cpu().tolist()) for p in parts]
+    if any(r != rows[0] for r in rows):
+        raise RuntimeError(f"vertex sets differ across ranks (size, fingerprint) = {rows}")
+
+
+def push_sharded(V, pis_local: np.ndarray) -> int:
+    """Vertex-set growth across ranks (exchange 2): each rank dedups its own duals against
+    the common set, rolls its set back, and every rank pushes the all-gathered locally-new
+    rows in (rank, index) order -- the set equals a sequential push! of all ranks' duals in
+    rank order on every rank.  Returns the new size."""
+    n0 = len(V)
+    pis_local = np.ascontiguousarray(np.atleast_2d(pis_local), dtype=np.float64)
+    if pis_local.shape[0]:
+        V.push_batch(pis_local)
+    new_rows = V.matrix(n0) if len(V) > n0 else np.zeros((0, V.ctx.m))
+    rank, G = world()
+    if G == 1:
+        return len(V)
+    V.truncate(n0)
+    t = torch.from_numpy(new_rows)
+    if dist.get_backend() == "nccl":
+        t = t.cuda()
+    allrows = allgather_rows_ordered(t).cpu().numpy()
+    if allrows.shape[0]:
+        V.push_batch(allrows)
+    return len(V)
 
 
 def finalize_from_partials(hist: np.ndarray, sums: np.ndarray, V: np.ndarray, r: np.ndarray, T: np.ndarray,

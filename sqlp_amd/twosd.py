@@ -43,8 +43,11 @@ class SDContext:
     (extract_coefficients, subprob.jl:15-69), the random-element layout, the shared
     warm-start basis, and the dual vertex set (cell.dual_vertices, cell.jl:25)."""
 
-    def __init__(self, sp2: spStageProblem, sto=None, positions=None, device: int = 0):
+    def __init__(self, sp2: spStageProblem, sto=None, positions=None, device: int = 0, index_base: int = 0):
+        """index_base = 1 hands the template and positions to the library 1-based, as a Julia
+        caller passes SparseMatrixCSC colptr / rowval (twosd_set_template, index_base)."""
         self.lib = _lib.load()
+        self.index_base = int(index_base)
         h = C.c_void_p()
         check(self.lib.twosd_create(device, C.byref(h)))
         self.h = h
@@ -52,14 +55,16 @@ class SDContext:
         self.m, self.n1, self.n2 = sp2.shape
         Tcp, Trv, Tnz = sp2.T
         Wcp, Wrv, Wnz = sp2.W
-        self._keep = [np.ascontiguousarray(a) for a in (Tcp, Trv, Tnz, Wcp, Wrv, Wnz)]
+        ib = self.index_base
+        self._keep = [np.ascontiguousarray(a + ib if a.dtype.kind == "i" else a)
+                      for a in (Tcp, Trv, Tnz, Wcp, Wrv, Wnz)]
         sense = np.frombuffer("".join(sp2.sense).encode(), dtype=np.int8).copy()
         self._keep += [sense]
         check(self.lib.twosd_set_template(
             self.h, self.m, self.n1, self.n2,
             ptr(self._keep[0]), ptr(self._keep[1]), ptr(self._keep[2]),
             ptr(self._keep[3]), ptr(self._keep[4]), ptr(self._keep[5]),
-            ptr(_f64(sp2.q)), ptr(_f64(sp2.r)), ptr(sense), ptr(_f64(sp2.ylb)), ptr(_f64(sp2.yub)), 0))
+            ptr(_f64(sp2.q)), ptr(_f64(sp2.r)), ptr(sense), ptr(_f64(sp2.ylb)), ptr(_f64(sp2.yub)), ib))
         self.row_lookup = {n: i for i, n in enumerate(sp2.stage_constraints)}
         self.col_lookup = {n: j for j, n in enumerate(sp2.last_stage_vars)}
         if sto is not None and positions is None:
@@ -77,7 +82,10 @@ class SDContext:
                          for p in self.positions], dtype=np.int32)
         self.k = len(self.positions)
         self.rows, self.cols = rows, cols
-        check(self.lib.twosd_set_random_positions(self.h, self.k, ptr(rows), ptr(cols), 0))
+        ib = self.index_base
+        rows_b = np.ascontiguousarray(rows + ib, dtype=np.int32)
+        cols_b = np.ascontiguousarray(np.where(cols < 0, -1, cols + ib), dtype=np.int32)
+        check(self.lib.twosd_set_random_positions(self.h, self.k, ptr(rows_b), ptr(cols_b), ib))
         # template value of every element (for scenario -> values conversion)
         T = self.sp2.dense_T()
         self.template_values = np.array(
@@ -284,6 +292,12 @@ class sdDualVertexSet:
     def truncate(self, size):
         check(self.ctx.lib.twosd_dvs_truncate(self.ctx.h, int(size)))
 
+    def fingerprint(self) -> int:
+        """Order-dependent 64-bit digest of the set (twosd_dvs_fingerprint)."""
+        d = C.c_uint64()
+        check(self.ctx.lib.twosd_dvs_fingerprint(self.ctx.h, C.byref(d)))
+        return d.value
+
 
 def push(dvs: sdDualVertexSet, vec):
     return dvs.push(vec)
@@ -478,14 +492,29 @@ def solve_push(epi: sdEpigraph, x, first, count):
     return obj, st, ns.value
 
 
-def sd_iteration_hot_path(epis, scenario_values, x_candidate, x_incumbent, V: sdDualVertexSet,
-                          update_incumbent_cut=True, tie_rel=DEFAULT_TIE_REL):
-    """The data-parallel part of sd_iteration! (algorithm.jl:45-55 and :79-85):
-    for every epigraph i: add_scenario!(epi_i, w_i, 1.0); solve at x_candidate and at
-    x_incumbent, push! both duals (in the reference's order: epi 1 cand, epi 1 inc,
-    epi 2 cand, ...); then build_sasa_cut at x_candidate (appended to epi.cuts) and, if
-    update_incumbent_cut, at x_incumbent (epi.incumbent_cut).  scenario_values[i] is a
-    (N_i x k) block of new scenarios for epigraph i."""
+@dataclass
+class sdEpigraphInfo:
+    """epigraph.jl:152-171: the cuts, incumbent cut and total weight of an epigraph at one
+    moment (copies), for the incumbent test of the next step."""
+    objective_weight: float
+    cuts: list
+    incumbent_cut: object
+    total_scenario_weight: float
+    lower_bound: float
+
+    @classmethod
+    def of(cls, epi: "sdEpigraph") -> "sdEpigraphInfo":
+        return cls(epi.objective_weight, list(epi.cuts), epi.incumbent_cut, epi.total_scenario_weight,
+                   epi.lower_bound)
+
+
+def sd_iteration_solve(epis, scenario_values, x_candidate, x_incumbent, V: sdDualVertexSet):
+    """algorithm.jl:45-55: for every epigraph i, add_scenario!(epi_i, w_i, 1.0), solve at
+    x_candidate and at x_incumbent and push! both duals.  The duals are pushed in the
+    reference's order (epi 1 cand, epi 1 inc, epi 2 cand, ...; for a block of several
+    scenarios per epigraph: cand/inc per scenario in order).  scenario_values[i] is a
+    (N_i x k) block of new scenarios for epigraph i.  Returns the vertex index of every
+    pushed dual (the order above)."""
     pis = []
     for epi, vals in zip(epis, scenario_values):
         vals = np.atleast_2d(vals)
@@ -497,8 +526,28 @@ def sd_iteration_hot_path(epis, scenario_values, x_candidate, x_incumbent, V: sd
         inter[0::2] = pc
         inter[1::2] = pinc
         pis.append(inter)
-    V.push_batch(np.vstack(pis))
+    return V.push_batch(np.vstack(pis))
+
+
+def sd_iteration_cuts(epis, x_candidate, x_incumbent, V: sdDualVertexSet, update_incumbent_cut=True,
+                      tie_rel=DEFAULT_TIE_REL):
+    """algorithm.jl:79-85: build_sasa_cut at x_candidate appended to epi.cuts and, if
+    update_incumbent_cut, at x_incumbent as epi.incumbent_cut."""
     for epi in epis:
         epi.cuts.append(build_sasa_cut(epi, x_candidate, V, tie_rel))
         if update_incumbent_cut:
             epi.incumbent_cut = build_sasa_cut(epi, x_incumbent, V, tie_rel)
+
+
+def sd_iteration_hot_path(epis, scenario_values, x_candidate, x_incumbent, V: sdDualVertexSet,
+                          update_incumbent_cut=True, tie_rel=DEFAULT_TIE_REL):
+    """The data-parallel part of sd_iteration! (algorithm.jl:45-55 and :79-85) in one call:
+    sd_iteration_solve, the sdEpigraphInfo snapshot the reference takes between the two
+    halves (algorithm.jl:76: after add_scenario!, before any new cut), sd_iteration_cuts.
+    Returns the snapshot (epi_info_last) for check_improvement.  Cut removal by master
+    multipliers (algorithm.jl:57-72) sits between the halves in the reference; callers with
+    a master use the two halves directly (sqlp_amd.master.sd_iteration)."""
+    sd_iteration_solve(epis, scenario_values, x_candidate, x_incumbent, V)
+    info = [sdEpigraphInfo.of(e) for e in epis]
+    sd_iteration_cuts(epis, x_candidate, x_incumbent, V, update_incumbent_cut, tie_rel)
+    return info
