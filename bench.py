@@ -2,19 +2,24 @@
 """bench.py -- TwoSD scenario-subproblem + cut-generation hot path on MI355X.
 
 Metric (BASELINE.json): stage-2 subproblems/sec + cut-gen HBM GB/s on STORM.
-One step = one pass of the hot path over the (sharded) scenario batch at the EV
-first-stage x:
+One step = one pass of the hot path over the (sharded) scenario batch at a first-stage x:
   1. solve_problem! for every scenario of the shard (GPU dual simplex, LP kernel),
-  2. push! of every dual into the dual vertex set (device dedup), then rollback of the
-     set to the fixed |V| pool so every step sees the same set,
+  2. push! of every dual into the dual vertex set (device dedup by dual keys), then rollback
+     of the set to the fixed |V| pool so every step sees the same set (fixed |V|),
   3. build_sasa_cut over the same scenarios with the |V| pool (MFMA argmax + cut),
-     RCCL all-reduce of the cut partials when N > 1.
-value = scenarios processed by all ranks / max-over-ranks step time.
+     RCCL all-reduce of the cut partials when N > 1, plus the SD-sized vertex all-gather
+     (2 new vertices per epigraph per step, as sd_iteration! adds).
+The timed steps cycle over X first-stage points: the EV solution (where the warm-start pool
+and its candidate lists were trained) and X-1 candidate points of an SD run on the same
+instance (master QP + GPU hot path, sqlp_amd/master.py), so the pool is timed at points it
+was not trained at.  Pivots and ms are reported per point.
+value = scenarios processed by all ranks / max-over-ranks time of the K timed steps.
 
 Workload: storm (data/smps/storm, reference spInput), 1,000,000 i.i.d. synthetic scenarios
-from storm.sto (numpy PCG64, per-chunk seeds so any sharding sees the same scenarios),
-x = EV solution (tests/golden/ev_x.json), |V| = 4096 real LP duals.  Strong scaling:
-the 1M scenarios are split over the ranks.
+from storm.sto drawn on the device, |V| = 4096 real LP duals.  Strong scaling: the 1M
+scenarios are split over the ranks.  After the timed region: a parity spot check of 4096
+scenarios per x point against the C oracle (LP objectives, cut alpha/beta) and the CPU
+baseline (C port, primary-basis and pooled warm starts).
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -80,7 +85,7 @@ def importance_values(sto, positions, lo, hi, seed, scale):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--instance", default="storm")
     ap.add_argument("--scenarios", type=int, default=1_000_000)
@@ -90,6 +95,16 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-dedup", action="store_true")
+    ap.add_argument("--x-points", default="0,4,12,30",
+                    help="first-stage points the timed steps cycle over: 0 = the EV solution (pool training "
+                         "point), i > 0 = the candidate of SD iteration i (storm master + GPU hot path)")
+    ap.add_argument("--spot", type=int, default=4096, help="parity spot-check scenarios per x point (0: off)")
+    ap.add_argument("--refresh", type=int, default=1,
+                    help="1: a step at an x other than the pool's rebuilds the pool there (twosd_pool_refresh + "
+                         "candidate lists, inside the timed step); 0: keep the x_EV pool for every x")
+    ap.add_argument("--refresh-train", type=int, default=16384, help="training scenarios of a pool refresh")
+    ap.add_argument("--refresh-pool", type=int, default=4096, help="pool size after a refresh")
+    ap.add_argument("--cpu-pool", type=int, default=128, help="bases of the pooled CPU baseline (0: off)")
     ap.add_argument("--pool", type=int, default=0,
                     help="warm-start basis pool size (1 = primary basis only; 0 = by the per-rank shard: "
                          "32768 from 500k scenarios per GPU, else 16384)")
@@ -134,6 +149,15 @@ def main():
     with open(os.path.join(ROOT, "tests", "golden", "ev_x.json")) as f:
         x = np.array(json.load(f)[name]["x"])
     positions = list(sto.indep.keys())
+    # first-stage points of the timed steps: x_EV and SD candidates (identical on every rank)
+    t_traj = time.perf_counter()
+    x_iters = sorted({int(v) for v in args.x_points.split(",")})
+    xs = sd_points(cor, tim, sp2, sto, positions, x, x_iters, args.seed + 7, device)
+    if world > 1:
+        t = torch.tensor(np.stack(xs), dtype=torch.float64, device=device)
+        torch.distributed.broadcast(t, 0)
+        xs = [row for row in t.cpu().numpy()]
+    t_traj = time.perf_counter() - t_traj
     ctx = twosd.SDContext(sp2, sto, device=device.index)
     ctx.compute_basis(x, smps.mean_values(sto, positions))
 
@@ -209,19 +233,53 @@ def main():
         V.truncate(args.vertices)
     nv = len(V)
 
-    def step(rec=None):
+    X = len(xs)
+    # pool refresh training scenarios (stream seed + 4, identical on every rank)
+    rtr = None
+    if args.refresh:
+        rtr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+        scenarios(rtr, 0, args.refresh_train, args.seed + 4)
+    pool_at = {"x": xs[0].copy()}    # the pool was built at x_EV
+
+    def refresh(xx):
+        """Per-x warm-start pool: rebuilt from the training scenarios' optimal bases at xx
+        (timed as part of the step), two-level selection lists from the same scenarios."""
+        if rtr is None or np.array_equal(pool_at["x"], xx):
+            return 0.0
+        t0 = time.perf_counter()
+        ctx.pool_refresh(rtr, xx, 0, args.refresh_train, args.refresh_pool)
+        if args.pool_level1 > 0 and ctx.pool_size() > args.pool_level1:
+            ctx.pool_build_candidates(rtr, xx, 0, args.refresh_train, args.pool_level1, args.pool_cands)
+        pool_at["x"] = xx.copy()
+        return time.perf_counter() - t0
+
+    heads_at = {}    # first pool bases at each x point (the pooled CPU baseline starts from the same bases)
+
+    def step(xx, rec=None):
+        t_ref = refresh(xx)
+        if rec:
+            per_x[cur["xi"]]["refresh"] += t_ref
+            if cur["xi"] not in heads_at and not args.no_cpu and rank == 0:
+                heads_at[cur["xi"]] = np.stack([ctx.pool_get(p) for p in range(min(args.cpu_pool, ctx.pool_size()))])
         ctx.invalidate_x()     # every pass pays its per-x setup (x_B of the pool, selection data)
         alpha = 0.0
         for epi_e, tw in zip(epis, total_weights):
             if args.no_dedup:
-                twosd.solve_batch(epi_e, x, 0, n_local, want_pi=False)
+                twosd.solve_batch(epi_e, xx, 0, n_local, want_pi=False)
             else:
-                twosd.solve_push(epi_e, x, 0, n_local)
+                twosd.solve_push(epi_e, xx, 0, n_local)
+                if world > 1:
+                    # exchange (2) at the SD volume: two new vertices per epigraph (the candidate
+                    # and incumbent duals of sd_iteration!, algorithm.jl:46-54) all-gathered
+                    # and pushed in (rank, index) order on every rank
+                    new = V.matrix(nv, min(2, len(V) - nv)) if len(V) > nv else np.zeros((0, m))
+                    V.truncate(nv)
+                    sdist.push_sharded(V, new)
                 V.truncate(nv)
             if world == 1:
-                alpha += twosd.build_sasa_cut(epi_e, x, V, args.tie_rel).alpha / E
+                alpha += twosd.build_sasa_cut(epi_e, xx, V, args.tie_rel).alpha / E
             else:
-                alpha += sdist.build_cut_sharded(ctx, epi_e, x, tw, args.tie_rel, device)[0] / E
+                alpha += sdist.build_cut_sharded(ctx, epi_e, xx, tw, args.tie_rel, device)[0] / E
             if rec:
                 rec()      # per-epigraph kernel timings (HIP events of the last calls)
         return alpha
@@ -232,10 +290,13 @@ def main():
             torch.distributed.barrier()
         torch.cuda.synchronize(device)
 
+    m = sp2.shape[0]
     for _ in range(args.warmup):
-        step()
+        step(xs[0])
     barrier()
     acc = {"lp": 0.0, "dd": 0.0, "cut": 0.0, "fin": 0.0, "sel": 0.0, "flops": 0.0, "piv": 0, "pmax": 0}
+    per_x = [{"piv": 0, "n": 0, "lp": 0.0, "wall": 0.0, "steps": 0, "alpha": None, "refresh": 0.0} for _ in xs]
+    cur = {"xi": 0}
 
     def record():
         tm = ctx.timings_us()
@@ -243,9 +304,15 @@ def main():
         acc["flops"] += ctx.lp_flops()
         ps, pm = ctx.lp_stats()
         acc["piv"] += ps; acc["pmax"] = max(acc["pmax"], pm)
+        px = per_x[cur["xi"]]
+        px["piv"] += ps; px["n"] += n_local; px["lp"] += tm[0]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        alpha = step(record)
+    for i in range(args.steps):
+        cur["xi"] = i % X
+        ts = time.perf_counter()
+        alpha = step(xs[i % X], record)
+        px = per_x[i % X]
+        px["wall"] += time.perf_counter() - ts; px["steps"] += 1; px["alpha"] = alpha
     barrier()
     elapsed = time.perf_counter() - t0
     t_lp, t_dd, t_cut, t_fin, t_sel = acc["lp"], acc["dd"], acc["cut"], acc["fin"], acc["sel"]
@@ -259,7 +326,6 @@ def main():
     value = N * K / elapsed
 
     k = len(positions)
-    m = sp2.shape[0]
     passes = K * E                 # LP launches / cut passes in the timed region
     # LP kernel (dominant): counted fp64 FLOPs of the executed pivot path per launch
     lp_us = t_lp / passes
@@ -270,6 +336,16 @@ def main():
     cut_us = t_cut / passes
     cut_gbs = bytes_alg / (cut_us * 1e-6) / 1e9
     t_roof = max(bytes_alg / (PEAK_HBM_GBS * 1e9), flops_alg / (PEAK_FP64_TFS * 1e12))
+    xnorm = float(np.linalg.norm(xs[0]))
+    x_points = [{"x": ("EV (pool training point)" if it == 0 else f"SD candidate, iteration {it}"),
+                 "rel_dist_from_ev": float(np.linalg.norm(xx - xs[0]) / xnorm),
+                 "steps": px["steps"],
+                 "ms_per_step": 1e3 * px["wall"] / max(px["steps"], 1),
+                 "pool_refresh_ms": 1e3 * px["refresh"] / max(px["steps"], 1),
+                 "lp_kernel_ms": px["lp"] / 1e3 / max(px["steps"], 1),
+                 "lp_pivots_mean": px["piv"] / max(px["n"], 1),
+                 "alpha": px["alpha"]}
+                for it, xx, px in zip(x_iters, xs, per_x)]
 
     out = {
         "metric": "stage-2 subproblems/sec + cut-gen HBM GB/s on STORM",
@@ -285,19 +361,26 @@ def main():
         "dtype": "f64",
         "data": (f"synthetic: i.i.d. scenarios of {name}.sto drawn on the device (Philox4x32-10, seed {args.seed}, "
                  f"{t_gen:.2f} s for the shard)" if args.sampler == "device" else
-                 f"synthetic: i.i.d. scenarios of {name}.sto (numpy PCG64, seed {args.seed})") + ", x = EV solution",
+                 f"synthetic: i.i.d. scenarios of {name}.sto (numpy PCG64, seed {args.seed})") +
+                f"; steps cycle over {X} first-stage points (EV + SD candidates, {t_traj:.1f} s to generate)",
         "config": {"workload": f"{name} {N} scenarios" + (f" in {E} epigraphs" if E > 1 else "") +
                                (f" (importance-sampled, scale {args.importance_scale})" if args.importance_scale > 0 else "") +
-                               f" sharded over {world} GPU(s), |V|={nv}, "
-                               f"warm-start pool {pool_size}, LP solve + dual dedup + build_sasa_cut per step",
+                               f" sharded over {world} GPU(s), fixed |V|={nv}, " +
+                               (f"warm-start pool rebuilt at every new x ({args.refresh_pool} bases from "
+                                f"{args.refresh_train} training scenarios, timed), " if args.refresh else
+                                f"warm-start pool {pool_size} (trained at x_EV), ") + f"{X} x points, "
+                               "LP solve + dual dedup + build_sasa_cut per step",
                    "instance": name, "scenarios": N, "epigraphs": E, "vertices": nv, "k": k, "m2": m,
                    "basis_pool": pool_size, "pool_build_s": round(t_pool, 3),
+                   "pool_refresh": ({"train": args.refresh_train, "pool": args.refresh_pool} if args.refresh else None),
                    "pool_selection": (f"two-level: {args.pool_level1} + {args.pool_cands} candidates"
                                       if args.pool_level1 > 0 and pool_size > args.pool_level1 else "flat"),
+                   "x_points": X,
                    "parallelism": f"scenario-dp{world}"},
         "phases_ms_per_step": {"pool_select": t_sel / K / 1e3, "lp_kernel": t_lp / K / 1e3, "dedup": t_dd / K / 1e3,
                                "cut_partial": t_cut / K / 1e3, "cut_finalize": t_fin / K / 1e3},
         "lp_pivots_mean": piv_sum / (passes * n_local), "lp_pivots_max": piv_max,
+        "x_points": x_points,
         "roofline": {"kernel": "lp_hyper_kernel", "bound": "mfma",
                      "note": "fp64 peak (vector == matrix on gfx950); achieved = counted fp64 FLOPs of the executed pivot path / LP kernel time",
                      "achieved": lp_tflops, "peak": PEAK_FP64_TFS, "unit": "TFLOP/s",
@@ -305,54 +388,89 @@ def main():
         "cutgen": {"kernel": "cut_argmax_kernel (+vbase/fixup/reduce)", "hbm_gbs": cut_gbs,
                    "bytes_alg": bytes_alg, "flops_alg": flops_alg, "t_roof_ms": t_roof * 1e3,
                    "t_ms": cut_us / 1e3, "frac": t_roof / (cut_us * 1e-6),
+                   "mfma_tflops": flops_alg / (cut_us * 1e-6) / 1e12,
                    "bound": "mfma" if flops_alg / (PEAK_FP64_TFS * 1e12) > bytes_alg / (PEAK_HBM_GBS * 1e9) else "hbm"},
-        "alpha_check": alpha,
     }
 
-    # measured peaks of this part (tools/mfma_f64_probe.hip, committed under profiles/): the
-    # fp64 MFMA and VALU rates reach ~60 % / ~88 % of the spec, so both fractions are reported
-    peaks = latest_peaks()
-    if peaks:
-        vf = max((p["tflops"] for p in peaks if p["probe"] == "v_fma_f64"), default=None)
-        mf = max((p["tflops"] for p in peaks if p["probe"].startswith("mfma_f64")), default=None)
-        if vf:
-            out["roofline"].update({"peak_measured": vf, "frac_measured": lp_tflops / vf,
-                                    "peak_measured_source": "v_fma_f64 probe, " + peaks[0]["file"]})
-        if mf:
-            out["cutgen"].update({"mfma_tflops": flops_alg / (cut_us * 1e-6) / 1e12, "peak_measured_tflops": mf,
-                                  "frac_measured": flops_alg / (cut_us * 1e-6) / 1e12 / mf,
-                                  "peak_measured_source": "mfma_f64_16x16x4f64 probe, " + peaks[0]["file"]})
-
-    # HBM traffic of the dominant kernel from the committed rocprofv3 PMC summary of this exact
-    # workload (separate --pmc passes, tools/profile_round.sh), per launch like `achieved`
+    # HBM traffic and MFMA counters of the dominant kernels from the committed rocprofv3 PMC
+    # summary of this exact workload (separate --pmc passes, tools/profile_round.sh), per launch
     pmc = latest_pmc_summary()
     if pmc and world == 1 and pmc.get("scenarios") == N:
-        k = pmc["kernels"].get("lp_hyper_kernel")
-        if k:
-            out["roofline"]["traffic"] = k["hbm_bytes_per_launch"]
+        kl = pmc["kernels"].get("lp_hyper_kernel")
+        if kl:
+            out["roofline"]["traffic"] = kl["hbm_bytes_per_launch"]
             out["roofline"]["traffic_source"] = pmc["file"]
         kc = pmc["kernels"].get("cut_argmax_kernel")
         if kc:
             out["cutgen"]["traffic"] = kc["hbm_bytes_per_launch"]
+            if "mfma_util" in kc:
+                out["cutgen"]["mfma_util"] = kc["mfma_util"]
+            out["cutgen"]["traffic_source"] = pmc["file"]
+    if rank == 0 and world == 1 and args.spot > 0:
+        out["parity_spot_check"] = spot_check(sp2, ctx, epi, V, xs, x_iters, positions, args)
     if rank == 0 and world == 1 and not args.no_cpu:
         vals = twosd.get_scenarios(epi, 0, min(n_local, 1 << 19))   # the CPU sample: same scenarios
-        out["cpu_baseline"] = cpu_baseline(sp2, ctx, x, vals, V.matrix(), positions, args)
+        out["cpu_baseline"] = cpu_baseline(sp2, ctx, xs, x_iters, heads_at, vals, V.matrix(), args)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 
 
-def latest_peaks():
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "peaks.jsonl")))
-    if not files:
-        return None
-    with open(files[-1]) as f:
-        rows = [json.loads(l) for l in f if l.strip()]
-    for r in rows:
-        r["file"] = os.path.relpath(files[-1], ROOT)
-    return rows
+def sd_points(cor, tim, sp2, sto, positions, x_ev, iters, seed, device):
+    """First-stage points: x_EV for 0, else the candidate of SD iteration i (sd_iteration!,
+    algorithm.jl:39-115: master QP on the host, hot path on this GPU, one scenario per
+    iteration from the i.i.d. stream of `seed`), on a context of its own."""
+    from sqlp_amd import master, smps, twosd
+    out = {0: np.array(x_ev, dtype=np.float64)}
+    last = max(iters)
+    if last > 0:
+        sp1 = smps.get_smps_stage_template(cor, tim, 1)
+        c2 = twosd.SDContext(sp2, sto, device=device.index)
+        c2.compute_basis(x_ev, smps.mean_values(sto, positions))
+        cell = master.sdCell(sp1, c2)
+        cell.bind_epigraph(twosd.sdEpigraph(c2, 1.0, 0.0))
+        cell.x_candidate = np.array(x_ev, dtype=np.float64)
+        cell.x_incumbent = cell.x_candidate.copy()
+        rng = np.random.default_rng(seed)
+        for it in range(1, last + 1):
+            master.sd_iteration(cell, [smps.sample_values(sto, 1, rng, positions)[0]])
+            if it in iters:
+                out[it] = cell.x_candidate.copy()
+        c2.close()
+    return [out[i] for i in iters]
+
+
+def spot_check(sp2, ctx, epi, V, xs, x_iters, positions, args):
+    """Parity at bench scale (outside the timed region): the first `spot` scenarios of the
+    shard at every x point -- GPU LP objectives vs the C dual simplex (unique optimum), and the
+    GPU cut over those scenarios vs the reference-order C argmax/cut with the bench's V."""
+    from oracle import cpu
+    from sqlp_amd import twosd
+    n = min(args.spot, epi.num_scenarios)
+    vals = twosd.get_scenarios(epi, 0, n)
+    W, T = sp2.dense_W(), sp2.dense_T()
+    lp = cpu.CpuLP(W, sp2.q, sp2.sense)
+    lp.set_basis(ctx.get_basis())
+    rows = ctx.rows
+    DR = vals - sp2.r[rows]
+    sub = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(sub, vals)
+    Vm = V.matrix()
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    res = []
+    for it, xx in zip(x_iters, xs):
+        obj, _, _, st = twosd.solve_batch(sub, xx, 0, n, want_pi=False)
+        o_obj, _, _, o_st, _ = lp.solve_batch(rows, sp2.r - T @ xx, DR, nthreads=threads)
+        ok = (st == 0) & (o_st == 0)
+        lp_err = float(np.max(np.abs(obj[ok] - o_obj[ok]) / (1.0 + np.abs(o_obj[ok])))) if ok.any() else None
+        cut = twosd.build_sasa_cut(sub, xx, V, args.tie_rel)
+        a, b, _, _ = cpu.build_cut(sp2.r, T, xx, Vm, rows, DR, np.ones(n), tie_rel=args.tie_rel, nthreads=threads)
+        res.append({"x_iteration": it, "scenarios": n, "lp_not_optimal": int((~ok).sum()),
+                    "lp_obj_max_rel_err": lp_err,
+                    "alpha_rel_err": abs(cut.alpha - a) / (1.0 + abs(a)),
+                    "beta_max_rel_err": float(np.max(np.abs(cut.beta - b)) / (1.0 + np.max(np.abs(b))))})
+    return res
 
 
 def latest_pmc_summary():
@@ -367,9 +485,13 @@ def latest_pmc_summary():
     return d
 
 
-def cpu_baseline(sp2, ctx, x, vals, Vmat, positions, args):
-    """Oracle C restatement (warm-started dual simplex from the same basis + the
-    reference-order argmax/cut loops) on a bounded sample of the same workload."""
+def cpu_baseline(sp2, ctx, xs, x_iters, heads_at, vals, Vmat, args):
+    """Oracle C restatement on a bounded sample of the same workload (same scenarios, the same
+    x points, equal shares of the time budget): warm-started dual simplex + the reference-order
+    argmax/cut loops, OpenMP over the host cores.  Two warm starts: (i) the primary basis for
+    every scenario, (ii) per scenario the least-infeasible of the first `cpu_pool` bases of the
+    GPU's pool at that x (dense inverses built untimed, like the GPU pool's setup).  value = the
+    faster of the two."""
     from oracle import cpu
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     threads = max(1, min(threads, len(os.sched_getaffinity(0))))
@@ -378,21 +500,59 @@ def cpu_baseline(sp2, ctx, x, vals, Vmat, positions, args):
     lp = cpu.CpuLP(W, sp2.q, sp2.sense)
     lp.set_basis(ctx.get_basis())
     rows = ctx.rows
-    base = sp2.r - T @ x
     DR = vals - sp2.r[rows]
-    n_done, t_lp = 0, 0.0
     chunk = 256 * threads
-    while t_lp < args.cpu_seconds and n_done + chunk <= DR.shape[0]:
+    budget = args.cpu_seconds / len(xs)
+    tot = {"primary_basis": [0, 0.0, 0], "pooled": [0, 0.0, 0]}   # scenarios, seconds, pivots
+    at = 0                                                          # next unused sample row
+
+    def timed(solve, key):
+        nonlocal at
+        n, t, piv = 0, 0.0, 0
+        while t < budget and at + chunk <= DR.shape[0]:
+            t0 = time.perf_counter()
+            it = solve(DR[at:at + chunk])
+            t += time.perf_counter() - t0
+            piv += int(it.sum())
+            n += chunk
+            at += chunk
+        tot[key][0] += n; tot[key][1] += t; tot[key][2] += piv
+        return at - n, n
+
+    t_cut = n_cut = 0
+    t_setup = 0.0
+    P = 0
+    for xi, xx in enumerate(xs):
+        base = sp2.r - T @ xx
+        a0, n1 = timed(lambda d: lp.solve_batch(rows, base, d, nthreads=threads)[4], "primary_basis")
         t0 = time.perf_counter()
-        lp.solve_batch(rows, base, DR[n_done:n_done + chunk], nthreads=threads)
-        t_lp += time.perf_counter() - t0
-        n_done += chunk
-    t0 = time.perf_counter()
-    cpu.build_cut(sp2.r, T, x, Vmat, rows, DR[:n_done], np.ones(n_done), tie_rel=args.tie_rel, nthreads=threads)
-    t_cut = time.perf_counter() - t0
-    return {"value": n_done / (t_lp + t_cut), "unit": "subproblems/s", "cores": threads, "kind": "port",
-            "sample": f"{n_done} storm scenarios of the same stream: warm-started C dual simplex "
-                      f"({t_lp:.2f}s) + reference-order argmax/cut with |V|={Vmat.shape[0]} ({t_cut:.2f}s)"}
+        cpu.build_cut(sp2.r, T, xx, Vmat, rows, DR[a0:a0 + n1], np.ones(n1), tie_rel=args.tie_rel, nthreads=threads)
+        t_cut += time.perf_counter() - t0
+        n_cut += n1
+        heads = heads_at.get(xi)
+        if heads is not None and args.cpu_pool > 1 and heads.shape[0] > 1:
+            P = heads.shape[0]
+            t0 = time.perf_counter()
+            lp.set_pool(heads)
+            t_setup += time.perf_counter() - t0
+            timed(lambda d: lp.solve_batch_pool(rows, base, d, nthreads=threads)[3], "pooled")
+    cut_per = t_cut / max(n_cut, 1)
+    out = {"unit": "subproblems/s", "cores": threads, "kind": "port"}
+    for key, (n, t, piv) in tot.items():
+        if n:
+            out[key] = {"value": n / (t + cut_per * n), "scenarios": n, "lp_s": round(t, 3), "lp_pivots_mean": piv / n}
+    if "pooled" in out:
+        out["pooled"].update({"bases": P, "setup_s": round(t_setup, 2)})
+    best = max((k for k in tot if k in out), key=lambda k: out[k]["value"])
+    out["value"] = out[best]["value"]
+    out["sample"] = (f"{tot['primary_basis'][0]} + {tot['pooled'][0]} storm scenarios of the same stream over the "
+                     f"{len(xs)} x points (iterations {x_iters}): C dual simplex from the primary basis "
+                     f"({out['primary_basis']['lp_pivots_mean']:.1f} pivots)" +
+                     (f" and from the least-infeasible of the GPU pool's first {P} bases at each x "
+                      f"({out['pooled']['lp_pivots_mean']:.1f} pivots)" if "pooled" in out else "") +
+                     f" + reference-order argmax/cut with |V|={Vmat.shape[0]} ({cut_per * 1e6:.0f} us per scenario); "
+                     f"value = {best}")
+    return out
 
 
 if __name__ == "__main__":

@@ -105,6 +105,17 @@ int twosd_pool_build(twosd_ctx *ctx, int epi, const double *x, int first, int co
  * by any change of the pool. */
 int twosd_pool_build_candidates(twosd_ctx *ctx, int epi, const double *x, int first, int count, int level1,
                                 int ncand);
+/* Rebuild the pool at x: solve the training scenarios [first, first+count) of epi at x from
+ * the current pool and replace the pool by the primary basis plus their max_pool - 1 most
+ * frequent optimal bases (ties: first occurrence).  A pool's bases are optimal near the x they
+ * were harvested at, so a first-stage point far from the last one (an SD candidate, the x
+ * of an evaluate) gets a pool of its own.  B^{-1} of each new basis is composed from its start
+ * basis and the eta file of its solve (no refactorisation).  Selection becomes flat (candidate
+ * lists reset).  last_refresh_ms: [training solves, re-solves of the harvested scenarios,
+ * host composition, upload of the pool's device form, total] of the last refresh. */
+int twosd_pool_refresh(twosd_ctx *ctx, int epi, const double *x, int first, int count, int max_pool,
+                       int *pool_size);
+int twosd_last_refresh_ms(twosd_ctx *ctx, double *ms5);
 int twosd_pool_size(twosd_ctx *ctx, int *size);
 int twosd_pool_get(twosd_ctx *ctx, int p, int *head);
 /* Pool basis each scenario of the last LP batch started from (first N of it; 0 = the
@@ -185,6 +196,10 @@ int twosd_dvs_fingerprint(twosd_ctx *ctx, uint64_t *digest);
  */
 int twosd_solve_push(twosd_ctx *ctx, int epi, const double *x, int first, int count,
                      double *obj, int *status, int *new_size);
+/* Scenarios whose dual the last twosd_solve_push recovered and pushed: the first scenario of
+ * each distinct optimal dual vertex of the batch (every later scenario at a vertex pushes an
+ * equal vector, a no-op of push!, dual_set.jl:84-94); `count` with TWOSD_PUSH_ALL=1. */
+int twosd_last_push_reps(twosd_ctx *ctx, int *reps);
 
 /*
  * build_sasa_cut (epigraph.jl:125-146) incl. argmax_procedure (subprob.jl:141-169) over

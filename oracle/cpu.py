@@ -37,6 +37,8 @@ def lib():
         L.oracle_lp_basis_dual_infeas.restype = C.c_double
         L.oracle_lp_solve_from_slack.argtypes = [P, P, P, P, P]
         L.oracle_lp_solve_batch.argtypes = [P, C.c_int, C.c_int, P, P, P, C.c_int, P, P, P, P, P, C.c_int]
+        L.oracle_lp_set_pool.argtypes = [P, C.c_int, P]
+        L.oracle_lp_solve_batch_pool.argtypes = [P, C.c_int, C.c_int, P, P, P, C.c_int, P, P, P, P, P, C.c_int]
         L.oracle_build_cut.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P, P, P,
                                        C.c_double, P, P, P, P, C.c_int]
         L.oracle_dense_inverse.argtypes = [C.c_int, P, P]
@@ -106,6 +108,27 @@ class CpuLP:
         lib().oracle_lp_solve_batch(self.h, N, k, _p(rows), _p(base), _p(DR), kmax, _p(obj), _p(pi),
                                     _p(y), _p(st), _p(it), nthreads)
         return obj, pi, y, st, it
+
+
+    def set_pool(self, heads):
+        """Warm-start pool: P bases (P x m heads) with dense inverses (setup)."""
+        self.pool_heads = np.ascontiguousarray(heads, dtype=np.int32)
+        rc = lib().oracle_lp_set_pool(self.h, self.pool_heads.shape[0], _p(self.pool_heads))
+        if rc != 0:
+            raise RuntimeError(f"singular pool basis {-1 - rc}")
+
+    def solve_batch_pool(self, rows, base, DR, kmax=512, nthreads=0):
+        """solve_batch with each scenario started from the pool basis of least total primal
+        infeasibility (the GPU's level-1 selection key); returns obj, pi, st, iters, picks."""
+        DR = np.ascontiguousarray(DR, dtype=np.float64)
+        N, k = DR.shape
+        rows = np.ascontiguousarray(rows, dtype=np.int32)
+        base = np.ascontiguousarray(base, dtype=np.float64)
+        obj = np.zeros(N); pi = np.zeros((N, self.m)); st = np.zeros(N, dtype=np.int32)
+        it = np.zeros(N, dtype=np.int32); picks = np.zeros(N, dtype=np.int32)
+        lib().oracle_lp_solve_batch_pool(self.h, N, k, _p(rows), _p(base), _p(DR), kmax, _p(obj), _p(pi),
+                                         _p(st), _p(it), _p(picks), nthreads)
+        return obj, pi, st, it, picks
 
 
 def build_cut(r, T, x, V, rows, DR, w, tie_rel=0.0, nthreads=0):

@@ -311,6 +311,9 @@ typedef struct {
     lp_t L;
     int *colptr, *rowidx; double *val, *q; signed char *sense;
     int *head0; double *B0inv, *B0invT, *pi0;
+    /* warm-start pool (oracle_lp_set_pool): P bases with dense inverses */
+    int P;
+    int *pheads; double *pBinv, *pBinvT, *ppi0;
 } oracle_ctx;
 
 void *oracle_lp_create(int m, int n, const int *colptr, const int *rowidx, const double *val,
@@ -333,6 +336,7 @@ void *oracle_lp_create(int m, int n, const int *colptr, const int *rowidx, const
 
 void oracle_lp_destroy(void *p) {
     oracle_ctx *C = (oracle_ctx *)p; if (!C) return;
+    free(C->pheads); free(C->pBinv); free(C->pBinvT); free(C->ppi0);
     free(C->colptr); free(C->rowidx); free(C->val); free(C->q); free(C->sense);
     free(C->head0); free(C->B0inv); free(C->B0invT); free(C->pi0); free(C);
 }
@@ -475,4 +479,110 @@ void oracle_build_cut(int m, int n1, int nv, int N, int k, const int *rows, cons
     }
     *alpha = a;
     free(g); free(base); free(vb);
+}
+
+/* ================= warm-start pool (CPU counterpart of the GPU basis pool) ================= */
+
+/*
+ * Install P dual-feasible bases (heads[P*m]) with their dense inverses (setup, OpenMP over
+ * the bases).  Returns 0, or -1 - p for the first singular basis p.
+ */
+int oracle_lp_set_pool(void *p, int P, const int *heads) {
+    oracle_ctx *C = (oracle_ctx *)p; const int m = C->L.m;
+    free(C->pheads); free(C->pBinv); free(C->pBinvT); free(C->ppi0);
+    C->P = P;
+    C->pheads = (int *)malloc(sizeof(int) * (size_t)P * m);
+    memcpy(C->pheads, heads, sizeof(int) * (size_t)P * m);
+    C->pBinv = (double *)malloc(sizeof(double) * (size_t)P * m * m);
+    C->pBinvT = (double *)malloc(sizeof(double) * (size_t)P * m * m);
+    C->ppi0 = (double *)malloc(sizeof(double) * (size_t)P * m);
+    int bad = 0;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int q = 0; q < P; ++q) {
+        const int *h = C->pheads + (size_t)q * m;
+        double *B = (double *)malloc(sizeof(double) * (size_t)m * m);
+        double *Bi = C->pBinv + (size_t)q * m * m, *BiT = C->pBinvT + (size_t)q * m * m;
+        build_basis(&C->L, h, B);
+        if (oracle_dense_inverse(m, B, Bi)) {
+#pragma omp critical
+            if (!bad) bad = -1 - q;
+        } else {
+            for (int i = 0; i < m; ++i) for (int j = 0; j < m; ++j) BiT[(size_t)j * m + i] = Bi[(size_t)i * m + j];
+            for (int j = 0; j < m; ++j) {
+                double sum = 0; for (int i = 0; i < m; ++i) sum += var_cost(&C->L, h[i]) * Bi[(size_t)i * m + j];
+                C->ppi0[(size_t)q * m + j] = sum;
+            }
+        }
+        free(B);
+    }
+    return bad;
+}
+
+/*
+ * Batched solve with a per-scenario warm start from the pool: the basis with the least total
+ * primal infeasibility sum_i |infeas(x_B,i)| at b_s (lowest p on ties) -- the selection key of
+ * the GPU's level-1 pool selection -- then the same dual simplex as oracle_lp_solve_batch.
+ * x_B of basis p at b_s = B_p^{-1} base + sum_j B_p^{-1}[:, rows_j] DR[s,j]; the second term
+ * runs over the nonzeros of B_p^{-1}[:, rows] (setup per call, like the GPU's per-x data).
+ * picks[N] (nullable): the chosen pool basis.
+ */
+int oracle_lp_solve_batch_pool(void *p, int N, int k, const int *rows, const double *base, const double *DR,
+                               int kmax, double *obj, double *pi, int *status, int *iters, int *picks, int nthreads) {
+    oracle_ctx *C = (oracle_ctx *)p; const int m = C->L.m, n = C->L.n, P = C->P;
+    if (P <= 0) return -1;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+    double *xb = (double *)malloc(sizeof(double) * (size_t)P * m);
+    int *kp = (int *)malloc(sizeof(int) * ((size_t)P * m + 1));
+    int *kc = NULL; double *kv = NULL; size_t cap = 0, nz = 0;
+    for (int q = 0; q < P; ++q) {   /* x-dependent part and the element columns as per-row lists */
+        const double *Bi = C->pBinv + (size_t)q * m * m;
+        for (int i = 0; i < m; ++i) {
+            double sum = 0; for (int j = 0; j < m; ++j) sum += Bi[(size_t)i * m + j] * base[j];
+            xb[(size_t)q * m + i] = sum;
+            kp[(size_t)q * m + i] = (int)nz;
+            for (int e = 0; e < k; ++e) {
+                const double v = Bi[(size_t)i * m + rows[e]];
+                if (v == 0.0) continue;
+                if (nz == cap) { cap = cap ? 2 * cap : 4096; kc = (int *)realloc(kc, sizeof(int) * cap); kv = (double *)realloc(kv, sizeof(double) * cap); }
+                kc[nz] = e; kv[nz] = v; ++nz;
+            }
+        }
+    }
+    kp[(size_t)P * m] = (int)nz;
+#pragma omp parallel
+    {
+        ws_t W; ws_alloc(&W, m, n, kmax);
+        double *b = (double *)malloc(sizeof(double) * m);
+        double *pi_l = (double *)malloc(sizeof(double) * m);
+#pragma omp for schedule(dynamic, 4)
+        for (int s = 0; s < N; ++s) {
+            const double *dr = DR + (size_t)s * k;
+            int best_p = 0; double best = INFINITY;
+            for (int q = 0; q < P; ++q) {
+                const int *h = C->pheads + (size_t)q * m;
+                double inf = 0.0;
+                for (int i = 0; i < m && inf < best; ++i) {
+                    double x = xb[(size_t)q * m + i];
+                    for (int t = kp[(size_t)q * m + i]; t < kp[(size_t)q * m + i + 1]; ++t) x += kv[t] * dr[kc[t]];
+                    const int j = h[i]; const double lb = var_lb(&C->L, j), ub = var_ub(&C->L, j);
+                    if (x < lb - TOL_P * (1.0 + fabs(lb))) inf += lb - x;
+                    else if (x > ub + TOL_P * (1.0 + fabs(ub))) inf += x - ub;
+                }
+                if (inf < best) { best = inf; best_p = q; }
+            }
+            memcpy(b, base, sizeof(double) * m);
+            for (int j = 0; j < k; ++j) b[rows[j]] += dr[j];
+            int it = 0;
+            status[s] = solve_one(&C->L, C->pheads + (size_t)best_p * m, C->pBinv + (size_t)best_p * m * m,
+                                  C->pBinvT + (size_t)best_p * m * m, C->ppi0 + (size_t)best_p * m, b, &W, 1 << 30,
+                                  &obj[s], pi ? pi + (size_t)s * m : pi_l, NULL, &it, NULL);
+            if (iters) iters[s] = it;
+            if (picks) picks[s] = best_p;
+        }
+        ws_free(&W); free(b); free(pi_l);
+    }
+    free(xb); free(kp); free(kc); free(kv);
+    return 0;
 }

@@ -37,6 +37,8 @@ SIGNATURES = [
     ("twosd_pool_add_basis", I, [P, P, P]),
     ("twosd_pool_build", I, [P, I, P, I, I, I, P]),
     ("twosd_pool_build_candidates", I, [P, I, P, I, I, I, I]),
+    ("twosd_pool_refresh", I, [P, I, P, I, I, I, P]),
+    ("twosd_last_refresh_ms", I, [P, P]),
     ("twosd_pool_size", I, [P, P]),
     ("twosd_pool_get", I, [P, I, P]),
     ("twosd_last_pool_picks", I, [P, I, P]),
@@ -57,6 +59,7 @@ SIGNATURES = [
     ("twosd_dvs_truncate", I, [P, I]),
     ("twosd_dvs_fingerprint", I, [P, P]),
     ("twosd_solve_push", I, [P, I, P, I, I, P, P, P]),
+    ("twosd_last_push_reps", I, [P, P]),
     ("twosd_build_cut", I, [P, I, P, D, P, P, P, P, P]),
     ("twosd_cut_partial_len", I, [P, P, P]),
     ("twosd_cut_partial", I, [P, I, P, D, D, P, P, P, P]),

@@ -14,6 +14,7 @@
 #include <string>
 #include <vector>
 #include <map>
+#include <memory>
 #include <thread>
 #include <chrono>
 #include "twosd_internal.h"
@@ -122,6 +123,30 @@ static void build_ell(int S, F colf, std::vector<int> &slot, std::vector<int> &i
     }
 }
 
+// f(i) for i in [0, n) on up to 16 host threads (per-basis pool preparation: independent work)
+template <typename F>
+static void parallel_for(int n, F f) {
+    const int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (n < 64 || nth == 1) {
+        for (int i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nth; ++t)
+        th.emplace_back([&, t]() {
+            for (int i = t; i < n; i += nth) f(i);
+        });
+    for (auto &t : th) t.join();
+}
+
+template <typename T>
+static int upload_raw(T **d, const T *h, size_t n) {
+    int rc = dalloc(d, std::max<size_t>(n, 1));
+    if (rc) return rc;
+    if (n) HIPCHK(hipMemcpy(*d, h, sizeof(T) * n, hipMemcpyHostToDevice));
+    return TWOSD_OK;
+}
+
 template <typename T>
 static int upload(T **d, const std::vector<T> &h) {
     int rc = dalloc(d, std::max<size_t>(h.size(), 1));
@@ -152,6 +177,11 @@ static void free_template(twosd_ctx *c) {
     c->out_cap = 0; c->dvtmp_cap = 0;
     dvs_free(c);
     cut_free(c);
+    vkey_free(c);
+    dfree(c->d_vkey); c->vkey_cap = 0;
+    dfree(c->d_bkey); c->bkey_cap = 0;
+    dfree(c->d_eo_pb); dfree(c->d_eo_K); dfree(c->d_eo_off); dfree(c->d_eo_etap); dfree(c->d_eo_etaoff);
+    dfree(c->d_eo_eidx); dfree(c->d_eo_evals); dfree(c->d_eo_used); c->eo_rows = c->eo_cap = 0; c->eo_kmax = 0;
     c->has_template = c->has_basis = false;
 }
 
@@ -356,15 +386,17 @@ static int make_pool_basis(twosd_ctx *c, const std::vector<int> &head, PoolBasis
 // d0 (64C), B^{-1} columns as sliced ELL (bslot absolute into the concatenated bix/bv),
 // B^{-1} rows as CSR (brptr absolute into the concatenated brcol/brval).
 static int upload_pool(twosd_ctx *c) {
+    const auto t_up0 = std::chrono::steady_clock::now();
     const HostLP &L = c->L;
     const int m = L.m, n = L.n, MP = c->MP, P = (int)c->pool.size();
     std::vector<int8_t> bt(n + m);
     HIPCHK(hipMemcpy(bt.data(), c->d_btype, n + m, hipMemcpyDeviceToHost));
     std::vector<int> hb((size_t)P * MP, -1), bnnz(P, 0);
     std::vector<uint64_t> basic((size_t)P * 64, 0);
-    std::vector<int> bs_all, bi_all, rp_all, rc_all;
-    std::vector<double> bv_all, rv_all, d0_all;
-    for (int p = 0; p < P; ++p) {
+    struct Up { std::vector<int> bs, bi; std::vector<double> bv; };
+    std::vector<Up> up(c->CH > 0 ? P : 0);
+    std::vector<double> d0_all(c->CH > 0 ? (size_t)P * 64 * c->CH : 0, 0.0);
+    parallel_for(P, [&](int p) {
         const PoolBasis &B = c->pool[p];
         std::vector<char> isb(n + m, 0);
         for (int i = 0; i < m; ++i) {
@@ -372,44 +404,66 @@ static int upload_pool(twosd_ctx *c) {
             basic[(size_t)p * 64 + (B.head[i] & 63)] |= 1ull << (B.head[i] >> 6);
             isb[B.head[i]] = 1;
         }
-        if (c->CH <= 0) continue;
-        std::vector<double> d0((size_t)64 * c->CH, 0.0);
+        bnnz[p] = (int)B.rcol.size();
+        if (c->CH <= 0) return;
+        double *d0 = d0_all.data() + (size_t)p * 64 * c->CH;
         for (int j = 0; j < n + m; ++j) {
             if (isb[j]) continue;
-            double s = 0.0;
-            if (j >= n) s = B.pi0[j - n];
+            double sum = 0.0;
+            if (j >= n) sum = B.pi0[j - n];
             else
-                for (int q = L.colptr[j]; q < L.colptr[j + 1]; ++q) s += B.pi0[L.rowidx[q]] * L.val[q];
-            d0[j] = (j < n ? L.q[j] : 0.0) - s;
+                for (int q = L.colptr[j]; q < L.colptr[j + 1]; ++q) sum += B.pi0[L.rowidx[q]] * L.val[q];
+            d0[j] = (j < n ? L.q[j] : 0.0) - sum;
         }
-        d0_all.insert(d0_all.end(), d0.begin(), d0.end());
         // columns of B^{-1} (CSC from the row CSR; rows ascending within a column)
         std::vector<std::vector<std::pair<int, double>>> cols(m);
         for (int i = 0; i < m; ++i)
             for (int q = B.rptr[i]; q < B.rptr[i + 1]; ++q) cols[B.rcol[q]].push_back({i, B.rval[q]});
-        std::vector<int> bs, bi;
-        std::vector<double> bvv;
         build_ell(c->R, [&](int cc, std::vector<std::pair<int, double>> &out) {
             if (cc < m) out = cols[cc];
-        }, bs, bi, bvv);
-        bnnz[p] = (int)B.rcol.size();
-        const int eoff = (int)(bi_all.size() / 64);
-        for (int v : bs) bs_all.push_back(v + eoff);
-        bi_all.insert(bi_all.end(), bi.begin(), bi.end());
-        bv_all.insert(bv_all.end(), bvv.begin(), bvv.end());
-        const int roff = (int)rc_all.size();
-        for (int i = 0; i <= MP; ++i) rp_all.push_back(roff + B.rptr[std::min(i, m)]);
-        rc_all.insert(rc_all.end(), B.rcol.begin(), B.rcol.end());
-        rv_all.insert(rv_all.end(), B.rval.begin(), B.rval.end());
+        }, up[p].bs, up[p].bi, up[p].bv);
+    });
+    const auto tb = std::chrono::steady_clock::now();
+    // concatenation: offsets first, then every basis copies its part (sizes known up front)
+    std::vector<size_t> eo(P + 1, 0), ro(P + 1, 0);
+    for (int p = 0; p < P; ++p) {
+        eo[p + 1] = eo[p] + (c->CH > 0 ? up[p].bi.size() : 0);
+        ro[p + 1] = ro[p] + c->pool[p].rcol.size();
     }
+    if (eo[P] / 64 > INT32_MAX || ro[P] > INT32_MAX) return fail(TWOSD_E_UNSUPPORTED, "basis pool too large (> 2^31 entries)");
+    // default-initialised (not zeroed) buffers: every entry is written below, first touch in parallel
+    std::vector<int> bs_all(c->CH > 0 ? (size_t)P * (c->R + 1) : 0), rp_all((size_t)P * (MP + 1));
+    std::unique_ptr<int[]> bi_all(new int[std::max<size_t>(eo[P], 1)]), rc_all(new int[std::max<size_t>(ro[P], 1)]);
+    std::unique_ptr<double[]> bv_all(new double[std::max<size_t>(eo[P], 1)]), rv_all(new double[std::max<size_t>(ro[P], 1)]);
+    parallel_for(P, [&](int p) {
+        const PoolBasis &B = c->pool[p];
+        if (c->CH > 0) {
+            const int e0 = (int)(eo[p] / 64);
+            for (int t = 0; t <= c->R; ++t) bs_all[(size_t)p * (c->R + 1) + t] = up[p].bs[t] + e0;
+            std::copy(up[p].bi.begin(), up[p].bi.end(), bi_all.get() + eo[p]);
+            std::copy(up[p].bv.begin(), up[p].bv.end(), bv_all.get() + eo[p]);
+        }
+        for (int i = 0; i <= MP; ++i) rp_all[(size_t)p * (MP + 1) + i] = (int)ro[p] + B.rptr[std::min(i, m)];
+        std::copy(B.rcol.begin(), B.rcol.end(), rc_all.get() + ro[p]);
+        std::copy(B.rval.begin(), B.rval.end(), rv_all.get() + ro[p]);
+    });
+    const auto tc = std::chrono::steady_clock::now();
     int rc;
     if ((rc = upload(&c->d_hb0, hb)) || (rc = upload(&c->d_basic0, basic)) || (rc = upload(&c->d_bnnz, bnnz))) return rc;
     if (c->CH > 0) {
-        if ((rc = upload(&c->d_bslot, bs_all)) || (rc = upload(&c->d_bix, bi_all)) || (rc = upload(&c->d_bv, bv_all)) ||
-            (rc = upload(&c->d_brptr, rp_all)) || (rc = upload(&c->d_brcol, rc_all)) || (rc = upload(&c->d_brval, rv_all)) ||
+        if ((rc = upload(&c->d_bslot, bs_all)) || (rc = upload_raw(&c->d_bix, bi_all.get(), eo[P])) ||
+            (rc = upload_raw(&c->d_bv, bv_all.get(), eo[P])) || (rc = upload(&c->d_brptr, rp_all)) ||
+            (rc = upload_raw(&c->d_brcol, rc_all.get(), ro[P])) || (rc = upload_raw(&c->d_brval, rv_all.get(), ro[P])) ||
             (rc = upload(&c->d_d0, d0_all)))
             return rc;
         c->b0_nnz = bnnz[0];
+    }
+    if (getenv("TWOSD_DEBUG")) {
+        const auto td = std::chrono::steady_clock::now();
+        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        fprintf(stderr, "upload_pool P=%d: build %.1f ms, concat %.1f ms, upload %.1f ms (%.1f MB: ell %zu, csr %zu, d0 %zu)\n", P,
+                ms(t_up0, tb), ms(tb, tc), ms(tc, td),
+                (eo[P] * 12.0 + ro[P] * 12.0 + d0_all.size() * 8.0) / 1e6, eo[P], ro[P], d0_all.size());
     }
     c->prep_valid = false;
     c->k_valid = false;
@@ -604,6 +658,226 @@ extern "C" int twosd_pool_build(twosd_ctx *c, int epi, const double *x, int firs
 }
 
 static int select_pool(twosd_ctx *c, const double *d_dv, int N, int *d_pick, int npool_override);
+static int prepare_elements(twosd_ctx *c);
+
+// ---- pool refresh at x: the pool's bases are optimal near the x they were harvested at
+// (storm: 8.9 pivots per scenario at the training x, 28-67 at SD candidates 25-37 % away), so a
+// new x gets a pool of its own.  B^{-1} of a harvested basis is composed from its start basis
+// and the eta file of its solve, B^{-1} = E_K..E_1 B_pb^{-1} (sparse row merges), so no
+// refactorisation: the cost is the training solves plus O(K nnz) host work per basis.
+
+// rows of B^{-1} (CSR, columns ascending) after the eta file, tiny entries dropped
+static void compose_binv(const PoolBasis &B0, int m, int K, const int *etap, const int *etaoff, const int *eidx,
+                         const double *evals, PoolBasis &out) {
+    std::vector<std::vector<std::pair<int, double>>> rows(m);
+    for (int i = 0; i < m; ++i)
+        for (int q = B0.rptr[i]; q < B0.rptr[i + 1]; ++q) rows[i].push_back({B0.rcol[q], B0.rval[q]});
+    std::vector<std::pair<int, double>> rr, tmp;
+    for (int t = 0; t < K; ++t) {
+        const int r = etap[t];
+        rr = rows[r];
+        for (int e = etaoff[t]; e < etaoff[t + 1]; ++e) {
+            const int i = eidx[e];
+            const double v = evals[e];
+            if (i == r) {
+                rows[r] = rr;
+                for (auto &cv : rows[r]) cv.second *= v;
+                continue;
+            }
+            // rows[i] += v * rr (both sorted by column)
+            tmp.clear();
+            const auto &a = rows[i];
+            size_t p = 0, q = 0;
+            while (p < a.size() || q < rr.size()) {
+                if (q == rr.size() || (p < a.size() && a[p].first < rr[q].first)) tmp.push_back(a[p++]);
+                else if (p == a.size() || rr[q].first < a[p].first) { tmp.push_back({rr[q].first, v * rr[q].second}); ++q; }
+                else { tmp.push_back({a[p].first, std::fma(v, rr[q].second, a[p].second)}); ++p; ++q; }
+            }
+            rows[i].swap(tmp);
+        }
+    }
+    double amax = 0.0;
+    for (auto &row : rows)
+        for (auto &cv : row) amax = std::max(amax, std::fabs(cv.second));
+    const double drop = 1e-14 * amax;
+    out.rptr.assign(1, 0);
+    out.rcol.clear(); out.rval.clear();
+    for (auto &row : rows) {
+        for (auto &cv : row)
+            if (std::fabs(cv.second) > drop) { out.rcol.push_back(cv.first); out.rval.push_back(cv.second); }
+        out.rptr.push_back((int)out.rcol.size());
+    }
+}
+
+// pi0 = c_B' B^{-1}; checks dual feasibility (1e-7) and B^{-1} a_{head[i]} = e_i on a few
+// positions (1e-8); nullptr if the basis is usable
+static const char *finish_composed(const twosd_ctx *c, PoolBasis &B) {
+    const HostLP &L = c->L;
+    const int m = L.m, n = L.n;
+    B.pi0.assign(m, 0.0);
+    for (int i = 0; i < m; ++i) {
+        const int j = B.head[i];
+        const double cb = j < n ? L.q[j] : 0.0;
+        if (cb == 0.0) continue;
+        for (int q = B.rptr[i]; q < B.rptr[i + 1]; ++q) B.pi0[B.rcol[q]] += cb * B.rval[q];
+    }
+    std::vector<char> isb(n + m, 0);
+    for (int i = 0; i < m; ++i) isb[B.head[i]] = 1;
+    for (int j = 0; j < n + m; ++j) {
+        if (isb[j]) continue;
+        double d;
+        char sense = 'Y';
+        if (j < n) {
+            d = L.q[j];
+            for (int q = L.colptr[j]; q < L.colptr[j + 1]; ++q) d -= B.pi0[L.rowidx[q]] * L.val[q];
+        } else {
+            sense = L.sense[j - n];
+            if (sense == 'E') continue;
+            d = -B.pi0[j - n];
+        }
+        const double inf = sense == 'G' ? d : -d;   // G slack sits at its upper bound 0
+        if (inf > 1e-7) return "composed basis is not dual feasible";
+    }
+    std::vector<double> a(m);
+    for (int probe = 0; probe < 4; ++probe) {
+        const int i0 = (int)(((long long)probe * 7919 + 13) % m);
+        const int j = B.head[i0];
+        std::fill(a.begin(), a.end(), 0.0);
+        if (j >= n) a[j - n] = 1.0;
+        else
+            for (int q = L.colptr[j]; q < L.colptr[j + 1]; ++q) a[L.rowidx[q]] = L.val[q];
+        for (int i = 0; i < m; ++i) {
+            double v = 0.0;
+            for (int q = B.rptr[i]; q < B.rptr[i + 1]; ++q) v += B.rval[q] * a[B.rcol[q]];
+            if (std::fabs(v - (i == i0 ? 1.0 : 0.0)) > 1e-8) return "composed B^{-1} inconsistent";
+        }
+    }
+    return nullptr;
+}
+
+extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int first, int count, int max_pool,
+                                  int *pool_size) {
+    if (!c || !c->has_basis) return fail(TWOSD_E_STATE, "pool_refresh: no primary basis");
+    if (epi < 0 || epi >= (int)c->epis.size()) return fail(TWOSD_E_ARG, "pool_refresh: epigraph %d does not exist", epi);
+    const EpiDevice &E = c->epis[epi];
+    if (first < 0 || count < 1 || first + count > E.count || max_pool < 1 || (c->n1 > 0 && !x))
+        return fail(TWOSD_E_ARG, "pool_refresh: bad arguments");
+    if (c->CH <= 0) return fail(TWOSD_E_UNSUPPORTED, "pool_refresh: needs the hypersparse LP kernel");
+    HIPCHK(hipSetDevice(c->device));
+    const auto t0 = std::chrono::steady_clock::now();
+    const int m = c->L.m;
+    const double *d_dv = E.d_dv + (size_t)first * c->k;
+    int rc;
+    // 1. training solves at x from the current pool, basis keys
+    LpRun o;
+    o.want_bkey = true;
+    if ((rc = run_lp_ex(c, x, d_dv, count, o))) return rc;
+    const auto t1 = std::chrono::steady_clock::now();
+    // 2. distinct optimal bases, most frequent first (ties: first occurrence), primary excluded
+    const int *d_list = nullptr, *d_counts = nullptr;
+    int U = 0;
+    if ((rc = vkey_first_occurrences(c, count, c->d_bkey, c->d_status, &d_list, &U, &d_counts))) return rc;
+    std::vector<int> reps(U), cnts(U);
+    if (U > 0) {
+        HIPCHK(hipMemcpy(reps.data(), d_list, sizeof(int) * U, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(cnts.data(), d_counts, sizeof(int) * U, hipMemcpyDeviceToHost));
+    }
+    std::vector<int> ord(U);
+    for (int a = 0; a < U; ++a) ord[a] = a;
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return cnts[a] > cnts[b]; });
+    const int R = std::min(U, max_pool - 1);
+    std::vector<int> sel(R);
+    for (int a = 0; a < R; ++a) sel[a] = reps[ord[a]];
+    std::vector<PoolBasis> fresh;
+    if (R > 0) {
+        // 3. re-solve the selected scenarios (same starts, so the same pivots) with their eta files
+        int *d_sel = nullptr;
+        if ((rc = dalloc(&d_sel, (size_t)R))) return rc;
+        HIPCHK(hipMemcpy(d_sel, sel.data(), sizeof(int) * R, hipMemcpyHostToDevice));
+        LpRun r;
+        r.d_list = d_sel;
+        r.nlist = R;
+        r.want_etas = true;
+        r.want_head = true;
+        rc = run_lp_ex(c, x, d_dv, count, r);
+        hipFree(d_sel);
+        if (rc) return rc;
+        const int kmax = c->eo_kmax;
+        std::vector<int> pb(R), K(R), off(R), etap((size_t)R * kmax), etaoff((size_t)R * (kmax + 1)), heads((size_t)R * m);
+        int used = 0;
+        HIPCHK(hipMemcpy(pb.data(), c->d_eo_pb, sizeof(int) * R, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(K.data(), c->d_eo_K, sizeof(int) * R, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(off.data(), c->d_eo_off, sizeof(int) * R, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(etap.data(), c->d_eo_etap, sizeof(int) * etap.size(), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(etaoff.data(), c->d_eo_etaoff, sizeof(int) * etaoff.size(), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(heads.data(), c->d_head_out, sizeof(int) * heads.size(), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&used, c->d_eo_used, sizeof(int), hipMemcpyDeviceToHost));
+        used = std::min<int>(used, (int)c->eo_cap);
+        std::vector<int> ei(std::max(used, 1));
+        std::vector<double> ev(std::max(used, 1));
+        if (used > 0) {
+            HIPCHK(hipMemcpy(ei.data(), c->d_eo_eidx, sizeof(int) * used, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(ev.data(), c->d_eo_evals, sizeof(double) * used, hipMemcpyDeviceToHost));
+        }
+        const auto t2 = std::chrono::steady_clock::now();
+        c->last_refresh_ms[1] = std::chrono::duration<double, std::milli>(t2 - t1).count();
+        // 4. compose B^{-1} of every new basis on the host threads
+        fresh.resize(R);
+        std::vector<char> ok(R, 0);
+        const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nth; ++t)
+            th.emplace_back([&, t]() {
+                for (int a = (int)t; a < R; a += (int)nth) {
+                    if (K[a] < 0 || pb[a] < 0 || pb[a] >= (int)c->pool.size()) continue;
+                    PoolBasis &B = fresh[a];
+                    B.head.assign(heads.begin() + (size_t)a * m, heads.begin() + (size_t)(a + 1) * m);
+                    const int *eo = etaoff.data() + (size_t)a * (kmax + 1);
+                    compose_binv(c->pool[pb[a]], m, K[a], etap.data() + (size_t)a * kmax, eo, ei.data() + off[a],
+                                 ev.data() + off[a], B);
+                    ok[a] = finish_composed(c, B) == nullptr;
+                }
+            });
+        for (auto &t : th) t.join();
+        c->last_refresh_ms[2] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count();
+        std::vector<PoolBasis> keep;
+        keep.reserve(R + 1);
+        keep.push_back(std::move(c->pool[0]));   // the primary basis stays pool[0]
+        for (int a = 0; a < R; ++a)
+            if (ok[a]) keep.push_back(std::move(fresh[a]));
+        c->pool.swap(keep);
+    } else {
+        c->pool.resize(1);
+        c->last_refresh_ms[1] = c->last_refresh_ms[2] = 0.0;
+    }
+    // training box of the deltas (selection row pruning), as twosd_pool_build
+    if (c->k > 0) {
+        std::vector<double> dv((size_t)count * c->k);
+        HIPCHK(hipMemcpy(dv.data(), d_dv, sizeof(double) * dv.size(), hipMemcpyDeviceToHost));
+        c->sel_lo.assign(c->k, INFINITY);
+        c->sel_hi.assign(c->k, -INFINITY);
+        for (int s2 = 0; s2 < count; ++s2)
+            for (int e = 0; e < c->k; ++e) {
+                c->sel_lo[e] = std::min(c->sel_lo[e], dv[(size_t)s2 * c->k + e]);
+                c->sel_hi[e] = std::max(c->sel_hi[e], dv[(size_t)s2 * c->k + e]);
+            }
+    }
+    const auto tu = std::chrono::steady_clock::now();
+    if ((rc = upload_pool(c)) || (rc = prepare_elements(c))) return rc;
+    const auto t3 = std::chrono::steady_clock::now();
+    c->last_refresh_ms[0] = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    c->last_refresh_ms[3] = std::chrono::duration<double, std::milli>(t3 - tu).count();
+    c->last_refresh_ms[4] = std::chrono::duration<double, std::milli>(t3 - t0).count();
+    if (pool_size) *pool_size = (int)c->pool.size();
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_last_refresh_ms(twosd_ctx *c, double *ms5) {
+    if (!c || !ms5) return fail(TWOSD_E_ARG, "last_refresh_ms: NULL");
+    for (int i = 0; i < 5; ++i) ms5[i] = c->last_refresh_ms[i];
+    return TWOSD_OK;
+}
+
 
 // Two-level selection from training scenarios [first, first + count) of epigraph epi at x:
 // level 1 = pool[0, level1) (the most frequent bases); the candidates of a level-1 basis p are
@@ -851,12 +1125,17 @@ extern "C" int twosd_epigraph_info(twosd_ctx *c, int epi, int *ns, double *tw) {
 // kraw, e ascending) and the same as sliced ELL on the device (kslot pool-strided, absolute
 // into kix/kv).  The kernels multiply the scenario deltas by coef_e(x) (d_kcoef) themselves.
 static int prepare_elements(twosd_ctx *c) {
+    const auto t_pe0 = std::chrono::steady_clock::now();
     const int m = c->L.m, k = c->k;
     std::vector<std::vector<int>> bycol(m);   // random elements on each row
     for (int e = 0; e < k; ++e) bycol[c->pos_row[e]].push_back(e);
     std::vector<int> ks, ki;
     std::vector<double> kv;
-    for (PoolBasis &B : c->pool) {
+    const int P0 = (int)c->pool.size();
+    struct Up { std::vector<int> sl, ix; std::vector<double> vv; };
+    std::vector<Up> up(P0);
+    parallel_for(P0, [&](int p) {
+        PoolBasis &B = c->pool[p];
         B.kptr.assign(1, 0);
         B.ke.clear(); B.kraw.clear();
         std::vector<std::pair<int, double>> row;
@@ -868,20 +1147,29 @@ static int prepare_elements(twosd_ctx *c) {
             for (auto &ev : row) { B.ke.push_back(ev.first); B.kraw.push_back(ev.second); }
             B.kptr.push_back((int)B.ke.size());
         }
-        if (c->CH <= 0) continue;
-        std::vector<int> sl, ix;
-        std::vector<double> vv;
+        if (c->CH <= 0) return;
         build_ell(c->R, [&](int i, std::vector<std::pair<int, double>> &out) {
             if (i < m)
                 for (int q = B.kptr[i]; q < B.kptr[i + 1]; ++q) out.push_back({B.ke[q], B.kraw[q]});
-        }, sl, ix, vv);
-        const int eoff = (int)(ki.size() / 64);
-        for (int v : sl) ks.push_back(v + eoff);
-        ki.insert(ki.end(), ix.begin(), ix.end());
-        kv.insert(kv.end(), vv.begin(), vv.end());
+        }, up[p].sl, up[p].ix, up[p].vv);
+    });
+    if (c->CH > 0) {
+        std::vector<size_t> ko(P0 + 1, 0);
+        for (int p = 0; p < P0; ++p) ko[p + 1] = ko[p] + up[p].ix.size();
+        ks.resize((size_t)P0 * (c->R + 1));
+        ki.resize(ko[P0]);
+        kv.resize(ko[P0]);
+        parallel_for(P0, [&](int p) {
+            const int e0 = (int)(ko[p] / 64);
+            for (int t = 0; t <= c->R; ++t) ks[(size_t)p * (c->R + 1) + t] = up[p].sl[t] + e0;
+            std::copy(up[p].ix.begin(), up[p].ix.end(), ki.begin() + ko[p]);
+            std::copy(up[p].vv.begin(), up[p].vv.end(), kv.begin() + ko[p]);
+        });
     }
+    const auto t_pe1 = std::chrono::steady_clock::now();
     int rc;
     if (c->CH > 0 && ((rc = upload(&c->d_kslot, ks)) || (rc = upload(&c->d_kix, ki)) || (rc = upload(&c->d_kv, kv)))) return rc;
+    const auto t_pe2 = std::chrono::steady_clock::now();
     if (c->CH > 0 && c->pool.size() > 1) {
         // device selection-stream inputs: CSR rows of every basis, and a static record capacity
         // per basis (every row active: m row starts + all its entries)
@@ -915,6 +1203,11 @@ static int prepare_elements(twosd_ctx *c) {
         c->sel_cap_total = cap[P];
     }
     c->k_valid = true;
+    if (getenv("TWOSD_DEBUG")) {
+        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        fprintf(stderr, "prepare_elements P=%zu: build %.1f ms, upload ell %.1f ms (%zu entries), selection inputs %.1f ms\n",
+                c->pool.size(), ms(t_pe0, t_pe1), ms(t_pe1, t_pe2), ki.size(), ms(t_pe2, std::chrono::steady_clock::now()));
+    }
     return TWOSD_OK;
 }
 
@@ -1191,8 +1484,22 @@ static int select_pool(twosd_ctx *c, const double *d_dv, int N, int *d_pick, int
 // Launch the LP kernel over N scenarios whose deltas start at d_dv (device); results in
 // c->d_obj / d_pi / d_y / d_status / d_iters [0, N).
 int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool want_pi, bool want_y) {
+    LpRun o;
+    o.want_pi = want_pi;
+    o.want_y = want_y;
+    return run_lp_ex(c, x, d_dv, N, o);
+}
+
+// N = scenarios of d_dv addressed by the launch (outputs obj / status / iters / pool picks are
+// indexed by scenario); list mode solves only o.d_list[0, o.nlist) from their recorded picks
+// and writes pi at the list position
+int twosd::run_lp_ex(twosd_ctx *c, const double *x, const double *d_dv, int N, const LpRun &o) {
+    const bool want_pi = o.want_pi, want_y = o.want_y;
+    const bool list = o.d_list != nullptr;
+    const int NL = list ? o.nlist : N;   // scenarios this launch solves
     int rc;
     if ((rc = prepare_x(c, x))) return rc;
+    if (list && c->pool.size() > 1 && (size_t)N > c->pick_cap) return fail(TWOSD_E_STATE, "LP list mode: no recorded pool picks");
     const int m = c->L.m, n = c->L.n, MP = c->MP, R = c->R;
     if (N > c->out_cap) {
         size_t cap = std::max<size_t>(N, 1024);
@@ -1203,9 +1510,17 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
         c->pi_cap = c->y_cap = 0;
         c->out_cap = (int)cap;
     }
-    if (want_pi && (size_t)N > c->pi_cap) {
+    if (want_pi && (size_t)NL > c->pi_cap) {
         if ((rc = dalloc(&c->d_pi, (size_t)c->out_cap * m))) return rc;
         c->pi_cap = c->out_cap;
+    }
+    if (o.want_key && (size_t)N > c->vkey_cap) {
+        if ((rc = dalloc(&c->d_vkey, (size_t)c->out_cap))) return rc;
+        c->vkey_cap = c->out_cap;
+    }
+    if (o.want_bkey && (size_t)N > c->bkey_cap) {
+        if ((rc = dalloc(&c->d_bkey, (size_t)c->out_cap))) return rc;
+        c->bkey_cap = c->out_cap;
     }
     if (want_y && (size_t)N > c->y_cap) {
         if ((rc = dalloc(&c->d_y, (size_t)c->out_cap * n))) return rc;
@@ -1220,7 +1535,7 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
         int bpc = hyper_max_blocks_per_cu(R, CH, n + m, kmax, c->k);
         if (const char *e = getenv("TWOSD_BPC")) bpc = std::min(bpc, std::max(1, atoi(e)));   // diagnostics: occupancy sweep
         if (bpc < 1) return fail(TWOSD_E_UNSUPPORTED, "LP kernel: LDS slice too large (m = %d, k = %d)", m, c->k);
-        const int nblocks = std::max(1, std::min((N + kWavesPerBlock - 1) / kWavesPerBlock, bpc * c->num_cus));
+        const int nblocks = std::max(1, std::min((NL + kWavesPerBlock - 1) / kWavesPerBlock, bpc * c->num_cus));
         const size_t slots = (size_t)nblocks * kWavesPerBlock;
         if (slots > c->earena_slots || ecap != c->earena_cap) {
             if ((rc = dalloc(&c->d_eidx, slots * ecap)) || (rc = dalloc(&c->d_evals, slots * ecap))) return rc;
@@ -1229,7 +1544,7 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
         }
         HIPCHK(hipMemsetAsync(c->d_queue, 0, sizeof(int) * kMaxQueueGroups * kQueueStride, c->stream));
         HyperParams H{};
-        H.m = m; H.n = n; H.k = c->k; H.N = N; H.kmax = kmax; H.ecap = ecap;
+        H.m = m; H.n = n; H.k = c->k; H.N = NL; H.kmax = kmax; H.ecap = ecap;
         H.colptr = c->d_colptr; H.rowidx = c->d_rowidx; H.val = c->d_val; H.q = c->d_q; H.btype = c->d_btype;
         H.wr_width = c->wr_width; H.wr_col = c->d_wr_col; H.wr_val = c->d_wr_val;
         H.wr_ocol = c->d_wr_ocol; H.wr_oval = c->d_wr_oval;
@@ -1242,6 +1557,33 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
         H.qgroups = std::max(1, std::min(16, nblocks));   // two ranges per XCD (8 / 16 / 32 / 64: 143.6 / 142.7 / 142.8 / 146.3 ms, storm 1M)
         if (const char *e = getenv("TWOSD_QGROUPS")) H.qgroups = std::max(1, std::min({kMaxQueueGroups, nblocks, atoi(e)}));   // A/B knob
         H.obj = c->d_obj; H.pi = want_pi ? c->d_pi : nullptr; H.y = want_y ? c->d_y : nullptr;
+        H.vkey = o.want_key ? c->d_vkey : nullptr;
+        H.bkey = o.want_bkey ? c->d_bkey : nullptr;
+        if (list && o.want_etas) {
+            if ((size_t)NL > c->eo_rows || c->eo_kmax != kmax) {
+                const size_t rows = std::max<size_t>(NL, 256);
+                if ((rc = dalloc(&c->d_eo_pb, rows)) || (rc = dalloc(&c->d_eo_K, rows)) || (rc = dalloc(&c->d_eo_off, rows)) ||
+                    (rc = dalloc(&c->d_eo_etap, rows * kmax)) || (rc = dalloc(&c->d_eo_etaoff, rows * (kmax + 1))) ||
+                    (rc = dalloc(&c->d_eo_eidx, rows * 4096)) || (rc = dalloc(&c->d_eo_evals, rows * 4096)))
+                    return rc;
+                if (!c->d_eo_used && (rc = dalloc(&c->d_eo_used, 1))) return rc;
+                c->eo_rows = rows;
+                c->eo_cap = rows * 4096;
+                c->eo_kmax = kmax;
+            }
+            HIPCHK(hipMemsetAsync(c->d_eo_used, 0, sizeof(int), c->stream));
+            H.eo_pb = c->d_eo_pb; H.eo_K = c->d_eo_K; H.eo_off = c->d_eo_off; H.eo_etap = c->d_eo_etap;
+            H.eo_etaoff = c->d_eo_etaoff; H.eo_eidx = c->d_eo_eidx; H.eo_evals = c->d_eo_evals; H.eo_used = c->d_eo_used;
+            H.eo_cap = (int)std::min<size_t>(c->eo_cap, INT32_MAX);
+        }
+        if (list && o.want_head) {
+            if ((size_t)NL > c->head_cap) {
+                if ((rc = dalloc(&c->d_head_out, (size_t)NL * m))) return rc;
+                c->head_cap = NL;
+            }
+            H.head_out = c->d_head_out;
+        }
+        H.pi_by_pos = list ? 1 : 0;
         H.status = c->d_status; H.iters = c->d_iters; H.ops = c->d_ops;
         if (!c->d_stamps) {
             if ((rc = dalloc(&c->d_stamps, 16))) return rc;
@@ -1250,7 +1592,7 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
         H.stamps = c->d_stamps;
         H.npool = (int)c->pool.size();
         H.bnnz = c->d_bnnz;
-        if (c->want_head) {
+        if (c->want_head && !list) {
             if ((size_t)N > c->head_cap) {
                 if ((rc = dalloc(&c->d_head_out, (size_t)N * m))) return rc;
                 c->head_cap = N;
@@ -1258,14 +1600,16 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
             H.head_out = c->d_head_out;
         }
         if (H.npool > 1) {
-            if ((size_t)N > c->pick_cap) {
+            if (!list && (size_t)N > c->pick_cap) {
                 if ((rc = dalloc(&c->d_pool_pick, (size_t)N))) return rc;
                 c->pick_cap = N;
             }
             H.pool_pick = c->d_pool_pick;
         }
         HIPCHK(hipEventRecord(c->ev[0], c->stream));
-        if (H.npool > 1) {
+        if (list) {
+            H.order = o.d_list;
+        } else if (H.npool > 1) {
             if ((rc = select_pool(c, d_dv, N, c->d_pool_pick, 0))) return rc;
             H.order = c->d_order;
         }
@@ -1278,6 +1622,7 @@ int twosd::run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool
         hipEventElapsedTime(&ms_sel, c->ev[0], c->ev[2]);
         c->t_us[0] = 1e3 * ms;
         c->t_us[4] = 1e3 * ms_sel;
+        if (list) return TWOSD_OK;
         c->last_lp_N = N;
         c->last_lp_blocks = nblocks;
         c->last_ops_width = 1;
@@ -1406,17 +1751,62 @@ extern "C" int twosd_solve_push(twosd_ctx *c, int epi, const double *x, int firs
     if (c->n1 > 0 && !x) return fail(TWOSD_E_ARG, "solve_push: x is NULL");
     if (count == 0) { if (new_size) *new_size = c->dvs.size; return TWOSD_OK; }
     HIPCHK(hipSetDevice(c->device));
-    int rc = run_lp(c, x, E.d_dv + (size_t)first * c->k, count, true, false);
+    const double *d_dv = E.d_dv + (size_t)first * c->k;
+    // TWOSD_PUSH_ALL=1: recover and push the dual of every scenario (the pre-key path, kept for
+    // the equivalence test); default: vertex keys, first occurrences, re-solve of those only
+    const bool all = getenv("TWOSD_PUSH_ALL") && atoi(getenv("TWOSD_PUSH_ALL")) != 0;
+    LpRun o;
+    o.want_pi = all;
+    o.want_key = !all;
+    int rc = run_lp_ex(c, x, d_dv, count, o);
     if (rc) return rc;
+    const double t_lp = c->t_us[0], t_sel = c->t_us[4];
     rc = copy_lp_outputs(c, count, obj, nullptr, nullptr, status);
     if (rc) return rc;   // some LP not optimal: nothing pushed
-    HIPCHK(hipEventRecord(c->ev[2], c->stream));
-    if ((rc = dvs_push_device(c, count, c->d_pi, nullptr))) return rc;
-    HIPCHK(hipEventRecord(c->ev[3], c->stream));
-    HIPCHK(hipEventSynchronize(c->ev[3]));
-    float ms = 0;
-    hipEventElapsedTime(&ms, c->ev[2], c->ev[3]);
-    c->t_us[1] = 1e3 * ms;
+    const int64_t piv_sum = c->last_pivots_sum, ops_sum = c->last_ops_sum;
+    const int piv_max = c->last_pivots_max;
+    float ms = 0, ms_key = 0;
+    if (all) {
+        HIPCHK(hipEventRecord(c->ev[2], c->stream));
+        if ((rc = dvs_push_device(c, count, c->d_pi, nullptr))) return rc;
+        HIPCHK(hipEventRecord(c->ev[3], c->stream));
+        HIPCHK(hipEventSynchronize(c->ev[3]));
+        hipEventElapsedTime(&ms, c->ev[2], c->ev[3]);
+        c->last_push_reps = count;
+    } else {
+        HIPCHK(hipEventRecord(c->ev[5], c->stream));
+        const int *d_list = nullptr;
+        int U = 0;
+        if ((rc = vkey_first_occurrences(c, count, c->d_vkey, c->d_status, &d_list, &U))) return rc;
+        HIPCHK(hipEventRecord(c->ev[6], c->stream));
+        HIPCHK(hipEventSynchronize(c->ev[6]));
+        hipEventElapsedTime(&ms_key, c->ev[5], c->ev[6]);
+        c->last_push_reps = U;
+        if (U > 0) {
+            LpRun r;
+            r.want_pi = true;
+            r.d_list = d_list;
+            r.nlist = U;
+            if ((rc = run_lp_ex(c, x, d_dv, count, r))) return rc;
+            c->t_us[0] += t_lp;   // LP kernel time of the batch: main pass + representatives
+            HIPCHK(hipEventRecord(c->ev[2], c->stream));
+            if ((rc = dvs_push_device(c, U, c->d_pi, nullptr))) return rc;
+            HIPCHK(hipEventRecord(c->ev[3], c->stream));
+            HIPCHK(hipEventSynchronize(c->ev[3]));
+            hipEventElapsedTime(&ms, c->ev[2], c->ev[3]);
+        } else {
+            c->t_us[0] = t_lp;
+        }
+        c->t_us[4] = t_sel;
+        c->last_pivots_sum = piv_sum; c->last_ops_sum = ops_sum; c->last_pivots_max = piv_max;
+    }
+    c->t_us[1] = 1e3 * (ms + ms_key);
     if (new_size) *new_size = c->dvs.size;
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_last_push_reps(twosd_ctx *c, int *reps) {
+    if (!c || !reps) return fail(TWOSD_E_ARG, "last_push_reps: NULL");
+    *reps = c->last_push_reps;
     return TWOSD_OK;
 }

@@ -29,6 +29,7 @@ namespace twosd {
 #define HTOL_PIV 1e-9
 #define HPI_ZERO 1e-12
 
+
 // Diagnostic build (-DTWOSD_STAMPS, libtwosd_hip_stamps.so): per-phase s_memtime cycle
 // totals summed over waves.  Never used for timing claims (stamps perturb the schedule).
 #ifdef TWOSD_STAMPS
@@ -189,6 +190,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             }
         }
         if (s < 0) break;
+        const int qpos = s;
         if (P.order) s = __builtin_amdgcn_readfirstlane(P.order[s]);   // grouped by pool basis
 
         const double *dvs = P.dv + (size_t)s * P.k;
@@ -392,9 +394,10 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                     const int c = c0 + u;
                     if (c >= C) break;
                     const uint64_t bit = 1ull << c;
-                    if ((bmask | fixedm) & bit) continue;
+                    if (bmask & bit) continue;
                     const double a = sg * av[u];
-                    if (a != 0.0) nzm |= bit;
+                    if (a != 0.0) nzm |= bit;   // fixed columns too: their d_j (slack: -pi_i) stay current
+                    if (fixedm & bit) continue;
                     const bool atlb = !(ubm & bit);
                     if (atlb ? a > HTOL_PIV : a < -HTOL_PIV) {
                         elm |= bit;
@@ -588,9 +591,50 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         pb = 0;
         }   // attempt
 
-        // ---- vertex recovery: pi = c_B' B^{-1}
+        // ---- objective, dual-vertex key, vertex recovery pi = c_B' B^{-1}
         double objv = NAN;
         if (status == TWOSD_LP_OPTIMAL) {
+            double ob = 0.0;
+#pragma unroll
+            for (int t = 0; t < R; ++t) {
+                const int j = hb[t] >> 2;
+                if (hb[t] >= 0 && j < n) ob = fma(P.q[j], xB[t], ob);
+            }
+            objv = wsum(ob);
+            if (P.vkey) {
+                // key of the dual: pi_i = -d_{n+i} is the reduced cost of row i's slack, kept
+                // current in registers by every pivot (fixed E-row slacks included).  Components
+                // at or below 1e-9 (1 + max) are snapped to zero and the rest rounded to 24
+                // significant bits; the key is the order-independent sum of mix64(row, bits).
+                // Scenarios with equal keys have duals equal to ~2^-23 relative -- the same vertex
+                // up to rounding noise, so their exactly recovered pi push as equal vectors
+                // (16-bit rule, dual_set.jl:24-53).  A vertex split over two keys only costs one
+                // more re-solved representative; the push dedup still merges it.
+                double pm = 0.0;
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    const int j = 64 * c + lane;
+                    if (j >= n && j < ncol) pm = fmax(pm, fabs(d[c]));
+                }
+                pm = wmax(pm);
+                const double zt = 1e-9 * (1.0 + pm);
+                unsigned long long h = 0;
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    const int j = 64 * c + lane;
+                    if (j >= n && j < ncol) {
+                        const double v = fabs(d[c]) <= zt ? 0.0 : d[c];
+                        // sign, exponent and 23 mantissa bits (35 bits) next to the row (< 2^24)
+                        const unsigned long long b = ((unsigned long long)__double_as_longlong(v) + (1ull << 28)) >> 29;
+                        h += mix64(((unsigned long long)(j - n) << 35) | b);
+                    }
+                }
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o);
+                if (lane == 0) P.vkey[s] = h;
+            }
+        }
+        if (status == TWOSD_LP_OPTIMAL && (P.pi || P.y || !P.vkey)) {
 #pragma unroll
             for (int t = 0; t < R; ++t) {
                 const int j = hb[t] >> 2;
@@ -623,19 +667,14 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             nops += P.bnnz[pb];
             pmax = wmax(pmax);
             const double zt = HPI_ZERO * (1.0 + pmax);
-            double ob = 0.0;
 #pragma unroll
-            for (int t = 0; t < R; ++t) {
+            for (int t = 0; t < R; ++t)
                 if (fabs(pv[t]) <= zt) pv[t] = 0.0;
-                const int j = hb[t] >> 2;
-                if (hb[t] >= 0 && j < n) ob = fma(P.q[j], xB[t], ob);
-            }
-            objv = wsum(ob);
             h_wave_sync();
 #pragma unroll
             for (int t = 0; t < R; ++t) ut[64 * t + lane] = 0.0;
             if (P.pi) {
-                double *po = P.pi + (size_t)s * m;
+                double *po = P.pi + (size_t)(P.pi_by_pos ? qpos : s) * m;
 #pragma unroll
                 for (int t = 0; t < R; ++t)
                     if (64 * t + lane < m) po[64 * t + lane] = pv[t];
@@ -651,16 +690,45 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                     if (hb[t] >= 0 && j < n) yo[j] = xB[t];
                 }
             }
-        } else if (P.pi) {
-            double *po = P.pi + (size_t)s * m;
+        } else if (status != TWOSD_LP_OPTIMAL && P.pi) {
+            double *po = P.pi + (size_t)(P.pi_by_pos ? qpos : s) * m;
 #pragma unroll
             for (int t = 0; t < R; ++t)
                 if (64 * t + lane < m) po[64 * t + lane] = NAN;
         }
         if (P.head_out) {
+            const size_t ho = (size_t)(P.pi_by_pos ? qpos : s) * m;
 #pragma unroll
             for (int t = 0; t < R; ++t)
-                if (64 * t + lane < m) P.head_out[(size_t)s * m + 64 * t + lane] = hb[t] >> 2;
+                if (64 * t + lane < m) P.head_out[ho + 64 * t + lane] = hb[t] >> 2;
+        }
+        if (P.bkey && status == TWOSD_LP_OPTIMAL) {   // the set of basic columns, order-independent
+            unsigned long long h = 0;
+#pragma unroll
+            for (int t = 0; t < R; ++t)
+                if (64 * t + lane < m) h += mix64((unsigned long long)(hb[t] >> 2));
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o);
+            if (lane == 0) P.bkey[s] = h;
+        }
+        if (P.eo_K) {   // eta file of the solve (pool refresh composes B^{-1} = E_K..E_1 B_pb^{-1} from it)
+            int off = 0;
+            if (lane == 0 && status == TWOSD_LP_OPTIMAL) off = atomicAdd(P.eo_used, eoff);
+            off = __builtin_amdgcn_readfirstlane(__shfl(off, 0));
+            const bool ok = status == TWOSD_LP_OPTIMAL && off + eoff <= P.eo_cap;
+            if (ok) {
+                for (int e = lane; e < eoff; e += 64) {
+                    P.eo_eidx[off + e] = eidx[e];
+                    P.eo_evals[off + e] = evals[e];
+                }
+                for (int t = lane; t < K; t += 64) P.eo_etap[(size_t)qpos * P.kmax + t] = etap[t];
+                for (int t = lane; t <= K; t += 64) P.eo_etaoff[(size_t)qpos * (P.kmax + 1) + t] = etaoff[t];
+            }
+            if (lane == 0) {
+                P.eo_K[qpos] = ok ? K : -1;
+                P.eo_off[qpos] = off;
+                P.eo_pb[qpos] = pb;
+            }
         }
         if (lane == 0) {
             P.obj[s] = objv;

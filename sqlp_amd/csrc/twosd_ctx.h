@@ -129,6 +129,18 @@ struct twosd_ctx {
     void *dvs_ws = nullptr;       // dvs scratch (dvs_kernel.hip)
     // cut workspace (cut_kernel.hip)
     void *cut_ws = nullptr;
+    // dual-vertex key workspace (vkey.hip) and the key output of the LP kernel
+    void *vkey_ws = nullptr;
+    unsigned long long *d_vkey = nullptr, *d_bkey = nullptr;
+    size_t vkey_cap = 0, bkey_cap = 0;
+    // eta-file output of a pool refresh (list positions x kmax / kmax + 1, shared entry arena)
+    int *d_eo_pb = nullptr, *d_eo_K = nullptr, *d_eo_off = nullptr, *d_eo_etap = nullptr, *d_eo_etaoff = nullptr;
+    int *d_eo_eidx = nullptr, *d_eo_used = nullptr;
+    double *d_eo_evals = nullptr;
+    size_t eo_rows = 0, eo_cap = 0;
+    int eo_kmax = 0;
+    double last_refresh_ms[5] = {0, 0, 0, 0, 0};   // train solves, re-solves, compose, upload, total
+    int last_push_reps = 0;       // representatives re-solved by the last solve_push
 };
 
 namespace twosd {
@@ -137,6 +149,21 @@ template <typename T>
 int dgrow(T **p, size_t *cap, size_t count, size_t keep, hipStream_t s);
 int prepare_x(twosd_ctx *c, const double *x);
 int run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool want_pi, bool want_y);
+// options of run_lp_ex: vertex keys instead of pi (solve_push), or a list of scenarios to
+// re-solve from their recorded pool picks with pi at the list position
+struct LpRun {
+    bool want_pi = false, want_y = false, want_key = false;
+    bool want_bkey = false;       // basis keys into c->d_bkey
+    bool want_etas = false;       // list mode: eta files into c->eo (pool refresh)
+    bool want_head = false;       // list mode: final heads by list position into c->d_head_out
+    const int *d_list = nullptr;  // list mode: scenarios (indices into d_dv) to solve, no selection
+    int nlist = 0;
+};
+int run_lp_ex(twosd_ctx *c, const double *x, const double *d_dv, int N, const LpRun &o);
+// vkey.hip
+int vkey_first_occurrences(twosd_ctx *c, int N, const unsigned long long *d_vkey, const int *d_status, const int **d_list,
+                           int *U, const int **d_counts = nullptr);
+void vkey_free(twosd_ctx *c);
 // dual vertex set (dvs_kernel.hip)
 int dvs_init(twosd_ctx *c);
 void dvs_free(twosd_ctx *c);

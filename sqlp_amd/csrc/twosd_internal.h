@@ -56,7 +56,28 @@ struct HyperParams {
     int *head_out;                                      // N x m final basis (nullable)
     int *pool_pick;                                     // N pool basis per scenario (in; npool > 1)
     const int *order;                                   // N visiting order of the scenarios (nullable)
+    // dual key mode (solve_push): per scenario a 64-bit key of its optimal dual (from the
+    // maintained slack reduced costs, 24 significant bits); with pi == y == nullptr the vertex
+    // recovery is skipped
+    unsigned long long *vkey;                           // N (nullable)
+    int pi_by_pos;                                      // pi / head row = queue position instead of scenario
+    // basis key (pool refresh): sum of mix64(j) over the basic columns of the optimal basis
+    unsigned long long *bkey;                           // N (nullable)
+    // eta-file output (pool refresh, list mode): per list position the start pool basis, the
+    // pivot count (-1: did not fit), the pivot rows and offsets (kmax / kmax + 1 per position)
+    // and the eta entries, appended at an atomically claimed offset of a shared arena
+    int *eo_pb, *eo_K, *eo_off, *eo_etap, *eo_etaoff;   // nullable (eo_K == nullptr: off)
+    int *eo_eidx; double *eo_evals;
+    int *eo_used; int eo_cap;
 };
+
+// splitmix64 finalizer (basis keys: host and device must agree)
+__host__ __device__ inline unsigned long long mix64(unsigned long long z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
 
 // warm-start selection over the basis pool (pool_select_kernel in lp_hyper.hip)
 struct PoolSelParams {

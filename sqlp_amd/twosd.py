@@ -154,6 +154,19 @@ class SDContext:
         """Drop the per-x cache (next solve / cut recomputes it; results unchanged)."""
         check(self.lib.twosd_invalidate_x(self.h))
 
+    def pool_refresh(self, epi, x, first, count, max_pool) -> int:
+        """Replace the warm-start pool by the primary basis plus the max_pool - 1 most frequent
+        optimal bases of training scenarios [first, first+count) of epi at x (twosd_pool_refresh)."""
+        n = C.c_int()
+        check(self.lib.twosd_pool_refresh(self.h, epi.index, ptr(_f64(x)), first, count, max_pool, C.byref(n)))
+        return n.value
+
+    def last_refresh_ms(self):
+        """[training solves, re-solves, host composition, upload, total] of the last refresh."""
+        out = np.zeros(5)
+        check(self.lib.twosd_last_refresh_ms(self.h, ptr(out)))
+        return out
+
     def pool_size(self) -> int:
         n = C.c_int(0)
         check(self.lib.twosd_pool_size(self.h, C.byref(n)))
@@ -207,6 +220,13 @@ class SDContext:
         mx = C.c_int()
         check(self.lib.twosd_last_lp_stats(self.h, C.byref(s), C.byref(mx)))
         return s.value, mx.value
+
+    def last_push_reps(self) -> int:
+        """Scenarios whose dual the last solve_push recovered and pushed (first scenario of
+        each distinct optimal dual vertex of the batch)."""
+        r = C.c_int()
+        check(self.lib.twosd_last_push_reps(self.h, C.byref(r)))
+        return r.value
 
     def lp_flops(self):
         """Counted fp64 FLOPs of the last LP batch (2 * row width per executed row op)."""

@@ -1,0 +1,81 @@
+"""twosd_pool_refresh: the warm-start pool rebuilt at a new first-stage point from the optimal
+bases of training scenarios there, with B^{-1} composed from the eta files of their solves.
+The pool only changes where each scenario starts: objectives must equal those from the
+primary basis (the LP optimum is unique), every scenario stays optimal, and pivots drop."""
+import numpy as np
+import pytest
+
+from tests import instances as I
+
+pytestmark = pytest.mark.gpu
+
+
+def _sd_x(n_iter=3):
+    from sqlp_amd import master, smps, twosd
+    inst = I.load("storm")
+    sp1 = smps.get_smps_stage_template(inst["cor"], inst["tim"], 1)
+    c2 = twosd.SDContext(inst["sp2"], inst["sto"])
+    x0 = I.x_ev("storm")
+    c2.compute_basis(x0, smps.mean_values(inst["sto"]))
+    cell = master.sdCell(sp1, c2)
+    cell.bind_epigraph(twosd.sdEpigraph(c2, 1.0, 0.0))
+    cell.x_candidate = x0.copy()
+    cell.x_incumbent = x0.copy()
+    for it in range(n_iter):
+        master.sd_iteration(cell, [I.sample("storm", 1, 70 + it)[0]])
+    return cell.x_candidate.copy()
+
+
+def test_pool_refresh_storm():
+    from sqlp_amd import smps, twosd
+    inst = I.load("storm")
+    x_ev = I.x_ev("storm")
+    x2 = _sd_x()
+    assert np.linalg.norm(x2 - x_ev) > 1e-3 * np.linalg.norm(x_ev)
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    ctx.compute_basis(x_ev, smps.mean_values(inst["sto"]))
+    tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(tr, I.sample("storm", 4096, seed=21))
+    ctx.pool_build(tr, x_ev, 0, 4096, 256)
+    ev = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    vals = I.sample("storm", 3000, seed=22)
+    twosd.add_scenarios(ev, vals)
+    ref = twosd.SDContext(inst["sp2"], inst["sto"])          # primary basis only
+    ref.compute_basis(x_ev, smps.mean_values(inst["sto"]))
+    o_ref, _, _, st_ref = ref.solve_values(x2, vals, want_pi=False)
+    assert (st_ref == 0).all()
+    o_old, _, _, st_old = twosd.solve_batch(ev, x2, 0, len(vals), want_pi=False)
+    piv_old = ctx.lp_stats()[0]
+    head0 = ctx.get_basis()
+    P = ctx.pool_refresh(tr, x2, 0, 4096, 512)
+    assert 1 < P <= 512
+    np.testing.assert_array_equal(ctx.pool_get(0), head0)     # the primary basis stays pool[0]
+    ms = ctx.last_refresh_ms()
+    assert (ms >= 0).all() and ms[4] > 0
+    o_new, _, _, st_new = twosd.solve_batch(ev, x2, 0, len(vals), want_pi=False)
+    piv_new = ctx.lp_stats()[0]
+    assert (st_new == 0).all()
+    np.testing.assert_allclose(o_new, o_ref, rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(o_old, o_ref, rtol=1e-9, atol=1e-9)
+    assert piv_new < piv_old
+    # duals of the refreshed starts satisfy strong duality (vertex recovery through the composed B^{-1})
+    o2, _, pi, st2 = twosd.solve_batch(ev, x2, 0, 256, want_pi=True)
+    sp = inst["osp2"]
+    b = np.tile(sp.r - sp.T @ x2, (256, 1))
+    b[:, ctx.rows] += vals[:256] - sp.r[ctx.rows]
+    np.testing.assert_allclose(np.einsum("ij,ij->i", pi, b), o2, rtol=1e-9, atol=1e-6)
+    print(f"pivots/scenario {piv_old / len(vals):.2f} -> {piv_new / len(vals):.2f}, pool {P}, refresh ms {ms}")
+
+
+def test_pool_refresh_bad_args():
+    from sqlp_amd import smps, twosd
+    from sqlp_amd._lib import TwoSDError
+    inst = I.load("lands")
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    x = I.x_ev("lands")
+    ctx.compute_basis(x, smps.mean_values(inst["sto"]))
+    tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(tr, I.sample("lands", 64, seed=1))
+    with pytest.raises(TwoSDError):
+        ctx.pool_refresh(tr, x, 0, 65, 8)
+    assert ctx.pool_refresh(tr, x, 0, 64, 8) <= 8

@@ -1,0 +1,72 @@
+"""solve_push by dual-vertex keys (vkey.hip) == pushing every scenario's dual.
+
+push!(V, pi_s) for s = 0..N-1 (dual_set.jl:84-94) only appends the first scenario's dual of
+each distinct vertex.  The default twosd_solve_push therefore solves the batch without
+recovering pi, keys each optimal dual vertex by its tight dual constraints, and re-solves
+only the first scenario of every key to push its pi.  TWOSD_PUSH_ALL=1 runs the direct path
+(pi of every scenario pushed in order, device dedup with the reference rule).  Both must give
+the identical ordered vertex set (bit for bit) and identical objectives."""
+import numpy as np
+import pytest
+
+from tests import instances as I
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name,N,pool", [("lands", 3000, 1), ("transship", 6000, 1), ("ssn", 12000, 1),
+                                         ("storm", 12000, 1), ("storm", 30000, 512)])
+def test_keyed_push_equals_push_all(name, N, pool, monkeypatch):
+    from sqlp_amd import smps, twosd
+    inst = I.load(name)
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    x = I.x_ev(name)
+    ctx.compute_basis(x, smps.mean_values(inst["sto"]))
+    if pool > 1:
+        tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+        twosd.add_scenarios(tr, I.sample(name, 4 * pool, seed=5))
+        ctx.pool_build(tr, x, 0, 4 * pool, pool)
+    epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(epi, I.sample(name, N, seed=17))
+    V = twosd.sdDualVertexSet(ctx)
+    half = N // 2
+    runs = []
+    for mode in ("1", None):
+        if mode:
+            monkeypatch.setenv("TWOSD_PUSH_ALL", mode)
+        else:
+            monkeypatch.delenv("TWOSD_PUSH_ALL", raising=False)
+        V.clear()
+        objs, reps = [], []
+        for lo, hi in ((0, half), (half, N)):          # two batches: the second meets a non-empty V
+            obj, st, _ = twosd.solve_push(epi, x, lo, hi - lo)
+            assert (st == 0).all()
+            objs.append(obj)
+            reps.append(ctx.last_push_reps())
+        runs.append((np.concatenate(objs), V.matrix(), reps))
+    (o_all, V_all, r_all), (o_key, V_key, r_key) = runs
+    np.testing.assert_array_equal(o_all, o_key)
+    assert V_all.shape == V_key.shape
+    np.testing.assert_array_equal(V_all, V_key)
+    assert r_all == [half, N - half]
+    assert all(r <= c for r, c in zip(r_key, (half, N - half)))
+    print(f"{name}: N={N} |V|={len(V_key)} representatives re-solved {r_key}")
+
+
+def test_keyed_push_nonoptimal_refused():
+    """A batch with a non-optimal scenario pushes nothing on the keyed path (as on the direct
+    one): TWOSD_E_LP, V unchanged."""
+    from sqlp_amd import smps, twosd
+    from sqlp_amd._lib import TwoSDError
+    inst = I.load("lands")
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    x = I.x_ev("lands")
+    ctx.compute_basis(x, smps.mean_values(inst["sto"]))
+    epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(epi, np.array([[5.0], [3.0], [1000.0], [7.0]]))
+    V = twosd.sdDualVertexSet(ctx)
+    with pytest.raises(TwoSDError):
+        twosd.solve_push(epi, x, 0, 4)
+    assert len(V) == 0
+    twosd.solve_push(epi, x, 0, 2)
+    assert len(V) >= 1 and ctx.last_push_reps() <= 2
