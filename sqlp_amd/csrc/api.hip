@@ -162,14 +162,14 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_xbase); dfree(c->d_queue); dfree(c->d_lpstats);
     dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_ops);
     dfree(c->d_dvtmp);
-    dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); dfree(c->d_head_out); dfree(c->d_pool_pick); dfree(c->d_order); dfree(c->d_sort_tmp);
+    dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); c->sel_code_cap = 0; dfree(c->d_head_out); dfree(c->d_pool_pick); dfree(c->d_order); dfree(c->d_sort_tmp);
     dfree(c->d_cand); dfree(c->d_sel_key); c->key_cap = 0; c->pool_l1 = c->pool_ncand = 0; c->order_cap = 0; c->sort_tmp_bytes = 0; c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
     dfree(c->d_dist_kind); dfree(c->d_dist_off); dfree(c->d_dist_val); dfree(c->d_dist_prob); dfree(c->d_dist_p0);
     dfree(c->d_dist_p1); dfree(c->d_dist_tmpl); c->has_dist = false;
     dfree(c->d_kslot); dfree(c->d_kix); dfree(c->d_kv); dfree(c->d_kcoef); c->k_valid = false;
     dfree(c->d_sel_end); dfree(c->d_kp); dfree(c->d_ke); dfree(c->d_kraw); dfree(c->d_xaux); c->xaux_cap = 0; c->sel_cap_total = 0;
     dfree(c->d_d0); dfree(c->d_eidx); dfree(c->d_evals); dfree(c->d_stamps);
-    dfree(c->d_wr_col); dfree(c->d_wr_val); dfree(c->d_wr_ocol); dfree(c->d_wr_oval); dfree(c->d_bslot); dfree(c->d_bix); dfree(c->d_bv);
+    dfree(c->d_wr_col); dfree(c->d_wr_val); dfree(c->d_wr_ocol); dfree(c->d_wr_oval); dfree(c->d_bcp); dfree(c->d_bci); dfree(c->d_bcv);
     dfree(c->d_brptr); dfree(c->d_brcol); dfree(c->d_brval);
     c->earena_slots = 0; c->earena_cap = 0;
     for (auto &e : c->epis) { dfree(e.d_dv); dfree(e.d_w); }
@@ -383,7 +383,7 @@ static int make_pool_basis(twosd_ctx *c, const std::vector<int> &head, PoolBasis
 
 // Upload the hypersparse-kernel form of every pool basis, pool-strided (pool[0] first, so
 // the leading MP / 64 / 64C entries are the primary basis): hb0 (MP), basic0 (64),
-// d0 (64C), B^{-1} columns as sliced ELL (bslot absolute into the concatenated bix/bv),
+// d0 (64C), B^{-1} columns as CSC (bcp absolute into the concatenated bci/bcv),
 // B^{-1} rows as CSR (brptr absolute into the concatenated brcol/brval).
 static int upload_pool(twosd_ctx *c) {
     const auto t_up0 = std::chrono::steady_clock::now();
@@ -393,9 +393,17 @@ static int upload_pool(twosd_ctx *c) {
     HIPCHK(hipMemcpy(bt.data(), c->d_btype, n + m, hipMemcpyDeviceToHost));
     std::vector<int> hb((size_t)P * MP, -1), bnnz(P, 0);
     std::vector<uint64_t> basic((size_t)P * 64, 0);
-    struct Up { std::vector<int> bs, bi; std::vector<double> bv; };
-    std::vector<Up> up(c->CH > 0 ? P : 0);
-    std::vector<double> d0_all(c->CH > 0 ? (size_t)P * 64 * c->CH : 0, 0.0);
+    // B^{-1} of every basis by rows (CSR) and by columns (CSC, rows ascending), both at the same
+    // per-basis offset ro[p]; offsets are known up front, so every basis fills its part of the
+    // concatenated arrays directly (default-initialised buffers, first touch in parallel)
+    std::vector<size_t> ro(P + 1, 0);
+    for (int p = 0; p < P; ++p) ro[p + 1] = ro[p] + c->pool[p].rcol.size();
+    if (ro[P] > INT32_MAX) return fail(TWOSD_E_UNSUPPORTED, "basis pool too large (> 2^31 entries)");
+    const size_t nz = std::max<size_t>(ro[P], 1);
+    std::vector<int> rp_all((size_t)P * (MP + 1)), cp_all((size_t)P * (MP + 1));
+    std::unique_ptr<int[]> rc_all(new int[nz]), ci_all(new int[nz]);
+    std::unique_ptr<double[]> rv_all(new double[nz]), cv_all(new double[nz]);
+    std::unique_ptr<double[]> d0_all(c->CH > 0 ? new double[(size_t)P * 64 * c->CH] : nullptr);
     parallel_for(P, [&](int p) {
         const PoolBasis &B = c->pool[p];
         std::vector<char> isb(n + m, 0);
@@ -405,65 +413,48 @@ static int upload_pool(twosd_ctx *c) {
             isb[B.head[i]] = 1;
         }
         bnnz[p] = (int)B.rcol.size();
+        const int base = (int)ro[p];
+        for (int i = 0; i <= MP; ++i) rp_all[(size_t)p * (MP + 1) + i] = base + B.rptr[std::min(i, m)];
+        std::copy(B.rcol.begin(), B.rcol.end(), rc_all.get() + base);
+        std::copy(B.rval.begin(), B.rval.end(), rv_all.get() + base);
+        // columns: counting sort of the row CSR (rows ascending within a column)
+        std::vector<int> pos(m + 1, 0);
+        for (int cc : B.rcol) ++pos[cc + 1];
+        for (int cc = 0; cc < m; ++cc) pos[cc + 1] += pos[cc];
+        for (int cc = 0; cc <= MP; ++cc) cp_all[(size_t)p * (MP + 1) + cc] = base + pos[std::min(cc, m)];
+        for (int i = 0; i < m; ++i)
+            for (int q = B.rptr[i]; q < B.rptr[i + 1]; ++q) {
+                const int at = base + pos[B.rcol[q]]++;
+                ci_all[at] = i;
+                cv_all[at] = B.rval[q];
+            }
         if (c->CH <= 0) return;
-        double *d0 = d0_all.data() + (size_t)p * 64 * c->CH;
-        for (int j = 0; j < n + m; ++j) {
-            if (isb[j]) continue;
+        double *d0 = d0_all.get() + (size_t)p * 64 * c->CH;
+        for (int j = 0; j < 64 * c->CH; ++j) {
+            if (j >= n + m || isb[j]) { d0[j] = 0.0; continue; }
             double sum = 0.0;
             if (j >= n) sum = B.pi0[j - n];
             else
                 for (int q = L.colptr[j]; q < L.colptr[j + 1]; ++q) sum += B.pi0[L.rowidx[q]] * L.val[q];
             d0[j] = (j < n ? L.q[j] : 0.0) - sum;
         }
-        // columns of B^{-1} (CSC from the row CSR; rows ascending within a column)
-        std::vector<std::vector<std::pair<int, double>>> cols(m);
-        for (int i = 0; i < m; ++i)
-            for (int q = B.rptr[i]; q < B.rptr[i + 1]; ++q) cols[B.rcol[q]].push_back({i, B.rval[q]});
-        build_ell(c->R, [&](int cc, std::vector<std::pair<int, double>> &out) {
-            if (cc < m) out = cols[cc];
-        }, up[p].bs, up[p].bi, up[p].bv);
-    });
-    const auto tb = std::chrono::steady_clock::now();
-    // concatenation: offsets first, then every basis copies its part (sizes known up front)
-    std::vector<size_t> eo(P + 1, 0), ro(P + 1, 0);
-    for (int p = 0; p < P; ++p) {
-        eo[p + 1] = eo[p] + (c->CH > 0 ? up[p].bi.size() : 0);
-        ro[p + 1] = ro[p] + c->pool[p].rcol.size();
-    }
-    if (eo[P] / 64 > INT32_MAX || ro[P] > INT32_MAX) return fail(TWOSD_E_UNSUPPORTED, "basis pool too large (> 2^31 entries)");
-    // default-initialised (not zeroed) buffers: every entry is written below, first touch in parallel
-    std::vector<int> bs_all(c->CH > 0 ? (size_t)P * (c->R + 1) : 0), rp_all((size_t)P * (MP + 1));
-    std::unique_ptr<int[]> bi_all(new int[std::max<size_t>(eo[P], 1)]), rc_all(new int[std::max<size_t>(ro[P], 1)]);
-    std::unique_ptr<double[]> bv_all(new double[std::max<size_t>(eo[P], 1)]), rv_all(new double[std::max<size_t>(ro[P], 1)]);
-    parallel_for(P, [&](int p) {
-        const PoolBasis &B = c->pool[p];
-        if (c->CH > 0) {
-            const int e0 = (int)(eo[p] / 64);
-            for (int t = 0; t <= c->R; ++t) bs_all[(size_t)p * (c->R + 1) + t] = up[p].bs[t] + e0;
-            std::copy(up[p].bi.begin(), up[p].bi.end(), bi_all.get() + eo[p]);
-            std::copy(up[p].bv.begin(), up[p].bv.end(), bv_all.get() + eo[p]);
-        }
-        for (int i = 0; i <= MP; ++i) rp_all[(size_t)p * (MP + 1) + i] = (int)ro[p] + B.rptr[std::min(i, m)];
-        std::copy(B.rcol.begin(), B.rcol.end(), rc_all.get() + ro[p]);
-        std::copy(B.rval.begin(), B.rval.end(), rv_all.get() + ro[p]);
     });
     const auto tc = std::chrono::steady_clock::now();
     int rc;
     if ((rc = upload(&c->d_hb0, hb)) || (rc = upload(&c->d_basic0, basic)) || (rc = upload(&c->d_bnnz, bnnz))) return rc;
     if (c->CH > 0) {
-        if ((rc = upload(&c->d_bslot, bs_all)) || (rc = upload_raw(&c->d_bix, bi_all.get(), eo[P])) ||
-            (rc = upload_raw(&c->d_bv, bv_all.get(), eo[P])) || (rc = upload(&c->d_brptr, rp_all)) ||
+        if ((rc = upload(&c->d_bcp, cp_all)) || (rc = upload_raw(&c->d_bci, ci_all.get(), ro[P])) ||
+            (rc = upload_raw(&c->d_bcv, cv_all.get(), ro[P])) || (rc = upload(&c->d_brptr, rp_all)) ||
             (rc = upload_raw(&c->d_brcol, rc_all.get(), ro[P])) || (rc = upload_raw(&c->d_brval, rv_all.get(), ro[P])) ||
-            (rc = upload(&c->d_d0, d0_all)))
+            (rc = upload_raw(&c->d_d0, d0_all.get(), (size_t)P * 64 * c->CH)))
             return rc;
         c->b0_nnz = bnnz[0];
     }
     if (getenv("TWOSD_DEBUG")) {
         const auto td = std::chrono::steady_clock::now();
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        fprintf(stderr, "upload_pool P=%d: build %.1f ms, concat %.1f ms, upload %.1f ms (%.1f MB: ell %zu, csr %zu, d0 %zu)\n", P,
-                ms(t_up0, tb), ms(tb, tc), ms(tc, td),
-                (eo[P] * 12.0 + ro[P] * 12.0 + d0_all.size() * 8.0) / 1e6, eo[P], ro[P], d0_all.size());
+        fprintf(stderr, "upload_pool P=%d: build %.1f ms, upload %.1f ms (%.1f MB, %zu nonzeros)\n", P, ms(t_up0, tc), ms(tc, td),
+                (ro[P] * 24.0 + (size_t)P * 64 * std::max(c->CH, 0) * 8.0) / 1e6, ro[P]);
     }
     c->prep_valid = false;
     c->k_valid = false;
@@ -666,51 +657,8 @@ static int prepare_elements(twosd_ctx *c);
 // and the eta file of its solve, B^{-1} = E_K..E_1 B_pb^{-1} (sparse row merges), so no
 // refactorisation: the cost is the training solves plus O(K nnz) host work per basis.
 
-// rows of B^{-1} (CSR, columns ascending) after the eta file, tiny entries dropped
-static void compose_binv(const PoolBasis &B0, int m, int K, const int *etap, const int *etaoff, const int *eidx,
-                         const double *evals, PoolBasis &out) {
-    std::vector<std::vector<std::pair<int, double>>> rows(m);
-    for (int i = 0; i < m; ++i)
-        for (int q = B0.rptr[i]; q < B0.rptr[i + 1]; ++q) rows[i].push_back({B0.rcol[q], B0.rval[q]});
-    std::vector<std::pair<int, double>> rr, tmp;
-    for (int t = 0; t < K; ++t) {
-        const int r = etap[t];
-        rr = rows[r];
-        for (int e = etaoff[t]; e < etaoff[t + 1]; ++e) {
-            const int i = eidx[e];
-            const double v = evals[e];
-            if (i == r) {
-                rows[r] = rr;
-                for (auto &cv : rows[r]) cv.second *= v;
-                continue;
-            }
-            // rows[i] += v * rr (both sorted by column)
-            tmp.clear();
-            const auto &a = rows[i];
-            size_t p = 0, q = 0;
-            while (p < a.size() || q < rr.size()) {
-                if (q == rr.size() || (p < a.size() && a[p].first < rr[q].first)) tmp.push_back(a[p++]);
-                else if (p == a.size() || rr[q].first < a[p].first) { tmp.push_back({rr[q].first, v * rr[q].second}); ++q; }
-                else { tmp.push_back({a[p].first, std::fma(v, rr[q].second, a[p].second)}); ++p; ++q; }
-            }
-            rows[i].swap(tmp);
-        }
-    }
-    double amax = 0.0;
-    for (auto &row : rows)
-        for (auto &cv : row) amax = std::max(amax, std::fabs(cv.second));
-    const double drop = 1e-14 * amax;
-    out.rptr.assign(1, 0);
-    out.rcol.clear(); out.rval.clear();
-    for (auto &row : rows) {
-        for (auto &cv : row)
-            if (std::fabs(cv.second) > drop) { out.rcol.push_back(cv.first); out.rval.push_back(cv.second); }
-        out.rptr.push_back((int)out.rcol.size());
-    }
-}
-
-// pi0 = c_B' B^{-1}; checks dual feasibility (1e-7) and B^{-1} a_{head[i]} = e_i on a few
-// positions (1e-8); nullptr if the basis is usable
+// pi0 = c_B' B^{-1} from the composed rows, then the checks of host_basis.cpp; nullptr if the
+// basis is usable
 static const char *finish_composed(const twosd_ctx *c, PoolBasis &B) {
     const HostLP &L = c->L;
     const int m = L.m, n = L.n;
@@ -721,37 +669,8 @@ static const char *finish_composed(const twosd_ctx *c, PoolBasis &B) {
         if (cb == 0.0) continue;
         for (int q = B.rptr[i]; q < B.rptr[i + 1]; ++q) B.pi0[B.rcol[q]] += cb * B.rval[q];
     }
-    std::vector<char> isb(n + m, 0);
-    for (int i = 0; i < m; ++i) isb[B.head[i]] = 1;
-    for (int j = 0; j < n + m; ++j) {
-        if (isb[j]) continue;
-        double d;
-        char sense = 'Y';
-        if (j < n) {
-            d = L.q[j];
-            for (int q = L.colptr[j]; q < L.colptr[j + 1]; ++q) d -= B.pi0[L.rowidx[q]] * L.val[q];
-        } else {
-            sense = L.sense[j - n];
-            if (sense == 'E') continue;
-            d = -B.pi0[j - n];
-        }
-        const double inf = sense == 'G' ? d : -d;   // G slack sits at its upper bound 0
-        if (inf > 1e-7) return "composed basis is not dual feasible";
-    }
-    std::vector<double> a(m);
-    for (int probe = 0; probe < 4; ++probe) {
-        const int i0 = (int)(((long long)probe * 7919 + 13) % m);
-        const int j = B.head[i0];
-        std::fill(a.begin(), a.end(), 0.0);
-        if (j >= n) a[j - n] = 1.0;
-        else
-            for (int q = L.colptr[j]; q < L.colptr[j + 1]; ++q) a[L.rowidx[q]] = L.val[q];
-        for (int i = 0; i < m; ++i) {
-            double v = 0.0;
-            for (int q = B.rptr[i]; q < B.rptr[i + 1]; ++q) v += B.rval[q] * a[B.rcol[q]];
-            if (std::fabs(v - (i == i0 ? 1.0 : 0.0)) > 1e-8) return "composed B^{-1} inconsistent";
-        }
-    }
+    if (sparse_dual_infeasibility(L, B.head, B.pi0) > 1e-7) return "composed basis is not dual feasible";
+    if (sparse_basis_residual(L, B.head, B.rptr, B.rcol, B.rval, 4) > 1e-8) return "composed B^{-1} inconsistent";
     return nullptr;
 }
 
@@ -833,8 +752,9 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
                     PoolBasis &B = fresh[a];
                     B.head.assign(heads.begin() + (size_t)a * m, heads.begin() + (size_t)(a + 1) * m);
                     const int *eo = etaoff.data() + (size_t)a * (kmax + 1);
-                    compose_binv(c->pool[pb[a]], m, K[a], etap.data() + (size_t)a * kmax, eo, ei.data() + off[a],
-                                 ev.data() + off[a], B);
+                    const PoolBasis &B0 = c->pool[pb[a]];
+                    compose_binv(m, B0.rptr, B0.rcol, B0.rval, K[a], etap.data() + (size_t)a * kmax, eo, ei.data() + off[a],
+                                 ev.data() + off[a], B.rptr, B.rcol, B.rval);
                     ok[a] = finish_composed(c, B) == nullptr;
                 }
             });
@@ -1126,87 +1046,111 @@ extern "C" int twosd_epigraph_info(twosd_ctx *c, int epi, int *ns, double *tw) {
 // into kix/kv).  The kernels multiply the scenario deltas by coef_e(x) (d_kcoef) themselves.
 static int prepare_elements(twosd_ctx *c) {
     const auto t_pe0 = std::chrono::steady_clock::now();
-    const int m = c->L.m, k = c->k;
+    const int m = c->L.m, k = c->k, R = c->R;
     std::vector<std::vector<int>> bycol(m);   // random elements on each row
     for (int e = 0; e < k; ++e) bycol[c->pos_row[e]].push_back(e);
-    std::vector<int> ks, ki;
-    std::vector<double> kv;
-    const int P0 = (int)c->pool.size();
-    struct Up { std::vector<int> sl, ix; std::vector<double> vv; };
-    std::vector<Up> up(P0);
-    parallel_for(P0, [&](int p) {
-        PoolBasis &B = c->pool[p];
-        B.kptr.assign(1, 0);
-        B.ke.clear(); B.kraw.clear();
+    const int P = (int)c->pool.size();
+    std::vector<int8_t> bt(c->L.n + m);
+    HIPCHK(hipMemcpy(bt.data(), c->d_btype, bt.size(), hipMemcpyDeviceToHost));
+    // pass 1: per basis and row the number of element entries; CSR / ELL / record sizes
+    std::vector<int> rowcnt((size_t)P * m), width((size_t)P * R);
+    std::vector<size_t> kcnt(P + 1, 0), ecnt(P + 1, 0);
+    std::vector<int64_t> ccnt(P + 1, 0);
+    parallel_for(P, [&](int p) {
+        const PoolBasis &B = c->pool[p];
+        int *rc = rowcnt.data() + (size_t)p * m;
+        size_t tot = 0;
+        int64_t cp = 0;   // selection records: every row active; rows of fixed (E) basics twice
+        for (int i = 0; i < m; ++i) {
+            int n_i = 0;
+            for (int q = B.rptr[i]; q < B.rptr[i + 1]; ++q) n_i += (int)bycol[B.rcol[q]].size();
+            rc[i] = n_i;
+            tot += n_i;
+            cp += (int64_t)(1 + n_i) * (bt[B.head[i]] == BT_E ? 2 : 1);
+        }
+        size_t ell = 0;
+        for (int t = 0; t < R; ++t) {
+            int w = 0;
+            for (int l = 0; l < 64 && 64 * t + l < m; ++l) w = std::max(w, rc[64 * t + l]);
+            width[(size_t)p * R + t] = w;
+            ell += (size_t)w * 64;
+        }
+        kcnt[p + 1] = tot;
+        ecnt[p + 1] = ell;
+        ccnt[p + 1] = cp;
+    });
+    for (int p = 0; p < P; ++p) { kcnt[p + 1] += kcnt[p]; ecnt[p + 1] += ecnt[p]; ccnt[p + 1] += ccnt[p]; }
+    if (kcnt[P] > INT32_MAX || ecnt[P] / 64 > INT32_MAX || ccnt[P] > INT32_MAX)
+        return fail(TWOSD_E_UNSUPPORTED, "basis pool element data too large (> 2^31 entries)");
+    // pass 2: rows of B_p^{-1}[:, row_e] (e ascending) as CSR (selection inputs) and sliced ELL
+    // by row (x_B warm start of the LP kernel), written in place
+    const size_t kz = std::max<size_t>(kcnt[P], 1), ez = std::max<size_t>(ecnt[P], 1);
+    std::vector<int> kp((size_t)P * (m + 1)), ks((size_t)P * (R + 1)), cap(P + 1);
+    std::unique_ptr<int[]> ke(new int[kz]), ki(new int[ez]);
+    std::unique_ptr<double[]> kr(new double[kz]), kv(new double[ez]);
+    for (int p = 0; p <= P; ++p) cap[p] = (int)ccnt[p];
+    parallel_for(P, [&](int p) {
+        const PoolBasis &B = c->pool[p];
+        const int *rc = rowcnt.data() + (size_t)p * m;
         std::vector<std::pair<int, double>> row;
+        size_t at = kcnt[p];
+        const size_t e_row0 = ecnt[p] / 64;   // first ELL entry row of this basis
+        size_t so = 0;                        // slot offset (entry rows) within the basis
+        for (int t = 0; t <= R; ++t) {
+            ks[(size_t)p * (R + 1) + t] = (int)(e_row0 + so);
+            if (t < R) so += width[(size_t)p * R + t];
+        }
         for (int i = 0; i < m; ++i) {
             row.clear();
             for (int q = B.rptr[i]; q < B.rptr[i + 1]; ++q)
                 for (int e : bycol[B.rcol[q]]) row.push_back({e, B.rval[q]});
             std::sort(row.begin(), row.end());
-            for (auto &ev : row) { B.ke.push_back(ev.first); B.kraw.push_back(ev.second); }
-            B.kptr.push_back((int)B.ke.size());
+            kp[(size_t)p * (m + 1) + i] = (int)at;
+            for (auto &ev : row) { ke[at] = ev.first; kr[at] = ev.second; ++at; }
         }
-        if (c->CH <= 0) return;
-        build_ell(c->R, [&](int i, std::vector<std::pair<int, double>> &out) {
-            if (i < m)
-                for (int q = B.kptr[i]; q < B.kptr[i + 1]; ++q) out.push_back({B.ke[q], B.kraw[q]});
-        }, up[p].sl, up[p].ix, up[p].vv);
+        kp[(size_t)p * (m + 1) + m] = (int)at;
+        (void)rc;
+        for (int t = 0; t < R; ++t) {
+            const int w = width[(size_t)p * R + t];
+            const size_t r0 = (size_t)ks[(size_t)p * (R + 1) + t];
+            for (int l = 0; l < 64; ++l) {
+                const int i = 64 * t + l;
+                const int q0 = i < m ? kp[(size_t)p * (m + 1) + i] : 0, q1 = i < m ? kp[(size_t)p * (m + 1) + i + 1] : 0;
+                for (int e = 0; e < w; ++e) {
+                    const bool has = q0 + e < q1;
+                    ki[(r0 + e) * 64 + l] = has ? ke[q0 + e] : 0;
+                    kv[(r0 + e) * 64 + l] = has ? kr[q0 + e] : 0.0;
+                }
+            }
+        }
     });
-    if (c->CH > 0) {
-        std::vector<size_t> ko(P0 + 1, 0);
-        for (int p = 0; p < P0; ++p) ko[p + 1] = ko[p] + up[p].ix.size();
-        ks.resize((size_t)P0 * (c->R + 1));
-        ki.resize(ko[P0]);
-        kv.resize(ko[P0]);
-        parallel_for(P0, [&](int p) {
-            const int e0 = (int)(ko[p] / 64);
-            for (int t = 0; t <= c->R; ++t) ks[(size_t)p * (c->R + 1) + t] = up[p].sl[t] + e0;
-            std::copy(up[p].ix.begin(), up[p].ix.end(), ki.begin() + ko[p]);
-            std::copy(up[p].vv.begin(), up[p].vv.end(), kv.begin() + ko[p]);
-        });
-    }
     const auto t_pe1 = std::chrono::steady_clock::now();
     int rc;
-    if (c->CH > 0 && ((rc = upload(&c->d_kslot, ks)) || (rc = upload(&c->d_kix, ki)) || (rc = upload(&c->d_kv, kv)))) return rc;
+    if (c->CH > 0 && ((rc = upload(&c->d_kslot, ks)) || (rc = upload_raw(&c->d_kix, ki.get(), ecnt[P])) ||
+                      (rc = upload_raw(&c->d_kv, kv.get(), ecnt[P]))))
+        return rc;
     const auto t_pe2 = std::chrono::steady_clock::now();
-    if (c->CH > 0 && c->pool.size() > 1) {
+    if (c->CH > 0 && P > 1) {
         // device selection-stream inputs: CSR rows of every basis, and a static record capacity
         // per basis (every row active: m row starts + all its entries)
-        const int P = (int)c->pool.size();
-        std::vector<int> kp, ke, cap(P + 1, 0);
-        std::vector<double> kr;
-        std::vector<int8_t> bt(c->L.n + m);
-        HIPCHK(hipMemcpy(bt.data(), c->d_btype, bt.size(), hipMemcpyDeviceToHost));
-        kp.reserve((size_t)P * (m + 1));
-        for (int p = 0; p < P; ++p) {
-            const PoolBasis &B = c->pool[p];
-            const int base = (int)ke.size();
-            for (int i = 0; i <= m; ++i) kp.push_back(base + B.kptr[i]);
-            ke.insert(ke.end(), B.ke.begin(), B.ke.end());
-            kr.insert(kr.end(), B.kraw.begin(), B.kraw.end());
-            int64_t cp = 0;   // every row active; rows of fixed (E) basics are emitted twice
-            for (int i = 0; i < m; ++i) cp += (int64_t)(1 + B.kptr[i + 1] - B.kptr[i]) * (bt[B.head[i]] == BT_E ? 2 : 1);
-            if (cap[p] + cp > INT32_MAX) return fail(TWOSD_E_UNSUPPORTED, "pool selection stream: > 2^31 records");
-            cap[p + 1] = cap[p] + (int)cp;
-        }
-        if (ke.empty()) { ke.push_back(0); kr.push_back(0.0); }
-        if ((rc = upload(&c->d_kp, kp)) || (rc = upload(&c->d_ke, ke)) || (rc = upload(&c->d_kraw, kr)) ||
+        if ((rc = upload(&c->d_kp, kp)) || (rc = upload_raw(&c->d_ke, ke.get(), kz)) || (rc = upload_raw(&c->d_kraw, kr.get(), kz)) ||
             (rc = upload(&c->d_sel_ptr, cap)))
             return rc;
-        dfree(c->d_sel_code);
+        if ((size_t)std::max(cap[P], 1) > c->sel_code_cap) {
+            dfree(c->d_sel_code);
+            if ((rc = dalloc(&c->d_sel_code, 2 * (size_t)std::max(cap[P], 1)))) return rc;
+            c->sel_code_cap = std::max(cap[P], 1);
+        }
         dfree(c->d_sel_end);
         dfree(c->d_sel_cinf);
-        if ((rc = dalloc(&c->d_sel_code, 2 * (size_t)std::max(cap[P], 1))) || (rc = dalloc(&c->d_sel_end, (size_t)P)) ||
-            (rc = dalloc(&c->d_sel_cinf, (size_t)P)))
-            return rc;
+        if ((rc = dalloc(&c->d_sel_end, (size_t)P)) || (rc = dalloc(&c->d_sel_cinf, (size_t)P))) return rc;
         c->sel_cap_total = cap[P];
     }
     c->k_valid = true;
     if (getenv("TWOSD_DEBUG")) {
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        fprintf(stderr, "prepare_elements P=%zu: build %.1f ms, upload ell %.1f ms (%zu entries), selection inputs %.1f ms\n",
-                c->pool.size(), ms(t_pe0, t_pe1), ms(t_pe1, t_pe2), ki.size(), ms(t_pe2, std::chrono::steady_clock::now()));
+        fprintf(stderr, "prepare_elements P=%d: build %.1f ms, upload ell %.1f ms (%zu entries), selection inputs %.1f ms\n",
+                P, ms(t_pe0, t_pe1), ms(t_pe1, t_pe2), ecnt[P], ms(t_pe2, std::chrono::steady_clock::now()));
     }
     return TWOSD_OK;
 }
@@ -1548,7 +1492,7 @@ int twosd::run_lp_ex(twosd_ctx *c, const double *x, const double *d_dv, int N, c
         H.colptr = c->d_colptr; H.rowidx = c->d_rowidx; H.val = c->d_val; H.q = c->d_q; H.btype = c->d_btype;
         H.wr_width = c->wr_width; H.wr_col = c->d_wr_col; H.wr_val = c->d_wr_val;
         H.wr_ocol = c->d_wr_ocol; H.wr_oval = c->d_wr_oval;
-        H.bslot = c->d_bslot; H.bix = c->d_bix; H.bv = c->d_bv;
+        H.bcp = c->d_bcp; H.bci = c->d_bci; H.bcv = c->d_bcv;
         H.brptr = c->d_brptr; H.brcol = c->d_brcol; H.brval = c->d_brval;
         H.kslot = c->d_kslot; H.kix = c->d_kix; H.kv = c->d_kv; H.kcoef = c->d_kcoef;
         H.xbase = c->d_xbase; H.d0 = c->d_d0; H.hb0 = c->d_hb0;

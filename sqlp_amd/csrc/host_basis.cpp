@@ -9,6 +9,7 @@
 // setup_solve: revised dual simplex with an explicit dense inverse updated by rank-1
 // pivots and re-inverted every kRefactor pivots (O(m^2) per pivot).  Dantzig leaving
 // row, Harris two-pass ratio test.  Requires q >= 0 so the slack basis is dual feasible.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -218,6 +219,90 @@ int setup_solve(const HostLP &L, const std::vector<double> &b, std::vector<int> 
     for (int i = 0; i < m; ++i)
         if (head[i] < n) obj += L.q[head[i]] * xB[i];
     return TWOSD_LP_OPTIMAL;
+}
+
+// ---- composed pool bases (twosd_pool_refresh) ---------------------------------------------
+
+void compose_binv(int m, const std::vector<int> &rptr0, const std::vector<int> &rcol0, const std::vector<double> &rval0,
+                  int K, const int *etap, const int *etaoff, const int *eidx, const double *evals, std::vector<int> &rptr,
+                  std::vector<int> &rcol, std::vector<double> &rval) {
+    // E_t = I + (eta - e_r) e_r' on the left: row r <- eta_r row r, row i <- row i + eta_i row r
+    // (the old row r for every i), as sorted sparse row merges
+    std::vector<std::vector<std::pair<int, double>>> rows(m);
+    for (int i = 0; i < m; ++i)
+        for (int q = rptr0[i]; q < rptr0[i + 1]; ++q) rows[i].push_back({rcol0[q], rval0[q]});
+    std::vector<std::pair<int, double>> rr, tmp;
+    for (int t = 0; t < K; ++t) {
+        const int r = etap[t];
+        rr = rows[r];
+        for (int e = etaoff[t]; e < etaoff[t + 1]; ++e) {
+            const int i = eidx[e];
+            const double v = evals[e];
+            if (i == r) {
+                rows[r] = rr;
+                for (auto &cv : rows[r]) cv.second *= v;
+                continue;
+            }
+            tmp.clear();
+            const auto &a = rows[i];
+            size_t p = 0, q = 0;
+            while (p < a.size() || q < rr.size()) {
+                if (q == rr.size() || (p < a.size() && a[p].first < rr[q].first)) tmp.push_back(a[p++]);
+                else if (p == a.size() || rr[q].first < a[p].first) { tmp.push_back({rr[q].first, v * rr[q].second}); ++q; }
+                else { tmp.push_back({a[p].first, std::fma(v, rr[q].second, a[p].second)}); ++p; ++q; }
+            }
+            rows[i].swap(tmp);
+        }
+    }
+    double amax = 0.0;
+    for (auto &row : rows)
+        for (auto &cv : row) amax = std::max(amax, std::fabs(cv.second));
+    const double drop = 1e-14 * amax;
+    rptr.assign(1, 0);
+    rcol.clear();
+    rval.clear();
+    for (auto &row : rows) {
+        for (auto &cv : row)
+            if (std::fabs(cv.second) > drop) { rcol.push_back(cv.first); rval.push_back(cv.second); }
+        rptr.push_back((int)rcol.size());
+    }
+}
+
+double sparse_dual_infeasibility(const HostLP &L, const std::vector<int> &head, const std::vector<double> &pi0) {
+    const int m = L.m, n = L.n;
+    std::vector<char> isb(n + m, 0);
+    for (int i = 0; i < m; ++i) isb[head[i]] = 1;
+    double worst = 0.0;
+    for (int j = 0; j < n + m; ++j) {
+        if (isb[j]) continue;
+        const int bt = btype_of(L, j);
+        if (bt == BT_E) continue;
+        const double d = (j < n ? L.q[j] : 0.0) - col_dot(L, j, pi0.data());
+        const double inf = bt == BT_G ? d : -d;   // a G slack sits at its upper bound 0
+        worst = std::max(worst, inf);
+    }
+    return worst;
+}
+
+double sparse_basis_residual(const HostLP &L, const std::vector<int> &head, const std::vector<int> &rptr,
+                             const std::vector<int> &rcol, const std::vector<double> &rval, int probes) {
+    const int m = L.m, n = L.n;
+    std::vector<double> a(m);
+    double worst = 0.0;
+    for (int probe = 0; probe < probes; ++probe) {
+        const int i0 = (int)(((long long)probe * 7919 + 13) % m);
+        const int j = head[i0];
+        std::fill(a.begin(), a.end(), 0.0);
+        if (j >= n) a[j - n] = 1.0;
+        else
+            for (int q = L.colptr[j]; q < L.colptr[j + 1]; ++q) a[L.rowidx[q]] = L.val[q];
+        for (int i = 0; i < m; ++i) {
+            double v = 0.0;
+            for (int q = rptr[i]; q < rptr[i + 1]; ++q) v += rval[q] * a[rcol[q]];
+            worst = std::max(worst, std::fabs(v - (i == i0 ? 1.0 : 0.0)));
+        }
+    }
+    return worst;
 }
 
 }  // namespace twosd

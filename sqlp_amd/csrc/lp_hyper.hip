@@ -212,7 +212,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         int hb[R];
         double d[C];
         uint64_t bmask;
-        const int *brptr, *bslot;
+        const int *brptr, *bcp;
         int K = 0, it = 0, status = TWOSD_LP_OPTIMAL;
         int eoff = 0;
         long long nops = 0;
@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         // primary basis, so the pool never changes which scenarios solve
         for (int attempt = 0; attempt < 2; ++attempt) {
         brptr = P.brptr + (size_t)pb * (MP + 1);
-        bslot = P.bslot + (size_t)pb * (R + 1);
+        bcp = P.bcp + (size_t)pb * (MP + 1);
 #pragma unroll
         for (int t = 0; t < R; ++t) {
             xB[t] = xb_row(pb, t);
@@ -458,21 +458,17 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             h_wave_sync();
             STAMP(6)
 
-            // ---- 4. FTRAN: ut = E_K..E_1 B0^{-1} a_q (ut is all zeros here).  Column cc of
-            // B0^{-1} is ELL slot cc/64, lane cc%64: its entry e sits at (bslot + e)*64 + cc%64.
+            // ---- 4. FTRAN: ut = E_K..E_1 B0^{-1} a_q (ut is all zeros here): the CSC columns of
+            // B0^{-1} under the nonzeros of a_q, lanes over a column's entries (distinct rows)
             {
                 const int np0 = q >= n ? 0 : P.colptr[q], np1 = q >= n ? 1 : P.colptr[q + 1];
                 for (int pw = np0; pw < np1; ++pw) {
                     const int cc = q >= n ? q - n : P.rowidx[pw];
                     const double aw = q >= n ? 1.0 : P.val[pw];
-                    const int ts = cc >> 6, cl = cc & 63;
-                    const int e0 = bslot[ts], e1 = bslot[ts + 1];
+                    const int e0 = bcp[cc], e1 = bcp[cc + 1];
                     for (int e = e0 + lane; e < e1; e += 64) {
-                        const double v = P.bv[e * 64 + cl];
-                        if (v != 0.0) {
-                            const int i = P.bix[e * 64 + cl];
-                            ut[i] = fma(aw, v, ut[i]);
-                        }
+                        const int i = P.bci[e];
+                        ut[i] = fma(aw, P.bcv[e], ut[i]);
                     }
                     nops += e1 - e0;
                     h_wave_sync();
@@ -653,14 +649,12 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             double pv[R];
             double pmax = 0.0;
 #pragma unroll
-            for (int t = 0; t < R; ++t) {
-                const int e0 = bslot[t], e1 = bslot[t + 1];
+            for (int t = 0; t < R; ++t) {   // lane: column 64t + lane of B^{-1} (CSC, rows ascending)
+                const int cc = 64 * t + lane;
+                const int e0 = cc < m ? bcp[cc] : 0, e1 = cc < m ? bcp[cc + 1] : 0;
                 double a = 0.0;
 #pragma unroll TWOSD_REC_UNROLL
-                for (int e = e0; e < e1; ++e) {
-                    const double v = P.bv[e * 64 + lane];
-                    a = fma(ut[P.bix[e * 64 + lane]], v, a);
-                }
+                for (int e = e0; e < e1; ++e) a = fma(ut[P.bci[e]], P.bcv[e], a);
                 pv[t] = a;
                 pmax = fmax(pmax, fabs(a));
             }

@@ -23,8 +23,6 @@ struct PoolBasis {
     std::vector<double> pi0;      // c_B' B^{-1}
     std::vector<int> rptr, rcol;  // B^{-1} rows, CSR (|v| > 1e-14 max|B^{-1}|)
     std::vector<double> rval;
-    std::vector<int> kptr, ke;    // rows of B^{-1}[:, row_e] over the random elements e (x-independent)
-    std::vector<double> kraw;
 };
 
 }  // namespace twosd
@@ -63,6 +61,7 @@ struct twosd_ctx {
     double *d_xaux = nullptr;            // per x: b (m), coef (k), box lo (k), box hi (k)
     size_t xaux_cap = 0;
     int64_t sel_cap_total = 0;           // records the static capacity layout holds
+    size_t sel_code_cap = 0;             // records d_sel_code has room for
     int64_t sel_nnz = 0, sel_rows = 0;
     float sel_cw = 0.0f;                 // pool selection key: sum |infeas| + sel_cw * #infeasible rows
     std::vector<double> sel_lo, sel_hi;   // training box of the deltas (empty: no row pruning)
@@ -90,8 +89,8 @@ struct twosd_ctx {
     int *d_kslot = nullptr, *d_kix = nullptr;
     double *d_kv = nullptr, *d_d0 = nullptr;
     int wr_width = 1;             // W row-ELL width (max row length)
-    int *d_wr_col = nullptr, *d_bslot = nullptr, *d_bix = nullptr;
-    double *d_wr_val = nullptr, *d_bv = nullptr;
+    int *d_wr_col = nullptr, *d_bcp = nullptr, *d_bci = nullptr;
+    double *d_wr_val = nullptr, *d_bcv = nullptr;
     int *d_wr_ocol = nullptr;
     double *d_wr_oval = nullptr;
     int *d_brptr = nullptr, *d_brcol = nullptr;

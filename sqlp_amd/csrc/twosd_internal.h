@@ -30,9 +30,9 @@ struct HyperParams {
     int wr_width;                                       // W by rows as row-ELL (columns ascending, width
     const int *wr_col; const double *wr_val;            //   min(max row length, 64), padding column -1);
     const int *wr_ocol; const double *wr_oval;          //   long rows continue in an overflow CSR
-    // sliced ELL (entry e of slot s for lane l at [(slot_off[s] + e) * 64 + l]; padding: idx 0, val 0):
-    const int *bslot, *bix; const double *bv;           // columns of B^{-1}, R slots (c = 64t + lane)
+    const int *bcp, *bci; const double *bcv;            // B^{-1} CSC (MP + 1 column pointers, rows ascending)
     const int *brptr, *brcol; const double *brval;      // B^{-1} CSR (MP rows)
+    // sliced ELL (entry e of slot s for lane l at [(slot_off[s] + e) * 64 + l]; padding: idx 0, val 0):
     // per pool basis p, rows i = 64t + lane of coef_e B_p^{-1}[i][row_e] as sliced ELL (R slots,
     // kslot pool-strided npool x (R+1), absolute into the concatenated kix (= e) / kv)
     const int *kslot, *kix; const double *kv;           // values B_p^{-1}[i][row_e] (x-independent)
@@ -49,8 +49,8 @@ struct HyperParams {
     int *status, *iters;
     long long *ops;                                     // executed FMAs
     unsigned long long *stamps;                         // [10] phase cycles (TWOSD_STAMPS builds only)
-    // basis pool: xbase, hb0 (npool x MP), brptr (npool x (MP+1), absolute offsets),
-    // bslot (npool x (R+1), absolute), basic0 (npool x 64), d0 (npool x 64C) are pool-strided
+    // basis pool: xbase, hb0 (npool x MP), brptr / bcp (npool x (MP+1), absolute offsets),
+    // basic0 (npool x 64), d0 (npool x 64C) are pool-strided
     int npool;
     const int *bnnz;                                    // npool: nnz of B^{-1} (ops accounting)
     int *head_out;                                      // N x m final basis (nullable)
@@ -147,6 +147,17 @@ int setup_solve(const HostLP &L, const std::vector<double> &b, std::vector<int> 
 // max dual infeasibility of basis head (0 = dual feasible); pi0 = c_B' B^{-1}
 double basis_dual_infeasibility(const HostLP &L, const std::vector<int> &head,
                                 const std::vector<double> &Binv, std::vector<double> &pi0);
+// pool refresh: rows of B^{-1} = E_K..E_1 B0^{-1} (CSR, columns ascending, |v| <= 1e-14 max
+// dropped) from B0^{-1}'s rows and an eta file (pivot rows etap[K], entries [etaoff[t],
+// etaoff[t+1]) of (eidx, evals), the pivot row's entry being 1 / alpha_rq)
+void compose_binv(int m, const std::vector<int> &rptr0, const std::vector<int> &rcol0, const std::vector<double> &rval0,
+                  int K, const int *etap, const int *etaoff, const int *eidx, const double *evals, std::vector<int> &rptr,
+                  std::vector<int> &rcol, std::vector<double> &rval);
+// max dual infeasibility of head given pi0 = c_B' B^{-1}; max |B^{-1} a_{head[i]} - e_i| over
+// `probes` positions i of the CSR rows of B^{-1}
+double sparse_dual_infeasibility(const HostLP &L, const std::vector<int> &head, const std::vector<double> &pi0);
+double sparse_basis_residual(const HostLP &L, const std::vector<int> &head, const std::vector<int> &rptr,
+                             const std::vector<int> &rcol, const std::vector<double> &rval, int probes);
 
 // ---- dual vertex set kernels (dvs_kernel.hip) ------------------------------------
 struct DvsDevice {

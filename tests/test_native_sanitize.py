@@ -1,0 +1,78 @@
+"""Host-side sanitizer runs (CPU): the host C++ of libtwosd_hip.so (host_basis.cpp: setup
+solve, dense inverse, B^{-1} composition of the pool refresh, the sparse checks) and the
+oracle's C restatement, each built with AddressSanitizer + UndefinedBehaviorSanitizer and run
+on LP files of the SMPS instances (tests/native/*).  Only host code is instrumented (no GPU
+sanitizer on this pool)."""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from tests import instances as I
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _write_lp(path, name):
+    from oracle import lp_highs
+    sp = I.load(name)["osp2"]
+    x = I.x_ev(name)
+    b = sp.r - sp.T @ x
+    st, obj, _, _ = lp_highs.solve_rhs(sp, b)
+    assert st == 0
+    W = np.asarray(sp.W)
+    m, n = W.shape
+    colptr, rows, vals = [0], [], []
+    for j in range(n):
+        nz = np.nonzero(W[:, j])[0]
+        rows += nz.tolist(); vals += W[nz, j].tolist(); colptr.append(len(rows))
+    with open(path, "wb") as f:
+        np.array([m, n], dtype=np.int32).tofile(f)
+        np.array(colptr, dtype=np.int32).tofile(f)
+        np.array(rows, dtype=np.int32).tofile(f)
+        np.array(vals, dtype=np.float64).tofile(f)
+        np.asarray(sp.q, dtype=np.float64).tofile(f)
+        np.frombuffer("".join(sp.senses).encode(), dtype=np.int8).tofile(f)
+        np.asarray(b, dtype=np.float64).tofile(f)
+        np.array([obj], dtype=np.float64).tofile(f)
+
+
+@pytest.fixture(scope="module")
+def lp_files(tmp_path_factory):
+    d = tmp_path_factory.mktemp("lps")
+    out = []
+    for name in ["lands", "newsvendor", "transship", "ssn"]:
+        p = str(d / f"{name}.lp")
+        _write_lp(p, name)
+        out.append(p)
+    return out
+
+
+def _env():
+    e = dict(os.environ)
+    e["ASAN_OPTIONS"] = "detect_leaks=1:abort_on_error=0:halt_on_error=1"
+    e["UBSAN_OPTIONS"] = "print_stacktrace=1:halt_on_error=1"
+    e["OMP_NUM_THREADS"] = "2"
+    return e
+
+
+@pytest.mark.skipif(shutil.which("make") is None, reason="make not available")
+def test_host_cpp_under_asan_ubsan(lp_files):
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "sqlp_amd", "csrc"), "sanitize"])
+    exe = os.path.join(ROOT, "sqlp_amd", "csrc", "build_san", "host_check")
+    r = subprocess.run([exe] + lp_files, capture_output=True, text=True, env=_env(), timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr
+    assert r.stdout.count("composed exchanges") == len(lp_files)
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="gcc not available")
+def test_oracle_c_under_asan_ubsan(lp_files):
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "sanitize"])
+    exe = os.path.join(ROOT, "oracle", "build", "oracle_check")
+    r = subprocess.run([exe] + lp_files, capture_output=True, text=True, env=_env(), timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr
+    assert r.stdout.count("batch optimal") == len(lp_files)
