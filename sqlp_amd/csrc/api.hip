@@ -123,6 +123,20 @@ static void build_ell(int S, F colf, std::vector<int> &slot, std::vector<int> &i
     }
 }
 
+// pinned host staging buffer `slot` of at least n elements of T (grown, never shrunk)
+template <typename T>
+static T *stage_buf(twosd_ctx *c, int slot, size_t n) {
+    const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+    if (bytes > c->stage_bytes[slot]) {
+        if (c->stage[slot]) hipHostFree(c->stage[slot]);
+        c->stage[slot] = nullptr;
+        c->stage_bytes[slot] = 0;
+        if (hipHostMalloc(&c->stage[slot], bytes + bytes / 4) != hipSuccess) return nullptr;
+        c->stage_bytes[slot] = bytes + bytes / 4;
+    }
+    return static_cast<T *>(c->stage[slot]);
+}
+
 // f(i) for i in [0, n) on up to 16 host threads (per-basis pool preparation: independent work)
 template <typename F>
 static void parallel_for(int n, F f) {
@@ -143,6 +157,20 @@ template <typename T>
 static int upload_raw(T **d, const T *h, size_t n) {
     int rc = dalloc(d, std::max<size_t>(n, 1));
     if (rc) return rc;
+    if (n) HIPCHK(hipMemcpy(*d, h, sizeof(T) * n, hipMemcpyHostToDevice));
+    return TWOSD_OK;
+}
+
+// grow-only device array (no hipFree / hipMalloc when the new contents fit)
+template <typename T>
+static int upload_big(twosd_ctx *c, T **d, const T *h, size_t n) {
+    size_t &cap = c->dcap[(const void *)d];
+    if (!*d || cap < std::max<size_t>(n, 1)) {
+        const size_t want = std::max<size_t>(n, 1) + std::max<size_t>(n, 1) / 4;
+        int rc = dalloc(d, want);
+        if (rc) { cap = 0; return rc; }
+        cap = want;
+    }
     if (n) HIPCHK(hipMemcpy(*d, h, sizeof(T) * n, hipMemcpyHostToDevice));
     return TWOSD_OK;
 }
@@ -178,6 +206,7 @@ static void free_template(twosd_ctx *c) {
     dvs_free(c);
     cut_free(c);
     vkey_free(c);
+    c->dcap.clear();
     dfree(c->d_vkey); c->vkey_cap = 0;
     dfree(c->d_bkey); c->bkey_cap = 0;
     dfree(c->d_eo_pb); dfree(c->d_eo_K); dfree(c->d_eo_off); dfree(c->d_eo_etap); dfree(c->d_eo_etaoff);
@@ -190,6 +219,8 @@ extern "C" int twosd_destroy(twosd_ctx *c) {
     hipSetDevice(c->device);
     free_template(c);
     for (int i = 0; i < 8; ++i) hipEventDestroy(c->ev[i]);
+    for (int i = 0; i < 16; ++i)
+        if (c->stage[i]) hipHostFree(c->stage[i]);
     hipStreamDestroy(c->stream);
     delete c;
     return TWOSD_OK;
@@ -401,9 +432,10 @@ static int upload_pool(twosd_ctx *c) {
     if (ro[P] > INT32_MAX) return fail(TWOSD_E_UNSUPPORTED, "basis pool too large (> 2^31 entries)");
     const size_t nz = std::max<size_t>(ro[P], 1);
     std::vector<int> rp_all((size_t)P * (MP + 1)), cp_all((size_t)P * (MP + 1));
-    std::unique_ptr<int[]> rc_all(new int[nz]), ci_all(new int[nz]);
-    std::unique_ptr<double[]> rv_all(new double[nz]), cv_all(new double[nz]);
-    std::unique_ptr<double[]> d0_all(c->CH > 0 ? new double[(size_t)P * 64 * c->CH] : nullptr);
+    int *rc_all = stage_buf<int>(c, 0, nz), *ci_all = stage_buf<int>(c, 1, nz);
+    double *rv_all = stage_buf<double>(c, 2, nz), *cv_all = stage_buf<double>(c, 3, nz);
+    double *d0_all = stage_buf<double>(c, 4, (size_t)P * 64 * std::max(c->CH, 1));
+    if (!rc_all || !ci_all || !rv_all || !cv_all || !d0_all) return fail(TWOSD_E_DEVICE, "pool upload: pinned staging allocation failed");
     parallel_for(P, [&](int p) {
         const PoolBasis &B = c->pool[p];
         std::vector<char> isb(n + m, 0);
@@ -415,8 +447,8 @@ static int upload_pool(twosd_ctx *c) {
         bnnz[p] = (int)B.rcol.size();
         const int base = (int)ro[p];
         for (int i = 0; i <= MP; ++i) rp_all[(size_t)p * (MP + 1) + i] = base + B.rptr[std::min(i, m)];
-        std::copy(B.rcol.begin(), B.rcol.end(), rc_all.get() + base);
-        std::copy(B.rval.begin(), B.rval.end(), rv_all.get() + base);
+        std::copy(B.rcol.begin(), B.rcol.end(), rc_all + base);
+        std::copy(B.rval.begin(), B.rval.end(), rv_all + base);
         // columns: counting sort of the row CSR (rows ascending within a column)
         std::vector<int> pos(m + 1, 0);
         for (int cc : B.rcol) ++pos[cc + 1];
@@ -429,7 +461,7 @@ static int upload_pool(twosd_ctx *c) {
                 cv_all[at] = B.rval[q];
             }
         if (c->CH <= 0) return;
-        double *d0 = d0_all.get() + (size_t)p * 64 * c->CH;
+        double *d0 = d0_all + (size_t)p * 64 * c->CH;
         for (int j = 0; j < 64 * c->CH; ++j) {
             if (j >= n + m || isb[j]) { d0[j] = 0.0; continue; }
             double sum = 0.0;
@@ -443,10 +475,10 @@ static int upload_pool(twosd_ctx *c) {
     int rc;
     if ((rc = upload(&c->d_hb0, hb)) || (rc = upload(&c->d_basic0, basic)) || (rc = upload(&c->d_bnnz, bnnz))) return rc;
     if (c->CH > 0) {
-        if ((rc = upload(&c->d_bcp, cp_all)) || (rc = upload_raw(&c->d_bci, ci_all.get(), ro[P])) ||
-            (rc = upload_raw(&c->d_bcv, cv_all.get(), ro[P])) || (rc = upload(&c->d_brptr, rp_all)) ||
-            (rc = upload_raw(&c->d_brcol, rc_all.get(), ro[P])) || (rc = upload_raw(&c->d_brval, rv_all.get(), ro[P])) ||
-            (rc = upload_raw(&c->d_d0, d0_all.get(), (size_t)P * 64 * c->CH)))
+        if ((rc = upload(&c->d_bcp, cp_all)) || (rc = upload_big(c, &c->d_bci, ci_all, ro[P])) ||
+            (rc = upload_big(c, &c->d_bcv, cv_all, ro[P])) || (rc = upload(&c->d_brptr, rp_all)) ||
+            (rc = upload_big(c, &c->d_brcol, rc_all, ro[P])) || (rc = upload_big(c, &c->d_brval, rv_all, ro[P])) ||
+            (rc = upload_big(c, &c->d_d0, d0_all, (size_t)P * 64 * c->CH)))
             return rc;
         c->b0_nnz = bnnz[0];
     }
@@ -1086,8 +1118,9 @@ static int prepare_elements(twosd_ctx *c) {
     // by row (x_B warm start of the LP kernel), written in place
     const size_t kz = std::max<size_t>(kcnt[P], 1), ez = std::max<size_t>(ecnt[P], 1);
     std::vector<int> kp((size_t)P * (m + 1)), ks((size_t)P * (R + 1)), cap(P + 1);
-    std::unique_ptr<int[]> ke(new int[kz]), ki(new int[ez]);
-    std::unique_ptr<double[]> kr(new double[kz]), kv(new double[ez]);
+    int *ke = stage_buf<int>(c, 5, kz), *ki = stage_buf<int>(c, 6, ez);
+    double *kr = stage_buf<double>(c, 7, kz), *kv = stage_buf<double>(c, 8, ez);
+    if (!ke || !ki || !kr || !kv) return fail(TWOSD_E_DEVICE, "pool elements: pinned staging allocation failed");
     for (int p = 0; p <= P; ++p) cap[p] = (int)ccnt[p];
     parallel_for(P, [&](int p) {
         const PoolBasis &B = c->pool[p];
@@ -1126,14 +1159,14 @@ static int prepare_elements(twosd_ctx *c) {
     });
     const auto t_pe1 = std::chrono::steady_clock::now();
     int rc;
-    if (c->CH > 0 && ((rc = upload(&c->d_kslot, ks)) || (rc = upload_raw(&c->d_kix, ki.get(), ecnt[P])) ||
-                      (rc = upload_raw(&c->d_kv, kv.get(), ecnt[P]))))
+    if (c->CH > 0 && ((rc = upload(&c->d_kslot, ks)) || (rc = upload_big(c, &c->d_kix, ki, ecnt[P])) ||
+                      (rc = upload_big(c, &c->d_kv, kv, ecnt[P]))))
         return rc;
     const auto t_pe2 = std::chrono::steady_clock::now();
     if (c->CH > 0 && P > 1) {
         // device selection-stream inputs: CSR rows of every basis, and a static record capacity
         // per basis (every row active: m row starts + all its entries)
-        if ((rc = upload(&c->d_kp, kp)) || (rc = upload_raw(&c->d_ke, ke.get(), kz)) || (rc = upload_raw(&c->d_kraw, kr.get(), kz)) ||
+        if ((rc = upload(&c->d_kp, kp)) || (rc = upload_big(c, &c->d_ke, ke, kz)) || (rc = upload_big(c, &c->d_kraw, kr, kz)) ||
             (rc = upload(&c->d_sel_ptr, cap)))
             return rc;
         if ((size_t)std::max(cap[P], 1) > c->sel_code_cap) {

@@ -227,43 +227,59 @@ void compose_binv(int m, const std::vector<int> &rptr0, const std::vector<int> &
                   int K, const int *etap, const int *etaoff, const int *eidx, const double *evals, std::vector<int> &rptr,
                   std::vector<int> &rcol, std::vector<double> &rval) {
     // E_t = I + (eta - e_r) e_r' on the left: row r <- eta_r row r, row i <- row i + eta_i row r
-    // (the old row r for every i), as sorted sparse row merges
-    std::vector<std::vector<std::pair<int, double>>> rows(m);
-    for (int i = 0; i < m; ++i)
-        for (int q = rptr0[i]; q < rptr0[i + 1]; ++q) rows[i].push_back({rcol0[q], rval0[q]});
+    // (the old row r for every i), as sorted sparse row merges.  Only rows in the support of
+    // some eta change (the pivot row is in its own eta); the others are copied from B0^{-1}.
+    std::vector<int> slot(m, -1);
+    std::vector<std::vector<std::pair<int, double>>> rows;
+    for (int e = 0; e < (K > 0 ? etaoff[K] : 0); ++e) {
+        const int i = eidx[e];
+        if (slot[i] >= 0) continue;
+        slot[i] = (int)rows.size();
+        rows.emplace_back();
+        auto &row = rows.back();
+        for (int q = rptr0[i]; q < rptr0[i + 1]; ++q) row.push_back({rcol0[q], rval0[q]});
+    }
     std::vector<std::pair<int, double>> rr, tmp;
     for (int t = 0; t < K; ++t) {
         const int r = etap[t];
-        rr = rows[r];
+        rr = rows[slot[r]];
         for (int e = etaoff[t]; e < etaoff[t + 1]; ++e) {
             const int i = eidx[e];
             const double v = evals[e];
+            auto &a = rows[slot[i]];
             if (i == r) {
-                rows[r] = rr;
-                for (auto &cv : rows[r]) cv.second *= v;
+                a = rr;
+                for (auto &cv : a) cv.second *= v;
                 continue;
             }
             tmp.clear();
-            const auto &a = rows[i];
             size_t p = 0, q = 0;
             while (p < a.size() || q < rr.size()) {
                 if (q == rr.size() || (p < a.size() && a[p].first < rr[q].first)) tmp.push_back(a[p++]);
                 else if (p == a.size() || rr[q].first < a[p].first) { tmp.push_back({rr[q].first, v * rr[q].second}); ++q; }
                 else { tmp.push_back({a[p].first, std::fma(v, rr[q].second, a[p].second)}); ++p; ++q; }
             }
-            rows[i].swap(tmp);
+            a.swap(tmp);
         }
     }
     double amax = 0.0;
+    for (double v : rval0) amax = std::max(amax, std::fabs(v));
     for (auto &row : rows)
         for (auto &cv : row) amax = std::max(amax, std::fabs(cv.second));
     const double drop = 1e-14 * amax;
     rptr.assign(1, 0);
     rcol.clear();
     rval.clear();
-    for (auto &row : rows) {
-        for (auto &cv : row)
-            if (std::fabs(cv.second) > drop) { rcol.push_back(cv.first); rval.push_back(cv.second); }
+    rcol.reserve(rcol0.size() + rcol0.size() / 4);
+    rval.reserve(rcol0.size() + rcol0.size() / 4);
+    for (int i = 0; i < m; ++i) {
+        if (slot[i] < 0) {
+            rcol.insert(rcol.end(), rcol0.begin() + rptr0[i], rcol0.begin() + rptr0[i + 1]);
+            rval.insert(rval.end(), rval0.begin() + rptr0[i], rval0.begin() + rptr0[i + 1]);
+        } else {
+            for (auto &cv : rows[slot[i]])
+                if (std::fabs(cv.second) > drop) { rcol.push_back(cv.first); rval.push_back(cv.second); }
+        }
         rptr.push_back((int)rcol.size());
     }
 }

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <map>
 #include <vector>
 #include "twosd_internal.h"
 
@@ -139,6 +140,11 @@ struct twosd_ctx {
     size_t eo_rows = 0, eo_cap = 0;
     int eo_kmax = 0;
     double last_refresh_ms[5] = {0, 0, 0, 0, 0};   // train solves, re-solves, compose, upload, total
+    // pinned host staging buffers of the pool upload, kept across uploads (no page faults,
+    // no unmapping per refresh, page-locked copies)
+    void *stage[16] = {};
+    size_t stage_bytes[16] = {};
+    std::map<const void *, size_t> dcap;   // element capacity of grow-only device arrays (by member address)
     int last_push_reps = 0;       // representatives re-solved by the last solve_push
 };
 
