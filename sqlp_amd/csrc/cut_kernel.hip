@@ -51,6 +51,8 @@ struct CutParams {
     const double *coef;    // k4 (zero padded)
     const double *PK;      // nv x k4
     const double *PKT;     // k4 x vcap
+    const double *PKTc;    // 4 KB x vcap32: coef_e(x) * PKT, zero padded (cut_argmax2_kernel's LDS-DMA source)
+    int vcap32;            // row stride of PKTc (a multiple of 32 >= nv)
     const double *base;    // nv
     int *arg; double *val; int *flag;   // N
     unsigned long long *hist;           // nv (fixed point)
@@ -67,6 +69,17 @@ __global__ void cut_pk_kernel(int from, int to, int m, int k, int k4, int vcap, 
     const double x = e < k ? V[(size_t)v * m + rows[e]] : 0.0;
     PK[(size_t)v * k4 + e] = x;
     PKT[(size_t)e * vcap + v] = x;
+}
+
+// PKTc[kk][v] = coef_kk * PKT[kk][v] over rows [0, rows) x columns [0, vcap32), zero outside
+// [0, k) x [0, nv) (the LDS-DMA source of cut_argmax2_kernel; per x)
+__global__ void cut_pktc_kernel(int nv, int k, int rows, int vcap, int vcap32, const double *__restrict__ PKT,
+                                const double *__restrict__ coef, double *__restrict__ PKTc) {
+    const size_t total = (size_t)rows * vcap32;
+    for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
+        const int kk = (int)(idx / vcap32), v = (int)(idx % vcap32);
+        PKTc[idx] = (kk < k && v < nv) ? coef[kk] * PKT[(size_t)kk * vcap + v] : 0.0;
+    }
 }
 
 __global__ void __launch_bounds__(256) cut_vbase_kernel(int nv, int m, const double *__restrict__ V,
@@ -259,6 +272,211 @@ __global__ void __launch_bounds__(256, 2) cut_argmax_kernel(CutParams P) {
     }
 }
 
+// ---- v2: the score tile transposed -- MFMA A operand = the staged vertex chunk, B operand =
+// the scenario deltas -- so the C/D layout puts one SCENARIO per lane column (j) and four
+// vertices per lane (rows g + 4r): a lane tracks the running argmax of ONE scenario per A tile
+// instead of four, which frees the registers for two scenario tiles per wave (32 scenarios,
+// 128 per block) and two vertex tiles per chunk (32 vertices): every chunk staged in LDS
+// serves twice the scenarios of v1, and each LDS fragment read feeds two MFMAs.  The deltas
+// stay raw in registers (coef_e(x) is folded into the staged chunk), so the S_e sums of the
+// cut reuse them instead of re-reading the deltas from HBM.  Chunks are double-buffered.
+#ifndef TWOSD_CUT_KG
+#define TWOSD_CUT_KG 6                   // k-blocks whose fragments are read ahead together
+#endif
+#ifndef TWOSD_CUT_SB
+#define TWOSD_CUT_SB 1                   // scheduling barrier between the groups
+#endif
+constexpr int kVT2 = 32;                 // vertices per LDS chunk (two 16-vertex MFMA tiles)
+constexpr int kCutTile2 = 128;           // scenarios per block tile (4 waves x 2 x 16)
+constexpr int kLdsRow2 = 32;             // doubles per k-row of a chunk
+
+// LDS position of (k-row kk, vertex vv): odd rows have their 16-double halves swapped, so the
+// two k-rows a half-wave reads together (g = 0, 1 / 2, 3) fall on disjoint banks
+__device__ __forceinline__ int lds2(int kk, int vv) { return kk * kLdsRow2 + (vv ^ ((kk & 1) << 4)); }
+
+template <int KB>
+__global__ void __launch_bounds__(256, 2) cut_argmax2_kernel(CutParams P) {
+    __shared__ double Bs[2][4 * KB * kLdsRow2];     // double-buffered chunk (k-major)
+    __shared__ double bs[2][kVT2];
+    extern __shared__ unsigned long long hl[];      // nv entries when P.hist_lds
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    if (P.hist_lds)
+        for (int v = threadIdx.x; v < P.nv; v += 256) hl[v] = 0ull;
+    const int g = lane >> 4, j = lane & 15;
+    const int ntiles = (P.N + kCutTile2 - 1) / kCutTile2;
+    const int nchunks = (P.nv + kVT2 - 1) / kVT2;
+    double pv_sum = 0.0;
+    double Sacc[2] = {0.0, 0.0};   // lane (g, j): e = 4 kb + g for kb = j, j + 16
+
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        // this wave: scenarios s0 + j (tile 0) and s0 + 16 + j (tile 1); lane (g, j) holds their
+        // deltas e = 4 kb + g (the B operand: k = g, column = j)
+        const int s0 = tile * kCutTile2 + wid * 32;
+        double a0[KB], a1[KB];
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+            const int e = 4 * kb + g;
+            const int sa = s0 + j, sb = s0 + 16 + j;
+            a0[kb] = (sa < P.N && e < P.k) ? P.dv[(size_t)sa * P.k + e] : 0.0;
+            a1[kb] = (sb < P.N && e < P.k) ? P.dv[(size_t)sb * P.k + e] : 0.0;
+        }
+        RowBest rb0, rb1;   // scenario s0 + j / s0 + 16 + j over this lane's vertices v0 + g + 4r (+16)
+        rb0.M = -INFINITY; rb0.SV = -INFINITY; rb0.I = -1; rb0.F = 0;
+        rb1 = rb0;
+
+        // chunk staging by LDS-DMA (global_load_lds_dwordx4, no VGPR round trip): instruction i
+        // of the chunk writes k-rows 4i .. 4i+3 (1 KiB, lane-linear), lane L the 16 bytes of
+        // row 4i + L/16 at LDS position 2 (L % 16); the source vertex pair is that position with
+        // the row's half swap (lds2) applied, so the image is exactly lds2's layout
+        double preb = -INFINITY;
+        auto stage = [&](int buf, int v0) {
+            for (int i = wid; i < KB; i += 4) {
+                const int kk = 4 * i + (lane >> 4);
+                const int vv = (2 * (lane & 15)) ^ ((kk & 1) << 4);
+                __builtin_amdgcn_global_load_lds((const void *)(P.PKTc + (size_t)kk * P.vcap32 + v0 + vv),
+                                                 (__attribute__((address_space(3))) void *)&Bs[buf][i * 4 * kLdsRow2], 16, 0, 0);
+            }
+            if (threadIdx.x < kVT2) preb = v0 + (int)threadIdx.x < P.nv ? P.base[v0 + threadIdx.x] : -INFINITY;
+        };
+        stage(0, 0);
+        if (threadIdx.x < kVT2) bs[0][threadIdx.x] = preb;
+        __syncthreads();            // chunk 0 landed (the barrier drains the DMA)
+        for (int ch = 0; ch < nchunks; ++ch) {
+            const int buf = ch & 1;
+            const int v0 = ch * kVT2;
+            // chunk ch+1 into the other buffer while this one is multiplied (its readers passed
+            // the last barrier)
+            if (ch + 1 < nchunks) stage(buf ^ 1, v0 + kVT2);
+            d4 c00 = {0.0, 0.0, 0.0, 0.0}, c01 = c00, c10 = c00, c11 = c00;   // c[vertex tile][scenario tile]
+            // fragments are read in groups of KG k-blocks ahead of their MFMAs; the scheduling
+            // barrier keeps the compiler from hoisting every read of the chunk (register spills)
+            constexpr int KG = TWOSD_CUT_KG;
+#pragma unroll
+            for (int k0 = 0; k0 < KB; k0 += KG) {
+                double x0[KG], x1[KG];
+#pragma unroll
+                for (int u = 0; u < KG; ++u) {
+                    if (k0 + u < KB) {
+                        x0[u] = Bs[buf][lds2(4 * (k0 + u) + g, j)];
+                        x1[u] = Bs[buf][lds2(4 * (k0 + u) + g, 16 + j)];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < KG; ++u) {
+                    if (k0 + u < KB) {
+                        c00 = __builtin_amdgcn_mfma_f64_16x16x4f64(x0[u], a0[k0 + u], c00, 0, 0, 0);
+                        c01 = __builtin_amdgcn_mfma_f64_16x16x4f64(x0[u], a1[k0 + u], c01, 0, 0, 0);
+                        c10 = __builtin_amdgcn_mfma_f64_16x16x4f64(x1[u], a0[k0 + u], c10, 0, 0, 0);
+                        c11 = __builtin_amdgcn_mfma_f64_16x16x4f64(x1[u], a1[k0 + u], c11, 0, 0, 0);
+                    }
+                }
+                if (TWOSD_CUT_SB) __builtin_amdgcn_sched_barrier(0);
+            }
+            // C/D: register r of a tile is vertex row g + 4r, scenario column j; this lane's
+            // vertices in increasing order: v0 + g + 4r, then v0 + 16 + g + 4r
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int va = v0 + g + 4 * r;
+                const double ba = va < P.nv ? bs[buf][g + 4 * r] : -INFINITY;
+                row_update(rb0, ba + c00[r], va, P.tie_rel);
+                row_update(rb1, ba + c01[r], va, P.tie_rel);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int vb = v0 + 16 + g + 4 * r;
+                const double bb = vb < P.nv ? bs[buf][16 + g + 4 * r] : -INFINITY;
+                row_update(rb0, bb + c10[r], vb, P.tie_rel);
+                row_update(rb1, bb + c11[r], vb, P.tie_rel);
+            }
+            if (ch + 1 < nchunks && threadIdx.x < kVT2) bs[buf ^ 1][threadIdx.x] = preb;
+            __syncthreads();
+        }
+        // combine the 4 lanes (g) of each scenario column: max M, band threshold, lowest candidate
+        // inside the band; a lane whose max reaches the band but whose candidate does not (or
+        // that flagged) -> exact fixup.  Every lane of the column ends with the result.
+        auto combine = [&](RowBest &rb) {
+            double M = rb.M;
+            M = fmax(M, __shfl_xor(M, 16));
+            M = fmax(M, __shfl_xor(M, 32));
+            const double thr = M - tolf(M, P.tie_rel);
+            const bool reach = rb.M != -INFINITY && rb.M >= thr;
+            int it = (reach && rb.SV >= thr) ? rb.I : 0x7fffffff;
+            double st = rb.SV;
+            int fl = reach && (rb.F || !(rb.SV >= thr));
+#pragma unroll
+            for (int o = 16; o <= 32; o <<= 1) {
+                const int i2 = __shfl_xor(it, o);
+                const double s2 = __shfl_xor(st, o);
+                fl |= __shfl_xor(fl, o);
+                if (i2 < it) { it = i2; st = s2; }
+            }
+            rb.I = (M == -INFINITY || it == 0x7fffffff) ? -1 : it;
+            rb.SV = st;
+            rb.F = fl;
+        };
+        combine(rb0);
+        combine(rb1);
+        const int sa = s0 + j, sb = s0 + 16 + j;
+        if (g == 0) {
+            if (sa < P.N) { P.arg[sa] = rb0.I; P.val[sa] = rb0.SV; P.flag[sa] = rb0.F; }
+            if (sb < P.N) { P.arg[sb] = rb1.I; P.val[sb] = rb1.SV; P.flag[sb] = rb1.F; }
+        }
+        const bool ok0 = sa < P.N && !rb0.F && rb0.I >= 0, ok1 = sb < P.N && !rb1.F && rb1.I >= 0;
+        const double p0 = ok0 ? P.w[sa] * P.inv_total : 0.0, p1 = ok1 ? P.w[sb] * P.inv_total : 0.0;
+        // sum p * val and the vertex histogram, scenarios in order (lane 0 reads them from lanes 0-15)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) {
+                const int ok = __shfl(t == 0 ? (int)ok0 : (int)ok1, jj);
+                const int ai = __shfl(t == 0 ? rb0.I : rb1.I, jj);
+                const double pp = __shfl(t == 0 ? p0 : p1, jj);
+                const double vl = __shfl(t == 0 ? rb0.SV : rb1.SV, jj);
+                if (lane == 0 && ok) {
+                    pv_sum = fma(pp, vl, pv_sum);
+                    const unsigned long long hq = (unsigned long long)__double2ull_rn(pp * kFix);
+                    if (P.hist_lds) __hip_atomic_fetch_add(&hl[ai], hq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    else atomicAdd(&P.hist[ai], hq);
+                }
+            }
+        }
+        // S_e = sum_w p_w PK[a(w), e] dv[w, e] from the delta registers: lane (g, j) holds
+        // scenario j's e = 4 kb + g and its pick; the 16 scenarios of a tile are summed by a
+        // fixed xor tree, lane (g, kb mod 16) keeps the sum
+        auto s_pass = [&](const double (&a)[KB], bool ok, int ai, double pp) {
+            const double *pk = P.PK + (size_t)(ok ? ai : 0) * P.k4;
+            const double pu = ok ? pp : 0.0;
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb) {
+                const int e = 4 * kb + g;
+                double v = (e < P.k) ? pu * pk[e] * a[kb] : 0.0;
+#pragma unroll
+                for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o);
+                if (j == (kb & 15)) {
+                    if (kb < 16) Sacc[0] += v;
+                    else Sacc[1] += v;
+                }
+            }
+        };
+        s_pass(a0, ok0, rb0.I, p0);
+        s_pass(a1, ok1, rb1.I, p1);
+    }
+    if (P.hist_lds) {
+        __syncthreads();
+        for (int v = threadIdx.x; v < P.nv; v += 256) P.hist_part[(size_t)blockIdx.x * P.nv + v] = hl[v];
+    }
+    const int slot = blockIdx.x * 4 + wid;
+    double *out = P.partial + (size_t)slot * (P.k + 1);
+    if (lane == 0) out[0] = pv_sum;
+    // lane (g, j) owns e = 4 j + g (kb = j) and e = 4 (j + 16) + g (kb = j + 16)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int e = 4 * (j + 16 * t) + g;
+        if (e < P.k) out[1 + e] = Sacc[t];
+    }
+}
+
 // hist[v] += sum over blocks of the block histograms (integers: exact in any order)
 __global__ void __launch_bounds__(256) cut_hist_reduce_kernel(int nb, int nv, const unsigned long long *__restrict__ part,
                                                               unsigned long long *__restrict__ hist) {
@@ -376,6 +594,8 @@ __global__ void cut_g_final_kernel(int nb, int m, const double *__restrict__ gpa
 // ---------------------------------------------------------------------------------
 struct CutWs {
     double *PK = nullptr, *PKT = nullptr;
+    double *PKTc = nullptr;
+    size_t pktc_cap = 0;
     int pk_count = 0, pk_vcap = 0, pk_k4 = 0;
     size_t pk_cap = 0;
     int *rows = nullptr;
@@ -399,7 +619,7 @@ static CutWs *cws(twosd_ctx *c) {
 void cut_free(twosd_ctx *c) {
     if (!c->cut_ws) return;
     CutWs *w = (CutWs *)c->cut_ws;
-    hipFree(w->PK); hipFree(w->PKT); hipFree(w->rows); hipFree(w->coef); hipFree(w->bvec); hipFree(w->base);
+    hipFree(w->PK); hipFree(w->PKT); hipFree(w->PKTc); hipFree(w->rows); hipFree(w->coef); hipFree(w->bvec); hipFree(w->base);
     hipFree(w->partial); hipFree(w->sums); hipFree(w->gpart); hipFree(w->g); hipFree(w->arg); hipFree(w->flag);
     hipFree(w->val); hipFree(w->hist); hipFree(w->part2); hipFree(w->hist_part);
     delete w;
@@ -436,10 +656,20 @@ static int kb_for(int k4) {
     return -1;
 }
 
+// kernel version: 2 = cut_argmax2_kernel (default), 1 = cut_argmax_kernel (TWOSD_CUT_V=1)
+static int cut_version() {
+    static const int v = getenv("TWOSD_CUT_V") ? atoi(getenv("TWOSD_CUT_V")) : 2;
+    return v == 1 ? 1 : 2;
+}
+
 template <int KB>
 static void launch_argmax_t(const CutParams &P, int nblocks, hipStream_t s) {
-    hipLaunchKernelGGL(cut_argmax_kernel<KB>, dim3(nblocks), dim3(256), P.hist_lds ? sizeof(unsigned long long) * P.nv : 0,
-                       s, P);
+    if (cut_version() == 2)
+        hipLaunchKernelGGL(cut_argmax2_kernel<KB>, dim3(nblocks), dim3(256), P.hist_lds ? sizeof(unsigned long long) * P.nv : 0,
+                           s, P);
+    else
+        hipLaunchKernelGGL(cut_argmax_kernel<KB>, dim3(nblocks), dim3(256), P.hist_lds ? sizeof(unsigned long long) * P.nv : 0,
+                           s, P);
 }
 
 // resident blocks per CU of one instantiation (registers and LDS): the persistent grid is
@@ -448,7 +678,11 @@ static void launch_argmax_t(const CutParams &P, int nblocks, hipStream_t s) {
 template <int KB>
 static int argmax_occupancy_t(size_t dyn_lds) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cut_argmax_kernel<KB>, 256, dyn_lds) != hipSuccess) nb = 0;
+    if (cut_version() == 2) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cut_argmax2_kernel<KB>, 256, dyn_lds) != hipSuccess) nb = 0;
+    } else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cut_argmax_kernel<KB>, 256, dyn_lds) != hipSuccess) {
+        nb = 0;
+    }
     return nb;
 }
 
@@ -548,7 +782,7 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     }
     HIPCHK(hipMemcpyAsync(w->coef, coef.data(), sizeof(double) * k4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(w->bvec, bvec.data(), sizeof(double) * m, hipMemcpyHostToDevice, c->stream));
-    const int ntiles = (N + kCutTile - 1) / kCutTile;
+    const int ntiles = (N + (cut_version() == 2 ? kCutTile2 : kCutTile) - 1) / (cut_version() == 2 ? kCutTile2 : kCutTile);
     // blocks per CU: resident occupancy of this instantiation (TWOSD_CUT_BPC overrides; the
     // |V| <= kHistLds case adds the LDS histogram, at most 2 KB)
     static const int bpc_env = getenv("TWOSD_CUT_BPC") ? atoi(getenv("TWOSD_CUT_BPC")) : 0;
@@ -576,6 +810,18 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     P.hist_part = w->hist_part;
     P.tie_rel = tie_rel; P.inv_total = 1.0 / total_weight;
     P.dv = E.d_dv; P.w = E.d_w; P.coef = w->coef; P.PK = w->PK; P.PKT = w->PKT; P.base = w->base;
+    if (cut_version() == 2) {
+        const int vcap32 = (nv + 31) & ~31, rows = 4 * KB;
+        if ((size_t)rows * vcap32 > w->pktc_cap) {
+            if ((rc = realloc_dev(&w->PKTc, (size_t)rows * vcap32))) return rc;
+            w->pktc_cap = (size_t)rows * vcap32;
+        }
+        const size_t tot = (size_t)rows * vcap32;
+        hipLaunchKernelGGL(cut_pktc_kernel, dim3((unsigned)std::min<size_t>(4096, (tot + 255) / 256)), dim3(256), 0, c->stream, nv, k,
+                           rows, w->pk_vcap, vcap32, w->PKT, w->coef, w->PKTc);
+        P.PKTc = w->PKTc;
+        P.vcap32 = vcap32;
+    }
     P.arg = w->arg; P.val = w->val; P.flag = w->flag; P.hist = d_hist; P.partial = w->partial;
     launch_argmax(KB, P, nblocks, c->stream);
     if (P.hist_lds)

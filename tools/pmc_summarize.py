@@ -43,16 +43,20 @@ def main():
             if k:
                 d = (float(r["End_Timestamp"]) - float(r["Start_Timestamp"])) / 1e6
                 dur[k] = max(dur.get(k, 0.0), d)
-    # timed-region stats: the trace run is bench.py --steps 2 --warmup 1, and every step starts
-    # with pool_xbase_kernel (invalidate_x), so the last two of those open the timed steps;
-    # per kernel: launches, average and total duration inside that region (the numbers the
-    # bench's HIP events time)
+    # timed-region stats: the trace run is bench.py --steps K --warmup 1 --spot 0 (K = 4 by
+    # default), one cut_argmax_kernel launch per step, so the timed steps start after the
+    # (K+1)-th last of those (the warmup's) and the cut kernels trailing it; per kernel:
+    # launches, average and total duration inside that region (what the bench's events time)
+    steps = int(sys.argv[4]) if len(sys.argv) > 4 else 4
     if traces:
         rows = sorted(csv.DictReader(open(traces[0])), key=lambda r: int(r["Start_Timestamp"]))
-        starts = [i for i, r in enumerate(rows) if "pool_xbase_kernel" in r["Kernel_Name"]]
-        if len(starts) >= 2:
+        cuts = [i for i, r in enumerate(rows) if "cut_argmax_kernel" in r["Kernel_Name"]]
+        if len(cuts) >= steps + 1:
+            i0 = cuts[-steps - 1] + 1
+            while i0 < len(rows) and "cut_" in rows[i0]["Kernel_Name"]:
+                i0 += 1
             agg = defaultdict(list)
-            for r in rows[starts[-2]:]:
+            for r in rows[i0:]:
                 agg[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
             with open(os.path.join(dst, "timed_kernel_stats.csv"), "w", newline="") as fh:
                 wr = csv.writer(fh)
@@ -62,7 +66,7 @@ def main():
                                  round(max(ds), 6)])
     pmc = defaultdict(lambda: defaultdict(list))
     scratch = {}
-    for tag in ("pmc_fetch", "pmc_write"):
+    for tag in ("pmc_fetch", "pmc_write", "pmc_mfma"):
         fs = glob.glob(os.path.join(src, tag, "**", "*counter_collection.csv"), recursive=True)
         if not fs:
             continue
@@ -73,7 +77,8 @@ def main():
                 pmc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
                 scratch[k] = int(float(r["Scratch_Size"]))
     out = {"workload": f"storm {scen} scenarios, bench.py defaults, 1 MI355X",
-           "source": "rocprofv3 --kernel-trace --stats; separate --pmc FETCH_SIZE / --pmc WRITE_SIZE passes (tools/profile_round.sh)",
+           "source": "rocprofv3 --kernel-trace --stats; separate --pmc FETCH_SIZE / --pmc WRITE_SIZE / fp64 MFMA passes "
+                     "(tools/profile_round.sh)",
            "correction": "FETCH_SIZE/WRITE_SIZE are KiB; gfx950 FETCH_SIZE counts 1/2 of wide coalesced reads, so "
                          "hbm_bytes = 1024*(2*FETCH_SIZE + WRITE_SIZE) (upper estimate for narrow accesses)",
            "scenarios": scen, "kernels": {}}
@@ -87,6 +92,18 @@ def main():
             w = max(c.get("WRITE_SIZE", [0.0]))
             e.update({"FETCH_SIZE_KiB": f, "WRITE_SIZE_KiB": w, "hbm_bytes_per_launch": 1024.0 * (2 * f + w),
                       "scratch_bytes_per_lane": scratch.get(k)})
+        if c and "SQ_INSTS_VALU_MFMA_MOPS_F64" in c:
+            mops = max(c["SQ_INSTS_VALU_MFMA_MOPS_F64"])
+            busy = max(c.get("SQ_VALU_MFMA_BUSY_CYCLES", [0.0]))
+            gui = max(c.get("GRBM_GUI_ACTIVE", [0.0]))
+            e.update({"SQ_INSTS_VALU_MFMA_MOPS_F64": mops, "SQ_INSTS_VALU_MFMA_F64": max(c.get("SQ_INSTS_VALU_MFMA_F64", [0.0])),
+                      "SQ_VALU_MFMA_BUSY_CYCLES": busy, "SQ_BUSY_CYCLES": max(c.get("SQ_BUSY_CYCLES", [0.0])),
+                      "GRBM_GUI_ACTIVE": gui, "mfma_f64_flops": 512.0 * mops})
+            if dur.get(k):
+                e["mfma_f64_tflops_counted"] = 512.0 * mops / (dur[k] * 1e-3) / 1e12
+                e["mfma_util"] = e["mfma_f64_tflops_counted"] / 78.6   # counted MFMA flops / kernel time vs the fp64 spec
+            if gui > 0:
+                e["mfma_busy_frac"] = busy / (gui * 4.0 * 256.0 / 8.0)   # per-SIMD busy cycles / (GRBM cycles (8 XCDs) x SIMDs)
         out["kernels"][k] = e
     with open(os.path.join(dst, "pmc_summary.json"), "w") as fh:
         json.dump(out, fh, indent=1)
