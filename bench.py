@@ -385,7 +385,7 @@ def main():
                      "note": "fp64 peak (vector == matrix on gfx950); achieved = counted fp64 FLOPs of the executed pivot path / LP kernel time",
                      "achieved": lp_tflops, "peak": PEAK_FP64_TFS, "unit": "TFLOP/s",
                      "frac": lp_tflops / PEAK_FP64_TFS, "traffic": None},
-        "cutgen": {"kernel": "cut_argmax_kernel (+vbase/fixup/reduce)", "hbm_gbs": cut_gbs,
+        "cutgen": {"kernel": "cut_argmax2_kernel (+pktc/vbase/fixup/reduce)", "hbm_gbs": cut_gbs,
                    "bytes_alg": bytes_alg, "flops_alg": flops_alg, "t_roof_ms": t_roof * 1e3,
                    "t_ms": cut_us / 1e3, "frac": t_roof / (cut_us * 1e-6),
                    "mfma_tflops": flops_alg / (cut_us * 1e-6) / 1e12,
@@ -400,11 +400,14 @@ def main():
         if kl:
             out["roofline"]["traffic"] = kl["hbm_bytes_per_launch"]
             out["roofline"]["traffic_source"] = pmc["file"]
-        kc = pmc["kernels"].get("cut_argmax_kernel")
+        kc = pmc["kernels"].get("cut_argmax2_kernel") or pmc["kernels"].get("cut_argmax_kernel")
         if kc:
             out["cutgen"]["traffic"] = kc["hbm_bytes_per_launch"]
+            if "hbm_bytes_per_launch_raw" in kc:
+                out["cutgen"]["traffic_raw"] = kc["hbm_bytes_per_launch_raw"]
             if "mfma_util" in kc:
-                out["cutgen"]["mfma_util"] = kc["mfma_util"]
+                out["cutgen"]["mfma_util"] = kc["mfma_util"]            # counted MFMA flops / time / 78.6 TF
+                out["cutgen"]["mfma_busy_frac"] = kc.get("mfma_busy_frac")   # SQ_VALU_MFMA_BUSY_CYCLES / SIMD cycles
             out["cutgen"]["traffic_source"] = pmc["file"]
     if rank == 0 and world == 1 and args.spot > 0:
         out["parity_spot_check"] = spot_check(sp2, ctx, epi, V, xs, x_iters, positions, args)

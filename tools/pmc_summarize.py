@@ -18,8 +18,8 @@ import shutil
 import sys
 from collections import defaultdict
 
-KERNELS = ["lp_hyper_kernel", "pool_select_kernel", "pool_refine_kernel", "pool_selstream_kernel", "pool_xbase_kernel", "cut_argmax_kernel", "cut_fixup_kernel", "cut_vbase_kernel",
-           "cut_pk_kernel", "dvs_batch_kernel", "dvs_lookup_kernel", "dvs_assign_kernel"]
+KERNELS = ["lp_hyper_kernel", "pool_select_kernel", "pool_refine_kernel", "pool_selstream_kernel", "pool_xbase_kernel", "cut_argmax2_kernel", "cut_argmax_kernel", "cut_fixup_kernel", "cut_vbase_kernel",
+           "cut_pk_kernel", "cut_pktc_kernel", "vkey_insert_kernel", "dvs_batch_kernel", "dvs_lookup_kernel", "dvs_assign_kernel"]
 
 
 def short(name):
@@ -50,7 +50,7 @@ def main():
     steps = int(sys.argv[4]) if len(sys.argv) > 4 else 4
     if traces:
         rows = sorted(csv.DictReader(open(traces[0])), key=lambda r: int(r["Start_Timestamp"]))
-        cuts = [i for i, r in enumerate(rows) if "cut_argmax_kernel" in r["Kernel_Name"]]
+        cuts = [i for i, r in enumerate(rows) if "cut_argmax" in r["Kernel_Name"]]
         if len(cuts) >= steps + 1:
             i0 = cuts[-steps - 1] + 1
             while i0 < len(rows) and "cut_" in rows[i0]["Kernel_Name"]:
@@ -79,8 +79,10 @@ def main():
     out = {"workload": f"storm {scen} scenarios, bench.py defaults, 1 MI355X",
            "source": "rocprofv3 --kernel-trace --stats; separate --pmc FETCH_SIZE / --pmc WRITE_SIZE / fp64 MFMA passes "
                      "(tools/profile_round.sh)",
-           "correction": "FETCH_SIZE/WRITE_SIZE are KiB; gfx950 FETCH_SIZE counts 1/2 of wide coalesced reads, so "
-                         "hbm_bytes = 1024*(2*FETCH_SIZE + WRITE_SIZE) (upper estimate for narrow accesses)",
+           "correction": "FETCH_SIZE/WRITE_SIZE are KiB; gfx950 FETCH_SIZE counts 1/2 of wide coalesced (16 B/lane) reads, "
+                         "so hbm_bytes = 1024*(2*FETCH_SIZE + WRITE_SIZE) (the guide's correction; an upper estimate for "
+                         "narrow accesses); hbm_bytes_raw = 1024*(FETCH_SIZE + WRITE_SIZE) is the estimate for kernels "
+                         "whose reads are 8 B per lane (the cut kernel's delta loads)",
            "scenarios": scen, "kernels": {}}
     for k in KERNELS:
         c = pmc.get(k)
@@ -91,6 +93,7 @@ def main():
             f = max(c.get("FETCH_SIZE", [0.0]))
             w = max(c.get("WRITE_SIZE", [0.0]))
             e.update({"FETCH_SIZE_KiB": f, "WRITE_SIZE_KiB": w, "hbm_bytes_per_launch": 1024.0 * (2 * f + w),
+                      "hbm_bytes_per_launch_raw": 1024.0 * (f + w),
                       "scratch_bytes_per_lane": scratch.get(k)})
         if c and "SQ_INSTS_VALU_MFMA_MOPS_F64" in c:
             mops = max(c["SQ_INSTS_VALU_MFMA_MOPS_F64"])
