@@ -102,8 +102,10 @@ def main():
     ap.add_argument("--refresh", type=int, default=1,
                     help="1: a step at an x other than the pool's rebuilds the pool there (twosd_pool_refresh + "
                          "candidate lists, inside the timed step); 0: keep the x_EV pool for every x")
-    ap.add_argument("--refresh-train", type=int, default=16384, help="training scenarios of a pool refresh")
-    ap.add_argument("--refresh-pool", type=int, default=4096, help="pool size after a refresh")
+    ap.add_argument("--refresh-train", type=int, default=0,
+                    help="training scenarios of a pool refresh (0: 4 x the refresh pool)")
+    ap.add_argument("--refresh-pool", type=int, default=0,
+                    help="pool size after a refresh (0: by the per-rank shard, 4096 per 1M scenarios, at least 512)")
     ap.add_argument("--cpu-pool", type=int, default=128, help="bases of the pooled CPU baseline (0: off)")
     ap.add_argument("--pool", type=int, default=0,
                     help="warm-start basis pool size (1 = primary basis only; 0 = by the per-rank shard: "
@@ -234,6 +236,12 @@ def main():
     nv = len(V)
 
     X = len(xs)
+    # refresh size by the per-rank shard: the refresh is a fixed cost per step (training solves,
+    # B^-1 composition, upload grow with the pool), so a smaller shard takes a smaller pool
+    if args.refresh_pool <= 0:
+        args.refresh_pool = max(512, min(4096, int(4096 * n_local * E / 1_000_000) // 256 * 256))
+    if args.refresh_train <= 0:
+        args.refresh_train = 4 * args.refresh_pool
     # pool refresh training scenarios (stream seed + 4, identical on every rank)
     rtr = None
     if args.refresh:
@@ -248,9 +256,12 @@ def main():
             return 0.0
         t0 = time.perf_counter()
         ctx.pool_refresh(rtr, xx, 0, args.refresh_train, args.refresh_pool)
+        t1 = time.perf_counter()
         if args.pool_level1 > 0 and ctx.pool_size() > args.pool_level1:
             ctx.pool_build_candidates(rtr, xx, 0, args.refresh_train, args.pool_level1, args.pool_cands)
         pool_at["x"] = xx.copy()
+        # [training solves, re-solves, composition, upload, refresh total, candidate lists] ms
+        pool_at["last_ms"] = list(ctx.last_refresh_ms()) + [1e3 * (time.perf_counter() - t1)]
         return time.perf_counter() - t0
 
     heads_at = {}    # first pool bases at each x point (the pooled CPU baseline starts from the same bases)
@@ -259,6 +270,8 @@ def main():
         t_ref = refresh(xx)
         if rec:
             per_x[cur["xi"]]["refresh"] += t_ref
+            if t_ref > 0:
+                per_x[cur["xi"]]["refresh_parts"] = [round(v, 2) for v in pool_at["last_ms"]]
             if cur["xi"] not in heads_at and not args.no_cpu and rank == 0:
                 heads_at[cur["xi"]] = np.stack([ctx.pool_get(p) for p in range(min(args.cpu_pool, ctx.pool_size()))])
         ctx.invalidate_x()     # every pass pays its per-x setup (x_B of the pool, selection data)
@@ -342,6 +355,7 @@ def main():
                  "steps": px["steps"],
                  "ms_per_step": 1e3 * px["wall"] / max(px["steps"], 1),
                  "pool_refresh_ms": 1e3 * px["refresh"] / max(px["steps"], 1),
+                 "pool_refresh_parts_ms": px.get("refresh_parts"),
                  "lp_kernel_ms": px["lp"] / 1e3 / max(px["steps"], 1),
                  "lp_pivots_mean": px["piv"] / max(px["n"], 1),
                  "alpha": px["alpha"]}

@@ -209,6 +209,7 @@ static void free_template(twosd_ctx *c) {
     c->dcap.clear();
     dfree(c->d_vkey); c->vkey_cap = 0;
     dfree(c->d_bkey); c->bkey_cap = 0;
+    dfree(c->d_refresh_sel); c->refresh_sel_cap = 0; c->box_epi = -1;
     dfree(c->d_eo_pb); dfree(c->d_eo_K); dfree(c->d_eo_off); dfree(c->d_eo_etap); dfree(c->d_eo_etaoff);
     dfree(c->d_eo_eidx); dfree(c->d_eo_evals); dfree(c->d_eo_used); c->eo_rows = c->eo_cap = 0; c->eo_kmax = 0;
     c->has_template = c->has_basis = false;
@@ -502,6 +503,7 @@ static int install_basis(twosd_ctx *c, const std::vector<int> &head) {
     c->pool.clear();
     c->sel_lo.clear();
     c->sel_hi.clear();
+    c->box_epi = -1;
     c->pool.push_back(std::move(pb));
     if ((rc = upload_pool(c))) return rc;
     c->has_basis = true;
@@ -604,6 +606,7 @@ extern "C" int twosd_pool_build(twosd_ctx *c, int epi, const double *x, int firs
     if (count > 0 && c->k > 0) {   // training box of the deltas (selection row pruning)
         std::vector<double> dv((size_t)count * c->k);
         HIPCHK(hipMemcpy(dv.data(), E.d_dv + (size_t)first * c->k, sizeof(double) * dv.size(), hipMemcpyDeviceToHost));
+        c->box_epi = -1;   // the refresh's cached box no longer applies
         c->sel_lo.assign(c->k, INFINITY);
         c->sel_hi.assign(c->k, -INFINITY);
         for (int s = 0; s < count; ++s)
@@ -733,6 +736,7 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
         HIPCHK(hipMemcpy(reps.data(), d_list, sizeof(int) * U, hipMemcpyDeviceToHost));
         HIPCHK(hipMemcpy(cnts.data(), d_counts, sizeof(int) * U, hipMemcpyDeviceToHost));
     }
+    const auto t1b = std::chrono::steady_clock::now();
     std::vector<int> ord(U);
     for (int a = 0; a < U; ++a) ord[a] = a;
     std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return cnts[a] > cnts[b]; });
@@ -742,8 +746,11 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
     std::vector<PoolBasis> fresh;
     if (R > 0) {
         // 3. re-solve the selected scenarios (same starts, so the same pivots) with their eta files
-        int *d_sel = nullptr;
-        if ((rc = dalloc(&d_sel, (size_t)R))) return rc;
+        if ((size_t)R > c->refresh_sel_cap) {
+            if ((rc = dalloc(&c->d_refresh_sel, (size_t)R))) return rc;
+            c->refresh_sel_cap = R;
+        }
+        int *d_sel = c->d_refresh_sel;
         HIPCHK(hipMemcpy(d_sel, sel.data(), sizeof(int) * R, hipMemcpyHostToDevice));
         LpRun r;
         r.d_list = d_sel;
@@ -751,7 +758,6 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
         r.want_etas = true;
         r.want_head = true;
         rc = run_lp_ex(c, x, d_dv, count, r);
-        hipFree(d_sel);
         if (rc) return rc;
         const int kmax = c->eo_kmax;
         std::vector<int> pb(R), K(R), off(R), etap((size_t)R * kmax), etaoff((size_t)R * (kmax + 1)), heads((size_t)R * m);
@@ -798,12 +804,17 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
         for (int a = 0; a < R; ++a)
             if (ok[a]) keep.push_back(std::move(fresh[a]));
         c->pool.swap(keep);
+        // the old pool's host data is released on a helper thread (thousands of vectors)
+        std::thread([old = std::move(keep)]() mutable { old.clear(); }).detach();
     } else {
         c->pool.resize(1);
         c->last_refresh_ms[1] = c->last_refresh_ms[2] = 0.0;
     }
-    // training box of the deltas (selection row pruning), as twosd_pool_build
-    if (c->k > 0) {
+    const auto tb = std::chrono::steady_clock::now();
+    // training box of the deltas (selection row pruning), as twosd_pool_build; cached per
+    // training range
+    if (c->k > 0 && !(c->box_epi == epi && c->box_first == first && c->box_count == count && c->box_n == E.count)) {
+        c->box_epi = epi; c->box_first = first; c->box_count = count; c->box_n = E.count;
         std::vector<double> dv((size_t)count * c->k);
         HIPCHK(hipMemcpy(dv.data(), d_dv, sizeof(double) * dv.size(), hipMemcpyDeviceToHost));
         c->sel_lo.assign(c->k, INFINITY);
@@ -815,8 +826,15 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
             }
     }
     const auto tu = std::chrono::steady_clock::now();
-    if ((rc = upload_pool(c)) || (rc = prepare_elements(c))) return rc;
+    if ((rc = upload_pool(c))) return rc;
+    const auto tua = std::chrono::steady_clock::now();
+    if ((rc = prepare_elements(c))) return rc;
     const auto t3 = std::chrono::steady_clock::now();
+    if (getenv("TWOSD_DEBUG")) {
+        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        fprintf(stderr, "pool_refresh: train %.2f, keys %.2f, re-solve+compose %.2f, box %.2f, upload_pool %.2f, elements %.2f ms (R=%d)\n",
+                ms(t0, t1), ms(t1, t1b), ms(t1b, tb), ms(tb, tu), ms(tu, tua), ms(tua, t3), R);
+    }
     c->last_refresh_ms[0] = std::chrono::duration<double, std::milli>(t1 - t0).count();
     c->last_refresh_ms[3] = std::chrono::duration<double, std::milli>(t3 - tu).count();
     c->last_refresh_ms[4] = std::chrono::duration<double, std::milli>(t3 - t0).count();

@@ -140,6 +140,9 @@ struct twosd_ctx {
     size_t eo_rows = 0, eo_cap = 0;
     int eo_kmax = 0;
     double last_refresh_ms[5] = {0, 0, 0, 0, 0};   // train solves, re-solves, compose, upload, total
+    int *d_refresh_sel = nullptr;                  // refresh: scenarios to re-solve
+    size_t refresh_sel_cap = 0;
+    int box_epi = -1, box_first = -1, box_count = -1, box_n = -1;   // training range of sel_lo / sel_hi
     // pinned host staging buffers of the pool upload, kept across uploads (no page faults,
     // no unmapping per refresh, page-locked copies)
     void *stage[16] = {};
