@@ -161,9 +161,10 @@ static int upload_raw(T **d, const T *h, size_t n) {
     return TWOSD_OK;
 }
 
-// grow-only device array (no hipFree / hipMalloc when the new contents fit)
+// grow-only device array of at least n elements (no hipFree / hipMalloc when they fit;
+// contents not kept on growth)
 template <typename T>
-static int upload_big(twosd_ctx *c, T **d, const T *h, size_t n) {
+static int dev_reserve(twosd_ctx *c, T **d, size_t n) {
     size_t &cap = c->dcap[(const void *)d];
     if (!*d || cap < std::max<size_t>(n, 1)) {
         const size_t want = std::max<size_t>(n, 1) + std::max<size_t>(n, 1) / 4;
@@ -171,7 +172,31 @@ static int upload_big(twosd_ctx *c, T **d, const T *h, size_t n) {
         if (rc) { cap = 0; return rc; }
         cap = want;
     }
+    return TWOSD_OK;
+}
+template <typename T>
+static int upload_big(twosd_ctx *c, T **d, const T *h, size_t n) {
+    int rc = dev_reserve(c, d, n);
+    if (rc) return rc;
     if (n) HIPCHK(hipMemcpy(*d, h, sizeof(T) * n, hipMemcpyHostToDevice));
+    return TWOSD_OK;
+}
+template <typename T>
+static int upload_big(twosd_ctx *c, T **d, const std::vector<T> &h) {
+    return upload_big(c, d, h.data(), h.size());
+}
+
+// device selection-stream outputs of a pool of P bases with `records` records (prepare_x
+// writes them per x)
+static int reserve_selection(twosd_ctx *c, int P, int records) {
+    int rc;
+    if ((size_t)std::max(records, 1) > c->sel_code_cap) {
+        dfree(c->d_sel_code);
+        if ((rc = dalloc(&c->d_sel_code, 2 * (size_t)std::max(records, 1)))) return rc;
+        c->sel_code_cap = std::max(records, 1);
+    }
+    if ((rc = dev_reserve(c, &c->d_sel_end, (size_t)P)) || (rc = dev_reserve(c, &c->d_sel_cinf, (size_t)P))) return rc;
+    c->sel_cap_total = records;
     return TWOSD_OK;
 }
 
@@ -212,6 +237,8 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_refresh_sel); c->refresh_sel_cap = 0; c->box_epi = -1;
     dfree(c->d_eo_pb); dfree(c->d_eo_K); dfree(c->d_eo_off); dfree(c->d_eo_etap); dfree(c->d_eo_etaoff);
     dfree(c->d_eo_eidx); dfree(c->d_eo_evals); dfree(c->d_eo_used); c->eo_rows = c->eo_cap = 0; c->eo_kmax = 0;
+    dfree(c->d_pg_D); dfree(c->d_pg_amax); dfree(c->d_pg_d0p); dfree(c->d_pg_cnt); dfree(c->d_pg_tot);
+    dfree(c->d_pg_valid); dfree(c->d_pg_head0); dfree(c->d_pg_map); dfree(c->d_pg_off); dfree(c->d_pg_pos);
     c->has_template = c->has_basis = false;
 }
 
@@ -413,12 +440,60 @@ static int make_pool_basis(twosd_ctx *c, const std::vector<int> &head, PoolBasis
     return why ? fail(TWOSD_E_ARG, "%s", why) : TWOSD_OK;
 }
 
+// pi0 = c_B' B^{-1} from the CSR rows (rows ascending)
+static void pi0_from_rows(const twosd_ctx *c, PoolBasis &B) {
+    const HostLP &L = c->L;
+    const int m = L.m, n = L.n;
+    B.pi0.assign(m, 0.0);
+    for (int i = 0; i < m; ++i) {
+        const int j = B.head[i];
+        const double cb = j < n ? L.q[j] : 0.0;
+        if (cb == 0.0) continue;
+        for (int q = B.rptr[i]; q < B.rptr[i + 1]; ++q) B.pi0[B.rcol[q]] += cb * B.rval[q];
+    }
+}
+
+// host CSR rows and pi0 of the bases a device refresh built (dev_only), read back from the
+// pool arrays: upload_pool, prepare_elements and the host compose work on the host forms
+static int ensure_host_pool(twosd_ctx *c) {
+    const int P = (int)c->pool.size(), MP = c->MP, m = c->L.m;
+    int last = -1;
+    for (int p = 0; p < P; ++p)
+        if (c->pool[p].dev_only) last = p;
+    if (last < 0) return TWOSD_OK;
+    const int Pd = last + 1;
+    std::vector<int> rp((size_t)Pd * (MP + 1));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpy(rp.data(), c->d_brptr, sizeof(int) * rp.size(), hipMemcpyDeviceToHost));
+    size_t nz = 0;
+    for (int p = 0; p < Pd; ++p) nz = std::max(nz, (size_t)rp[(size_t)p * (MP + 1) + m]);
+    std::vector<int> col(std::max<size_t>(nz, 1));
+    std::vector<double> val(std::max<size_t>(nz, 1));
+    if (nz) {
+        HIPCHK(hipMemcpy(col.data(), c->d_brcol, sizeof(int) * nz, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(val.data(), c->d_brval, sizeof(double) * nz, hipMemcpyDeviceToHost));
+    }
+    parallel_for(Pd, [&](int p) {
+        PoolBasis &B = c->pool[p];
+        if (!B.dev_only) return;
+        const int *r = rp.data() + (size_t)p * (MP + 1);
+        B.rptr.resize(m + 1);
+        for (int i = 0; i <= m; ++i) B.rptr[i] = r[i] - r[0];
+        B.rcol.assign(col.begin() + r[0], col.begin() + r[m]);
+        B.rval.assign(val.begin() + r[0], val.begin() + r[m]);
+        pi0_from_rows(c, B);
+        B.dev_only = false;
+    });
+    return TWOSD_OK;
+}
+
 // Upload the hypersparse-kernel form of every pool basis, pool-strided (pool[0] first, so
 // the leading MP / 64 / 64C entries are the primary basis): hb0 (MP), basic0 (64),
 // d0 (64C), B^{-1} columns as CSC (bcp absolute into the concatenated bci/bcv),
 // B^{-1} rows as CSR (brptr absolute into the concatenated brcol/brval).
 static int upload_pool(twosd_ctx *c) {
     const auto t_up0 = std::chrono::steady_clock::now();
+    if (int rc0 = ensure_host_pool(c)) return rc0;
     const HostLP &L = c->L;
     const int m = L.m, n = L.n, MP = c->MP, P = (int)c->pool.size();
     std::vector<int8_t> bt(n + m);
@@ -474,10 +549,10 @@ static int upload_pool(twosd_ctx *c) {
     });
     const auto tc = std::chrono::steady_clock::now();
     int rc;
-    if ((rc = upload(&c->d_hb0, hb)) || (rc = upload(&c->d_basic0, basic)) || (rc = upload(&c->d_bnnz, bnnz))) return rc;
+    if ((rc = upload_big(c, &c->d_hb0, hb)) || (rc = upload_big(c, &c->d_basic0, basic)) || (rc = upload_big(c, &c->d_bnnz, bnnz))) return rc;
     if (c->CH > 0) {
-        if ((rc = upload(&c->d_bcp, cp_all)) || (rc = upload_big(c, &c->d_bci, ci_all, ro[P])) ||
-            (rc = upload_big(c, &c->d_bcv, cv_all, ro[P])) || (rc = upload(&c->d_brptr, rp_all)) ||
+        if ((rc = upload_big(c, &c->d_bcp, cp_all)) || (rc = upload_big(c, &c->d_bci, ci_all, ro[P])) ||
+            (rc = upload_big(c, &c->d_bcv, cv_all, ro[P])) || (rc = upload_big(c, &c->d_brptr, rp_all)) ||
             (rc = upload_big(c, &c->d_brcol, rc_all, ro[P])) || (rc = upload_big(c, &c->d_brval, rv_all, ro[P])) ||
             (rc = upload_big(c, &c->d_d0, d0_all, (size_t)P * 64 * c->CH)))
             return rc;
@@ -696,17 +771,120 @@ static int prepare_elements(twosd_ctx *c);
 // basis is usable
 static const char *finish_composed(const twosd_ctx *c, PoolBasis &B) {
     const HostLP &L = c->L;
-    const int m = L.m, n = L.n;
-    B.pi0.assign(m, 0.0);
-    for (int i = 0; i < m; ++i) {
-        const int j = B.head[i];
-        const double cb = j < n ? L.q[j] : 0.0;
-        if (cb == 0.0) continue;
-        for (int q = B.rptr[i]; q < B.rptr[i + 1]; ++q) B.pi0[B.rcol[q]] += cb * B.rval[q];
-    }
+    pi0_from_rows(c, B);
     if (sparse_dual_infeasibility(L, B.head, B.pi0) > 1e-7) return "composed basis is not dual feasible";
     if (sparse_basis_residual(L, B.head, B.rptr, B.rcol, B.rval, 4) > 1e-8) return "composed B^{-1} inconsistent";
     return nullptr;
+}
+
+// Device build of the refreshed pool (pool_gpu.hip) from the re-solve's eta files and heads
+// (list positions 0..R-1 in c->d_eo_* / c->d_head_out): sources a = 0 (primary) .. R, composed
+// and checked in batches that fit the dense scratch, then the sources that passed are written
+// in order as pool[0..P) -- the arrays upload_pool + prepare_elements would produce.  One
+// batch (the start pool's CSC is overwritten by the fill); returns 1, with nothing changed, when
+// the sources do not fit the scratch or the primary fails the checks (then the host composes).
+static int refresh_build_device(twosd_ctx *c, int R) {
+    const HostLP &L = c->L;
+    const int m = L.m, n = L.n, MP = c->MP, nsrc = R + 1, W = pg_tile_width(m);
+    const size_t per = (size_t)m * m;
+    size_t freeb = 0, totalb = 0;
+    HIPCHK(hipMemGetInfo(&freeb, &totalb));
+    const size_t budget = std::min<size_t>(freeb / 3, (size_t)12 << 30);
+    const int NB = (int)std::max<size_t>(1, std::min<size_t>(nsrc, budget / (per * sizeof(double))));
+    if (W == 0 || NB < nsrc) return 1;   // does not fit: the caller composes on the host
+    int rc;
+    if ((rc = dev_reserve(c, &c->d_pg_D, (size_t)NB * per)) || (rc = dev_reserve(c, &c->d_pg_pos, (size_t)std::max(c->k, 1))) || (rc = dev_reserve(c, &c->d_pg_amax, (size_t)nsrc)) ||
+        (rc = dev_reserve(c, &c->d_pg_cnt, (size_t)3 * nsrc * m)) || (rc = dev_reserve(c, &c->d_pg_tot, (size_t)4 * nsrc)) ||
+        (rc = dev_reserve(c, &c->d_pg_valid, (size_t)nsrc)) || (rc = dev_reserve(c, &c->d_pg_head0, (size_t)m)) ||
+        (rc = dev_reserve(c, &c->d_pg_d0p, (size_t)64 * c->CH)))
+        return rc;
+    std::vector<int8_t> bt(n + m);
+    HIPCHK(hipMemcpyAsync(c->d_pg_head0, c->head0.data(), sizeof(int) * m, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_pg_d0p, c->d_d0, sizeof(double) * 64 * c->CH, hipMemcpyDeviceToDevice, c->stream));
+    if (c->k) HIPCHK(hipMemcpyAsync(c->d_pg_pos, c->pos_row.data(), sizeof(int) * c->k, hipMemcpyHostToDevice, c->stream));
+    PgArgs A{};
+    A.m = m; A.n = n; A.MP = MP; A.CH = c->CH; A.R9 = c->R; A.k = c->k; A.W = W; A.kmax = c->eo_kmax;
+    A.npool_old = (int)c->pool.size();
+    A.colptr = c->d_colptr; A.rowidx = c->d_rowidx; A.val = c->d_val; A.q = c->d_q; A.btype = c->d_btype;
+    A.pos_row = c->d_pg_pos;
+    A.bcp0 = c->d_bcp; A.bci0 = c->d_bci; A.bcv0 = c->d_bcv;
+    A.eo_pb = c->d_eo_pb; A.eo_K = c->d_eo_K; A.eo_off = c->d_eo_off; A.eo_etap = c->d_eo_etap;
+    A.eo_etaoff = c->d_eo_etaoff; A.eo_eidx = c->d_eo_eidx; A.eo_evals = c->d_eo_evals;
+    A.head0 = c->d_pg_head0; A.heads = c->d_head_out;
+    A.D = c->d_pg_D; A.amax = c->d_pg_amax;
+    A.rowcnt = c->d_pg_cnt; A.colcnt = c->d_pg_cnt + (size_t)nsrc * m; A.erowcnt = c->d_pg_cnt + (size_t)2 * nsrc * m;
+    A.tot = c->d_pg_tot; A.valid = c->d_pg_valid;
+    for (int a0 = 0; a0 < nsrc; a0 += NB) {
+        A.a0 = a0;
+        const int nb = std::min(NB, nsrc - a0);
+        HIPCHK(pg_launch_dense(A, nb, c->stream));
+        HIPCHK(pg_launch_count(A, nb, c->stream));
+    }
+    int *h_tot = stage_buf<int>(c, 9, (size_t)5 * nsrc), *h_heads = stage_buf<int>(c, 10, (size_t)R * m);
+    if (!h_tot || !h_heads) return fail(TWOSD_E_DEVICE, "pool refresh: pinned staging allocation failed");
+    int *h_valid = h_tot + (size_t)4 * nsrc;
+    HIPCHK(hipMemcpyAsync(h_tot, c->d_pg_tot, sizeof(int) * 4 * nsrc, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(h_valid, c->d_pg_valid, sizeof(int) * nsrc, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(h_heads, c->d_head_out, sizeof(int) * R * m, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (!h_valid[0]) return 1;   // the primary basis failed the device checks: host path
+    // pool = the sources that passed, in order; offsets = prefix sums of their totals
+    std::vector<int> map, off;
+    std::vector<int64_t> acc(4, 0);
+    for (int a = 0; a < nsrc; ++a) {
+        if (!h_valid[a]) continue;
+        map.push_back(a);
+        for (int f = 0; f < 4; ++f) {
+            off.push_back((int)acc[f]);
+            acc[f] += h_tot[(size_t)a * 4 + f];
+        }
+        if (acc[0] > INT32_MAX || acc[1] > INT32_MAX || acc[2] * 64 > INT32_MAX || acc[3] > INT32_MAX)
+            return fail(TWOSD_E_UNSUPPORTED, "basis pool too large (> 2^31 entries)");
+    }
+    const int P = (int)map.size();
+    if ((rc = dev_reserve(c, &c->d_pg_map, (size_t)P)) || (rc = dev_reserve(c, &c->d_pg_off, (size_t)4 * P))) return rc;
+    HIPCHK(hipMemcpyAsync(c->d_pg_map, map.data(), sizeof(int) * P, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_pg_off, off.data(), sizeof(int) * 4 * P, hipMemcpyHostToDevice, c->stream));
+    const size_t nz = (size_t)acc[0], kz = (size_t)acc[1], ez = (size_t)acc[2] * 64;
+    if ((rc = dev_reserve(c, &c->d_brptr, (size_t)P * (MP + 1))) || (rc = dev_reserve(c, &c->d_brcol, nz)) ||
+        (rc = dev_reserve(c, &c->d_brval, nz)) || (rc = dev_reserve(c, &c->d_bcp, (size_t)P * (MP + 1))) ||
+        (rc = dev_reserve(c, &c->d_bci, nz)) || (rc = dev_reserve(c, &c->d_bcv, nz)) ||
+        (rc = dev_reserve(c, &c->d_kp, (size_t)P * (m + 1))) || (rc = dev_reserve(c, &c->d_ke, kz)) ||
+        (rc = dev_reserve(c, &c->d_kraw, kz)) || (rc = dev_reserve(c, &c->d_kslot, (size_t)P * (c->R + 1))) ||
+        (rc = dev_reserve(c, &c->d_kix, ez)) || (rc = dev_reserve(c, &c->d_kv, ez)) ||
+        (rc = dev_reserve(c, &c->d_hb0, (size_t)P * MP)) || (rc = dev_reserve(c, &c->d_basic0, (size_t)P * 64)) ||
+        (rc = dev_reserve(c, &c->d_bnnz, (size_t)P)) || (rc = dev_reserve(c, &c->d_d0, (size_t)P * 64 * c->CH)) ||
+        (rc = dev_reserve(c, &c->d_sel_ptr, (size_t)P + 1)) || (rc = reserve_selection(c, P, (int)acc[3])))
+        return rc;
+    // (a grown array is reallocated, so the start pool's CSC is read only by the dense pass
+    // above: with one batch the fill needs no re-composition)
+    PgFill F{};
+    F.P = P; F.map = c->d_pg_map; F.off = c->d_pg_off; F.sel_total = (int)acc[3]; F.d0_primary = c->d_pg_d0p;
+    F.brptr = c->d_brptr; F.brcol = c->d_brcol; F.brval = c->d_brval; F.bcp = c->d_bcp; F.bci = c->d_bci; F.bcv = c->d_bcv;
+    F.kp = c->d_kp; F.ke = c->d_ke; F.kraw = c->d_kraw; F.kslot = c->d_kslot; F.kix = c->d_kix; F.kv = c->d_kv;
+    F.hb0 = c->d_hb0; F.basic0 = c->d_basic0; F.bnnz = c->d_bnnz; F.d0 = c->d_d0; F.sel_ptr = c->d_sel_ptr;
+    A.a0 = 0;
+    F.P0 = 0;
+    HIPCHK(pg_launch_fill(A, F, P, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    // host pool: the primary keeps its host forms; the new bases carry their heads
+    std::vector<PoolBasis> keep;
+    keep.reserve(P);
+    keep.push_back(std::move(c->pool[0]));
+    for (int p = 1; p < P; ++p) {
+        PoolBasis B;
+        const int l = map[p] - 1;
+        B.head.assign(h_heads + (size_t)l * m, h_heads + (size_t)(l + 1) * m);
+        B.dev_only = true;
+        keep.push_back(std::move(B));
+    }
+    c->pool.swap(keep);
+    std::thread([old = std::move(keep)]() mutable { old.clear(); }).detach();
+    c->b0_nnz = h_tot[0];
+    c->prep_valid = false;
+    c->k_valid = true;
+    c->pool_l1 = c->pool_ncand = 0;
+    return TWOSD_OK;
 }
 
 extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int first, int count, int max_pool,
@@ -744,6 +922,7 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
     std::vector<int> sel(R);
     for (int a = 0; a < R; ++a) sel[a] = reps[ord[a]];
     std::vector<PoolBasis> fresh;
+    bool device_built = false;
     if (R > 0) {
         // 3. re-solve the selected scenarios (same starts, so the same pivots) with their eta files
         if ((size_t)R > c->refresh_sel_cap) {
@@ -759,6 +938,18 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
         r.want_head = true;
         rc = run_lp_ex(c, x, d_dv, count, r);
         if (rc) return rc;
+        int dev = 1;
+        if (!getenv("TWOSD_REFRESH_HOST")) {
+            HIPCHK(hipStreamSynchronize(c->stream));
+            const auto t2 = std::chrono::steady_clock::now();
+            c->last_refresh_ms[1] = std::chrono::duration<double, std::milli>(t2 - t1).count();
+            if ((dev = refresh_build_device(c, R)) < 0) return dev;
+            c->last_refresh_ms[2] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count();
+        }
+        device_built = dev == 0;
+    }
+    if (R > 0 && !device_built) {
+        if ((rc = ensure_host_pool(c))) return rc;   // start bases in host form
         const int kmax = c->eo_kmax;
         std::vector<int> pb(R), K(R), off(R), etap((size_t)R * kmax), etaoff((size_t)R * (kmax + 1)), heads((size_t)R * m);
         int used = 0;
@@ -806,7 +997,7 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
         c->pool.swap(keep);
         // the old pool's host data is released on a helper thread (thousands of vectors)
         std::thread([old = std::move(keep)]() mutable { old.clear(); }).detach();
-    } else {
+    } else if (R == 0) {
         c->pool.resize(1);
         c->last_refresh_ms[1] = c->last_refresh_ms[2] = 0.0;
     }
@@ -826,9 +1017,9 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
             }
     }
     const auto tu = std::chrono::steady_clock::now();
-    if ((rc = upload_pool(c))) return rc;
+    if (!device_built && (rc = upload_pool(c))) return rc;
     const auto tua = std::chrono::steady_clock::now();
-    if ((rc = prepare_elements(c))) return rc;
+    if (!device_built && (rc = prepare_elements(c))) return rc;
     const auto t3 = std::chrono::steady_clock::now();
     if (getenv("TWOSD_DEBUG")) {
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -1096,6 +1287,7 @@ extern "C" int twosd_epigraph_info(twosd_ctx *c, int epi, int *ns, double *tw) {
 // into kix/kv).  The kernels multiply the scenario deltas by coef_e(x) (d_kcoef) themselves.
 static int prepare_elements(twosd_ctx *c) {
     const auto t_pe0 = std::chrono::steady_clock::now();
+    if (int rc0 = ensure_host_pool(c)) return rc0;
     const int m = c->L.m, k = c->k, R = c->R;
     std::vector<std::vector<int>> bycol(m);   // random elements on each row
     for (int e = 0; e < k; ++e) bycol[c->pos_row[e]].push_back(e);
@@ -1177,25 +1369,16 @@ static int prepare_elements(twosd_ctx *c) {
     });
     const auto t_pe1 = std::chrono::steady_clock::now();
     int rc;
-    if (c->CH > 0 && ((rc = upload(&c->d_kslot, ks)) || (rc = upload_big(c, &c->d_kix, ki, ecnt[P])) ||
+    if (c->CH > 0 && ((rc = upload_big(c, &c->d_kslot, ks)) || (rc = upload_big(c, &c->d_kix, ki, ecnt[P])) ||
                       (rc = upload_big(c, &c->d_kv, kv, ecnt[P]))))
         return rc;
     const auto t_pe2 = std::chrono::steady_clock::now();
     if (c->CH > 0 && P > 1) {
         // device selection-stream inputs: CSR rows of every basis, and a static record capacity
         // per basis (every row active: m row starts + all its entries)
-        if ((rc = upload(&c->d_kp, kp)) || (rc = upload_big(c, &c->d_ke, ke, kz)) || (rc = upload_big(c, &c->d_kraw, kr, kz)) ||
-            (rc = upload(&c->d_sel_ptr, cap)))
+        if ((rc = upload_big(c, &c->d_kp, kp)) || (rc = upload_big(c, &c->d_ke, ke, kz)) || (rc = upload_big(c, &c->d_kraw, kr, kz)) ||
+            (rc = upload_big(c, &c->d_sel_ptr, cap)) || (rc = reserve_selection(c, P, cap[P])))
             return rc;
-        if ((size_t)std::max(cap[P], 1) > c->sel_code_cap) {
-            dfree(c->d_sel_code);
-            if ((rc = dalloc(&c->d_sel_code, 2 * (size_t)std::max(cap[P], 1)))) return rc;
-            c->sel_code_cap = std::max(cap[P], 1);
-        }
-        dfree(c->d_sel_end);
-        dfree(c->d_sel_cinf);
-        if ((rc = dalloc(&c->d_sel_end, (size_t)P)) || (rc = dalloc(&c->d_sel_cinf, (size_t)P))) return rc;
-        c->sel_cap_total = cap[P];
     }
     c->k_valid = true;
     if (getenv("TWOSD_DEBUG")) {

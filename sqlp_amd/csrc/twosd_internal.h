@@ -71,6 +71,39 @@ struct HyperParams {
     int *eo_used; int eo_cap;
 };
 
+// ---- device pool build of a refresh (pool_gpu.hip) ---------------------------------
+// Source a of a build: a = 0 the primary basis (start pool basis 0, no etas, head0), a >= 1
+// the eta file and head of list position a - 1 of the refresh re-solve.  B^{-1} of every
+// source is composed densely (column tiles of W in LDS), checked, counted, and then written
+// into the pool-strided arrays of upload_pool / prepare_elements at host-computed offsets.
+struct PgArgs {
+    int m, n, MP, CH, R9, k, W, kmax, npool_old;
+    const int *colptr, *rowidx; const double *val, *q; const int8_t *btype; const int *pos_row;
+    const int *bcp0, *bci0; const double *bcv0;          // start pool: B^{-1} CSC (pool-strided)
+    const int *eo_pb, *eo_K, *eo_off, *eo_etap, *eo_etaoff, *eo_eidx; const double *eo_evals;
+    const int *head0, *heads;                            // primary head (m); heads by list position
+    double *D;                                           // dense B^{-1} of sources [a0, a0 + batch)
+    int a0;
+    double *amax;                                        // nsrc (-1: source unusable)
+    int *rowcnt, *colcnt, *erowcnt;                      // nsrc x m
+    int *tot;                                            // nsrc x 4: nnz, element entries, ELL rows, records
+    int *valid;                                          // nsrc
+};
+struct PgFill {
+    int P0, P;                                           // pool bases [P0, P0 + grid) of P
+    const int *map;                                      // P: source of pool basis p
+    const int *off;                                      // P x 4: offsets (prefix of tot over the pool)
+    int sel_total;
+    const double *d0_primary;                            // 64 CH: d0 of pool[0], kept as uploaded
+    int *brptr, *brcol; double *brval; int *bcp, *bci; double *bcv;
+    int *kp, *ke; double *kraw; int *kslot, *kix; double *kv;
+    int *hb0; uint64_t *basic0; int *bnnz; double *d0; int *sel_ptr;
+};
+int pg_tile_width(int m);                                // 0: m too large for the LDS tile
+hipError_t pg_launch_dense(const PgArgs &A, int nb, hipStream_t s);
+hipError_t pg_launch_count(const PgArgs &A, int nb, hipStream_t s);
+hipError_t pg_launch_fill(const PgArgs &A, const PgFill &F, int np, hipStream_t s);
+
 // splitmix64 finalizer (basis keys: host and device must agree)
 __host__ __device__ inline unsigned long long mix64(unsigned long long z) {
     z += 0x9E3779B97F4A7C15ull;

@@ -79,3 +79,51 @@ def test_pool_refresh_bad_args():
     with pytest.raises(TwoSDError):
         ctx.pool_refresh(tr, x, 0, 65, 8)
     assert ctx.pool_refresh(tr, x, 0, 64, 8) <= 8
+
+
+@pytest.mark.parametrize("chain", [1, 2])
+def test_pool_refresh_device_build_equals_host(monkeypatch, chain):
+    """The device pool build (pool_gpu.hip) and the host one (compose_binv + upload_pool +
+    prepare_elements, TWOSD_REFRESH_HOST=1) produce the same pool: the same bases, and solves
+    from it with identical objectives and pivot counts.  chain = 2 refreshes twice, so the second
+    composes from device-built start bases; afterwards a host-side pool change (pool_build,
+    which reads every basis back in host form) must keep the objectives exact."""
+    from sqlp_amd import smps, twosd
+    inst = I.load("storm")
+    x_ev = I.x_ev("storm")
+    x2 = _sd_x()
+    x3 = x_ev + 0.6 * (x2 - x_ev)
+    xs = [x2, x3][:chain]
+    vals = I.sample("storm", 3000, seed=23)
+    runs = []
+    for mode in ("host", "device"):
+        if mode == "host":
+            monkeypatch.setenv("TWOSD_REFRESH_HOST", "1")
+        else:
+            monkeypatch.delenv("TWOSD_REFRESH_HOST", raising=False)
+        ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+        ctx.compute_basis(x_ev, smps.mean_values(inst["sto"]))
+        tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+        twosd.add_scenarios(tr, I.sample("storm", 4096, seed=21))
+        ctx.pool_build(tr, x_ev, 0, 4096, 256)
+        ev = twosd.sdEpigraph(ctx, 1.0, 0.0)
+        twosd.add_scenarios(ev, vals)
+        for x in xs:
+            P = ctx.pool_refresh(tr, x, 0, 4096, 512)
+        o, _, _, st = twosd.solve_batch(ev, xs[-1], 0, len(vals), want_pi=False)
+        runs.append((P, [ctx.pool_get(p) for p in range(P)], o, st, ctx.lp_stats()[0], ctx, tr, ev))
+    (P_h, heads_h, o_h, st_h, piv_h, _, _, _), (P_d, heads_d, o_d, st_d, piv_d, ctx, tr, ev) = runs
+    assert P_h == P_d
+    for a, b in zip(heads_h, heads_d):
+        np.testing.assert_array_equal(a, b)
+    assert (st_h == 0).all() and (st_d == 0).all()
+    np.testing.assert_allclose(o_d, o_h, rtol=1e-12, atol=1e-12)
+    assert piv_d == piv_h
+    ref = twosd.SDContext(inst["sp2"], inst["sto"])
+    ref.compute_basis(x_ev, smps.mean_values(inst["sto"]))
+    o_ref, _, _, _ = ref.solve_values(xs[-1], vals, want_pi=False)
+    ctx.pool_build(tr, x_ev, 0, 4096, P_d + 64)          # host path over the device-built pool
+    o_after, _, _, st_after = twosd.solve_batch(ev, xs[-1], 0, len(vals), want_pi=False)
+    assert (st_after == 0).all()
+    np.testing.assert_allclose(o_after, o_ref, rtol=1e-9, atol=1e-9)
+    print(f"chain {chain}: pool {P_d}, pivots {piv_d / len(vals):.2f}, refresh ms {ctx.last_refresh_ms()}")
