@@ -237,7 +237,7 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_refresh_sel); c->refresh_sel_cap = 0; c->box_epi = -1;
     dfree(c->d_eo_pb); dfree(c->d_eo_K); dfree(c->d_eo_off); dfree(c->d_eo_etap); dfree(c->d_eo_etaoff);
     dfree(c->d_eo_eidx); dfree(c->d_eo_evals); dfree(c->d_eo_used); c->eo_rows = c->eo_cap = 0; c->eo_kmax = 0;
-    dfree(c->d_pg_D); dfree(c->d_pg_amax); dfree(c->d_pg_d0p); dfree(c->d_pg_cnt); dfree(c->d_pg_tot);
+    dfree(c->d_pg_ival); dfree(c->d_pg_irow); dfree(c->d_pg_ioff); dfree(c->d_pg_amax); dfree(c->d_pg_d0p); dfree(c->d_pg_cnt); dfree(c->d_pg_tot);
     dfree(c->d_pg_valid); dfree(c->d_pg_head0); dfree(c->d_pg_map); dfree(c->d_pg_off); dfree(c->d_pg_pos);
     c->has_template = c->has_basis = false;
 }
@@ -778,32 +778,26 @@ static const char *finish_composed(const twosd_ctx *c, PoolBasis &B) {
 }
 
 // Device build of the refreshed pool (pool_gpu.hip) from the re-solve's eta files and heads
-// (list positions 0..R-1 in c->d_eo_* / c->d_head_out): sources a = 0 (primary) .. R, composed
-// and checked in batches that fit the dense scratch, then the sources that passed are written
-// in order as pool[0..P) -- the arrays upload_pool + prepare_elements would produce.  One
-// batch (the start pool's CSC is overwritten by the fill); returns 1, with nothing changed, when
-// the sources do not fit the scratch or the primary fails the checks (then the host composes).
+// (list positions 0..R-1 in c->d_eo_* / c->d_head_out): sources a = 0 (primary) .. R are
+// composed column by column, checked, and the sources that passed are written in order as
+// pool[0..P) -- the arrays upload_pool + prepare_elements would produce.  Returns 1, with the
+// pool unchanged, when the LDS layouts do not fit or the primary fails the device checks (the
+// caller then composes on the host).
 static int refresh_build_device(twosd_ctx *c, int R) {
     const HostLP &L = c->L;
-    const int m = L.m, n = L.n, MP = c->MP, nsrc = R + 1, W = pg_tile_width(m);
-    const size_t per = (size_t)m * m;
-    size_t freeb = 0, totalb = 0;
-    HIPCHK(hipMemGetInfo(&freeb, &totalb));
-    const size_t budget = std::min<size_t>(freeb / 3, (size_t)12 << 30);
-    const int NB = (int)std::max<size_t>(1, std::min<size_t>(nsrc, budget / (per * sizeof(double))));
-    if (W == 0 || NB < nsrc) return 1;   // does not fit: the caller composes on the host
+    const int m = L.m, n = L.n, MP = c->MP, nsrc = R + 1;
+    if (!pg_supported(m, n, c->eo_kmax)) return 1;
     int rc;
-    if ((rc = dev_reserve(c, &c->d_pg_D, (size_t)NB * per)) || (rc = dev_reserve(c, &c->d_pg_pos, (size_t)std::max(c->k, 1))) || (rc = dev_reserve(c, &c->d_pg_amax, (size_t)nsrc)) ||
-        (rc = dev_reserve(c, &c->d_pg_cnt, (size_t)3 * nsrc * m)) || (rc = dev_reserve(c, &c->d_pg_tot, (size_t)4 * nsrc)) ||
+    if ((rc = dev_reserve(c, &c->d_pg_pos, (size_t)std::max(c->k, 1))) || (rc = dev_reserve(c, &c->d_pg_amax, (size_t)nsrc)) ||
+        (rc = dev_reserve(c, &c->d_pg_cnt, (size_t)4 * nsrc * m)) || (rc = dev_reserve(c, &c->d_pg_tot, (size_t)5 * nsrc)) ||
         (rc = dev_reserve(c, &c->d_pg_valid, (size_t)nsrc)) || (rc = dev_reserve(c, &c->d_pg_head0, (size_t)m)) ||
-        (rc = dev_reserve(c, &c->d_pg_d0p, (size_t)64 * c->CH)))
+        (rc = dev_reserve(c, &c->d_pg_d0p, (size_t)64 * c->CH)) || (rc = dev_reserve(c, &c->d_pg_ioff, (size_t)nsrc)))
         return rc;
-    std::vector<int8_t> bt(n + m);
     HIPCHK(hipMemcpyAsync(c->d_pg_head0, c->head0.data(), sizeof(int) * m, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->d_pg_d0p, c->d_d0, sizeof(double) * 64 * c->CH, hipMemcpyDeviceToDevice, c->stream));
     if (c->k) HIPCHK(hipMemcpyAsync(c->d_pg_pos, c->pos_row.data(), sizeof(int) * c->k, hipMemcpyHostToDevice, c->stream));
     PgArgs A{};
-    A.m = m; A.n = n; A.MP = MP; A.CH = c->CH; A.R9 = c->R; A.k = c->k; A.W = W; A.kmax = c->eo_kmax;
+    A.m = m; A.n = n; A.MP = MP; A.CH = c->CH; A.R9 = c->R; A.k = c->k; A.kmax = c->eo_kmax;
     A.npool_old = (int)c->pool.size();
     A.colptr = c->d_colptr; A.rowidx = c->d_rowidx; A.val = c->d_val; A.q = c->d_q; A.btype = c->d_btype;
     A.pos_row = c->d_pg_pos;
@@ -811,15 +805,36 @@ static int refresh_build_device(twosd_ctx *c, int R) {
     A.eo_pb = c->d_eo_pb; A.eo_K = c->d_eo_K; A.eo_off = c->d_eo_off; A.eo_etap = c->d_eo_etap;
     A.eo_etaoff = c->d_eo_etaoff; A.eo_eidx = c->d_eo_eidx; A.eo_evals = c->d_eo_evals;
     A.head0 = c->d_pg_head0; A.heads = c->d_head_out;
-    A.D = c->d_pg_D; A.amax = c->d_pg_amax;
-    A.rowcnt = c->d_pg_cnt; A.colcnt = c->d_pg_cnt + (size_t)nsrc * m; A.erowcnt = c->d_pg_cnt + (size_t)2 * nsrc * m;
-    A.tot = c->d_pg_tot; A.valid = c->d_pg_valid;
-    for (int a0 = 0; a0 < nsrc; a0 += NB) {
-        A.a0 = a0;
-        const int nb = std::min(NB, nsrc - a0);
-        HIPCHK(pg_launch_dense(A, nb, c->stream));
-        HIPCHK(pg_launch_count(A, nb, c->stream));
+    A.a0 = 0;
+    A.amax = c->d_pg_amax;
+    A.nzc = c->d_pg_cnt; A.keptc = c->d_pg_cnt + (size_t)nsrc * m;
+    A.rowcnt = c->d_pg_cnt + (size_t)2 * nsrc * m; A.erowcnt = c->d_pg_cnt + (size_t)3 * nsrc * m;
+    A.tot = c->d_pg_tot; A.nztot = c->d_pg_tot + (size_t)4 * nsrc; A.valid = c->d_pg_valid;
+    const bool dbg = getenv("TWOSD_DEBUG") != nullptr;
+    auto now = [&]() {
+        if (dbg) hipStreamSynchronize(c->stream);
+        return std::chrono::steady_clock::now();
+    };
+    const auto t0 = now();
+    HIPCHK(pg_launch_ftran(A, 0, nsrc, c->stream));
+    // intermediate CSC offsets from the nonzero counts
+    int *h_nz = stage_buf<int>(c, 11, (size_t)nsrc);
+    long long *h_ioff = stage_buf<long long>(c, 12, (size_t)nsrc);
+    if (!h_nz || !h_ioff) return fail(TWOSD_E_DEVICE, "pool refresh: pinned staging allocation failed");
+    HIPCHK(hipMemcpyAsync(h_nz, A.nztot, sizeof(int) * nsrc, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    long long inz = 0;
+    for (int a = 0; a < nsrc; ++a) {
+        h_ioff[a] = inz;
+        inz += h_nz[a];
     }
+    if ((rc = dev_reserve(c, &c->d_pg_irow, (size_t)inz)) || (rc = dev_reserve(c, &c->d_pg_ival, (size_t)inz))) return rc;
+    HIPCHK(hipMemcpyAsync(c->d_pg_ioff, h_ioff, sizeof(long long) * nsrc, hipMemcpyHostToDevice, c->stream));
+    A.inter_off = c->d_pg_ioff; A.inter_row = c->d_pg_irow; A.inter_val = c->d_pg_ival;
+    const auto t1 = now();
+    HIPCHK(pg_launch_ftran(A, 1, nsrc, c->stream));
+    HIPCHK(pg_launch_count(A, nsrc, c->stream));
+    const auto t2 = now();
     int *h_tot = stage_buf<int>(c, 9, (size_t)5 * nsrc), *h_heads = stage_buf<int>(c, 10, (size_t)R * m);
     if (!h_tot || !h_heads) return fail(TWOSD_E_DEVICE, "pool refresh: pinned staging allocation failed");
     int *h_valid = h_tot + (size_t)4 * nsrc;
@@ -856,8 +871,7 @@ static int refresh_build_device(twosd_ctx *c, int R) {
         (rc = dev_reserve(c, &c->d_bnnz, (size_t)P)) || (rc = dev_reserve(c, &c->d_d0, (size_t)P * 64 * c->CH)) ||
         (rc = dev_reserve(c, &c->d_sel_ptr, (size_t)P + 1)) || (rc = reserve_selection(c, P, (int)acc[3])))
         return rc;
-    // (a grown array is reallocated, so the start pool's CSC is read only by the dense pass
-    // above: with one batch the fill needs no re-composition)
+    // (a grown array is reallocated: the start pool's CSC was read only by the FTRAN passes)
     PgFill F{};
     F.P = P; F.map = c->d_pg_map; F.off = c->d_pg_off; F.sel_total = (int)acc[3]; F.d0_primary = c->d_pg_d0p;
     F.brptr = c->d_brptr; F.brcol = c->d_brcol; F.brval = c->d_brval; F.bcp = c->d_bcp; F.bci = c->d_bci; F.bcv = c->d_bcv;
@@ -865,8 +879,14 @@ static int refresh_build_device(twosd_ctx *c, int R) {
     F.hb0 = c->d_hb0; F.basic0 = c->d_basic0; F.bnnz = c->d_bnnz; F.d0 = c->d_d0; F.sel_ptr = c->d_sel_ptr;
     A.a0 = 0;
     F.P0 = 0;
+    const auto t3 = now();
     HIPCHK(pg_launch_fill(A, F, P, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    if (dbg) {
+        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        fprintf(stderr, "refresh_build_device: %d sources, ftran-0 %.2f, ftran-1+count %.2f, offsets %.2f, fill %.2f ms (%lld intermediate)\n", nsrc, ms(t0, t1),
+                ms(t1, t2), ms(t2, t3), ms(t3, std::chrono::steady_clock::now()), inz);
+    }
     // host pool: the primary keeps its host forms; the new bases carry their heads
     std::vector<PoolBasis> keep;
     keep.reserve(P);

@@ -4,21 +4,25 @@
 // The host path of api.hip (compose_binv in host_basis.cpp, then upload_pool and
 // prepare_elements) composes B^{-1} = E_K..E_1 B_pb^{-1} by sparse row merges and re-derives
 // CSC, element rows, sliced ELL, d0 and the basis words on 16 host threads before a PCIe
-// upload -- at 4096 bases that is ~60 ms of a ~90 ms refresh.  Here, per source basis (one
-// workgroup):
-//   pg_dense_kernel  B_pb^{-1} column tile (m x W doubles, all rows, in LDS) <- the start
-//                    basis's CSC columns; the K etas applied in order (row r <- eta_r row r,
-//                    row i <- fma(eta_i, old row r, row i): the same operations and rounding
-//                    as compose_binv); the tile written to a dense scratch D (HBM).
-//   pg_count_kernel  the entries kept (rows an eta touched: |v| > 1e-14 max|.|, the others
-//                    exactly B_pb^{-1}'s pattern, as compose_binv), per row / column /
-//                    element-row counts, pi0, the dual-feasibility and 4-probe residual checks
-//                    of finish_composed, and the per-basis totals.
-//   pg_fill_kernel   at offsets the host prefix-summed from the totals: B^{-1} CSR (columns
-//                    ascending) and CSC (rows ascending), element rows as CSR (e ascending)
-//                    and sliced ELL, hb0 / basic0 / bnnz / d0 / selection-record pointers --
-//                    the layouts (and entry order) of upload_pool and prepare_elements.
-// Bytes: D is written once and read ~3x (2.2 MB per storm basis); the rest is the output.
+// upload -- at 4096 bases ~60 ms of a ~90 ms refresh.  Here every column of B^{-1} is the
+// eta sequence applied to the start basis's column (a sparse FTRAN: eta t is skipped when the
+// column's entry in its pivot row is zero), one wavefront per column with the column dense in
+// LDS, so no HBM round trip of a dense B^{-1}:
+//   pg_ftran_kernel<0>  per source: max |.| over B_pb^{-1} and the result (drop threshold
+//                       1e-14 max, as compose_binv) and per column the nonzero count;
+//   pg_ftran_kernel<1>  the same FTRAN again, the kept entries of each column written (rows
+//                       ascending) into an intermediate CSC at host-prefixed offsets.  Kept:
+//                       rows some eta touched |v| > drop, other rows exactly B_pb^{-1}'s
+//                       entries -- compose_binv's rule, and its arithmetic: row r <- eta_r x_r,
+//                       row i <- fma(eta_i, x_r, row i), so the values are bit-identical;
+//   pg_count_kernel     per source: row / element-row counts, pi0, the dual-feasibility and
+//                       4-probe residual checks of finish_composed, the per-basis totals;
+//   pg_fill_kernel      at host-prefixed offsets: CSC (compacted), CSR (columns ascending,
+//                       one wave walking the columns), element rows as CSR and sliced ELL (one
+//                       wave walking the elements, e ascending), hb0 / basic0 / bnnz / d0 /
+//                       selection pointers -- upload_pool's and prepare_elements's layouts and
+//                       entry order.
+// HBM traffic is O(nnz) per basis (~0.2 MB for storm) instead of the dense m x m.
 #include <hip/hip_runtime.h>
 #include "twosd_internal.h"
 
@@ -27,7 +31,7 @@ namespace twosd {
 namespace {
 
 constexpr int kPgThreads = 256;
-constexpr size_t kPgTileBytes = 144 * 1024;   // LDS tile budget (gfx950: 160 KB per workgroup)
+constexpr int kPgWaves = kPgThreads / 64;
 
 struct Src {
     int pb, K, off;
@@ -48,6 +52,10 @@ __device__ inline Src src_of(const PgArgs &A, int a) {
     s.etap = A.eo_etap + (size_t)l * A.kmax;
     s.etaoff = A.eo_etaoff + (size_t)l * (A.kmax + 1);
     return s;
+}
+
+__device__ inline bool src_ok(const PgArgs &A, const Src &S) {
+    return S.K >= 0 && S.K <= A.kmax && S.pb >= 0 && S.pb < A.npool_old;
 }
 
 // exclusive prefix of in[0, n) into out[0, n], out[n] = total (all threads of the block)
@@ -73,83 +81,127 @@ __device__ void block_scan(const int *in, int *out, int n, int *tmp) {
     __syncthreads();
 }
 
-__device__ inline bool keep_entry(const unsigned char *touched, int i, double v, double drop) {
-    return touched[i] ? fabs(v) > drop : v != 0.0;
-}
-
 __device__ inline unsigned long long lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
+
+// rows any eta of the source touches (compose_binv re-filters exactly these rows)
+__device__ void mark_touched(const PgArgs &A, const Src &S, unsigned char *touched) {
+    for (int i = threadIdx.x; i < A.m; i += kPgThreads) touched[i] = 0;
+    __syncthreads();
+    const int ne = S.K > 0 ? S.etaoff[S.K] : 0;
+    for (int e = threadIdx.x; e < ne; e += kPgThreads) touched[A.eo_eidx[S.off + e]] = 1;
+    __syncthreads();
+}
 
 }  // namespace
 
-int pg_tile_width(int m) {
-    for (int W = 32; W >= 8; W >>= 1)
-        if ((size_t)m * W * sizeof(double) <= kPgTileBytes) return W;
-    return 0;
-}
-
-// ---- 1. dense composition ------------------------------------------------------------
-__global__ __launch_bounds__(kPgThreads) void pg_dense_kernel(PgArgs A) {
-    extern __shared__ double tile[];   // m x W, row-major
-    __shared__ double red[kPgThreads / 64];
-    const int a = A.a0 + blockIdx.x, m = A.m, W = A.W, tid = threadIdx.x;
+// ---- 1. FTRAN of every column of B_pb^{-1} through the eta file ----------------------------
+template <int PASS>
+__global__ __launch_bounds__(kPgThreads) void pg_ftran_kernel(PgArgs A) {
+    extern __shared__ double smem[];
+    __shared__ int tmp[kPgThreads];
+    __shared__ double red[kPgWaves];
+    const int a = A.a0 + blockIdx.x, m = A.m, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const Src S = src_of(A, a);
-    if (S.K < 0 || S.K > A.kmax || S.pb < 0 || S.pb >= A.npool_old) {   // eta file did not fit: unusable
-        if (tid == 0) A.amax[a] = -1.0;
+    if (!src_ok(A, S) || (PASS == 1 && !(A.amax[a] >= 0.0))) {   // eta file did not fit: unusable
+        if (PASS == 0 && tid == 0) { A.amax[a] = -1.0; A.nztot[a] = 0; }
         return;
     }
-    double *D = A.D + (size_t)blockIdx.x * m * m;
-    const int *cp = A.bcp0 + (size_t)S.pb * (A.MP + 1);
-    const int G = kPgThreads / W, jj = tid % W, g = tid / W;   // G groups of W columns
-    double amax = 0.0;
-    for (int cb = 0; cb < m; cb += W) {
-        const int wc = min(W, m - cb);
-        for (int idx = tid; idx < m * W; idx += kPgThreads) tile[idx] = 0.0;
-        __syncthreads();
-        if (jj < wc)
-            for (int q = cp[cb + jj] + g; q < cp[cb + jj + 1]; q += G) {
-                const double v = A.bcv0[q];
-                tile[A.bci0[q] * W + jj] = v;
-                amax = fmax(amax, fabs(v));
-            }
-        __syncthreads();
-        for (int t = 0; t < S.K; ++t) {
-            const int r = S.etap[t];
-            const double rr = tile[r * W + jj];   // the old row r, before this eta
-            __syncthreads();
-            const int e1 = S.etaoff[t + 1];
-            for (int e = S.etaoff[t] + g; e < e1; e += G) {   // distinct rows within one eta
-                const int i = A.eo_eidx[S.off + e];
-                const double v = A.eo_evals[S.off + e];
-                double &x = tile[i * W + jj];
-                x = i == r ? v * rr : fma(v, rr, x);
-            }
-            __syncthreads();
-        }
-        for (int idx = tid; idx < m * W; idx += kPgThreads) {
-            const int i = idx / W, j = idx - (idx / W) * W;
-            if (j < wc) {
-                const double v = tile[idx];
-                D[(size_t)i * m + cb + j] = v;
-                amax = fmax(amax, fabs(v));
-            }
-        }
-        __syncthreads();
+    double *x = smem + (size_t)wv * m;                    // this wave's column, dense
+    int *etap = reinterpret_cast<int *>(smem + (size_t)kPgWaves * m);
+    int *etaoff = etap + A.kmax;
+    int *cstart = etaoff + A.kmax + 1;                    // PASS 1: column offsets (m + 1)
+    unsigned char *touched = reinterpret_cast<unsigned char *>(cstart + m + 1);
+    for (int t = tid; t < S.K; t += kPgThreads) etap[t] = S.etap[t];
+    for (int t = tid; t <= S.K; t += kPgThreads) etaoff[t] = S.K > 0 ? S.etaoff[t] : 0;
+    mark_touched(A, S, touched);
+    double drop = 0.0;
+    int *nzc = A.nzc + (size_t)a * m;
+    if (PASS == 1) {
+        block_scan(nzc, cstart, m, tmp);
+        drop = 1e-14 * A.amax[a];
     }
-    for (int o = 32; o > 0; o >>= 1) amax = fmax(amax, __shfl_xor(amax, o));
-    if ((tid & 63) == 0) red[tid >> 6] = amax;
-    __syncthreads();
-    if (tid == 0) {
-        double v = red[0];
-        for (int w = 1; w < kPgThreads / 64; ++w) v = fmax(v, red[w]);
-        A.amax[a] = v;
+    const int *cp = A.bcp0 + (size_t)S.pb * (A.MP + 1);
+    const int *eidx = A.eo_eidx + S.off;
+    const double *evals = A.eo_evals + S.off;
+    double amax = 0.0;
+    int nzsum = 0;   // PASS 0, lane 0: nonzeros of this wave's columns
+    for (int c = wv; c < m; c += kPgWaves) {
+        for (int i = lane; i < m; i += 64) x[i] = 0.0;
+        __builtin_amdgcn_wave_barrier();
+        for (int q = cp[c] + lane; q < cp[c + 1]; q += 64) {
+            const double v = A.bcv0[q];
+            x[A.bci0[q]] = v;
+            amax = fmax(amax, fabs(v));
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (int t = 0; t < S.K; ++t) {
+            const int r = etap[t];
+            const double xr = x[r];
+            __builtin_amdgcn_wave_barrier();
+            if (xr != 0.0) {   // E_t x = x + (eta - e_r) x_r: nothing to do when x_r = 0
+                for (int e = etaoff[t] + lane; e < etaoff[t + 1]; e += 64) {   // distinct rows
+                    const int i = eidx[e];
+                    const double v = evals[e];
+                    x[i] = i == r ? v * xr : fma(v, xr, x[i]);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (PASS == 0) {
+            int cnt = 0;
+            for (int i0 = 0; i0 < m; i0 += 64) {
+                const int i = i0 + lane;
+                const double v = i < m ? x[i] : 0.0;
+                amax = fmax(amax, fabs(v));
+                cnt += __popcll(__ballot(v != 0.0));
+            }
+            if (lane == 0) nzc[c] = cnt;
+            nzsum += cnt;
+        } else {
+            const size_t base = (size_t)A.inter_off[a] + cstart[c];
+            int run = 0;
+            for (int i0 = 0; i0 < m; i0 += 64) {
+                const int i = i0 + lane;
+                const double v = i < m ? x[i] : 0.0;
+                const bool kk = i < m && (touched[i] ? fabs(v) > drop : v != 0.0);
+                const unsigned long long msk = __ballot(kk);
+                if (kk) {
+                    const size_t at = base + run + __popcll(msk & lanemask_lt(lane));
+                    A.inter_row[at] = i;
+                    A.inter_val[at] = v;
+                }
+                run += __popcll(msk);
+            }
+            if (lane == 0) A.keptc[(size_t)a * m + c] = run;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (PASS == 0) {
+        for (int o = 32; o > 0; o >>= 1) amax = fmax(amax, __shfl_xor(amax, o));
+        if (lane == 0) {
+            red[wv] = amax;
+            tmp[wv] = nzsum;
+        }
+        __syncthreads();
+        if (tid == 0) {   // nztot: read back by the host for the intermediate offsets
+            double v = red[0];
+            int t = tmp[0];
+            for (int w = 1; w < kPgWaves; ++w) {
+                v = fmax(v, red[w]);
+                t += tmp[w];
+            }
+            A.amax[a] = v;
+            A.nztot[a] = t;
+        }
     }
 }
 
-// ---- 2. counts, pi0, checks ------------------------------------------------------------
+// ---- 2. counts, pi0, checks --------------------------------------------------------------
 __global__ __launch_bounds__(kPgThreads) void pg_count_kernel(PgArgs A) {
     extern __shared__ double smem[];
     __shared__ int s_tot[4], s_bad;
-    const int a = A.a0 + blockIdx.x, m = A.m, n = A.n, k = A.k, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    __shared__ int tmp[kPgThreads];
+    const int a = A.a0 + blockIdx.x, m = A.m, n = A.n, k = A.k, tid = threadIdx.x;
     const double amax = A.amax[a];
     if (!(amax >= 0.0)) {
         if (tid < 4) A.tot[(size_t)a * 4 + tid] = 0;
@@ -157,58 +209,37 @@ __global__ __launch_bounds__(kPgThreads) void pg_count_kernel(PgArgs A) {
         return;
     }
     const Src S = src_of(A, a);
-    double *pi0 = smem, *cbv = smem + m;
-    int *erow = reinterpret_cast<int *>(cbv + m);
-    unsigned char *touched = reinterpret_cast<unsigned char *>(erow + m), *isb = touched + m;
+    double *pi0 = smem, *cbv = smem + m, *y = cbv + m;
+    int *rowc = reinterpret_cast<int *>(y + m), *erow = rowc + m, *cstart = erow + m;   // cstart: m + 1
+    unsigned char *isb = reinterpret_cast<unsigned char *>(cstart + m + 1);
     if (tid < 4) s_tot[tid] = 0;
     if (tid == 0) s_bad = 0;
-    for (int i = tid; i < m; i += kPgThreads) touched[i] = 0;
+    for (int i = tid; i < m; i += kPgThreads) { rowc[i] = 0; erow[i] = 0; }
     for (int j = tid; j < n + m; j += kPgThreads) isb[j] = 0;
     __syncthreads();
-    const int ne = S.K > 0 ? S.etaoff[S.K] : 0;
-    for (int e = tid; e < ne; e += kPgThreads) touched[A.eo_eidx[S.off + e]] = 1;
     for (int i = tid; i < m; i += kPgThreads) {
         const int j = S.head[i];
         isb[j] = 1;
         cbv[i] = j < n ? A.q[j] : 0.0;
     }
-    __syncthreads();
-    const double drop = 1e-14 * amax;
-    const double *D = A.D + (size_t)blockIdx.x * m * m;
-    // rows (one wave per row): B^{-1} entries and element entries
-    for (int i = wv; i < m; i += kPgThreads / 64) {
-        int cnt = 0, ec = 0;
-        for (int c0 = 0; c0 < m; c0 += 64) {
-            const int c = c0 + lane;
-            const bool kk = c < m && keep_entry(touched, i, D[(size_t)i * m + c], drop);
-            cnt += __popcll(__ballot(kk));
-        }
-        for (int e0 = 0; e0 < k; e0 += 64) {
-            const int e = e0 + lane;
-            const bool kk = e < k && keep_entry(touched, i, D[(size_t)i * m + A.pos_row[e]], drop);
-            ec += __popcll(__ballot(kk));
-        }
-        if (lane == 0) {
-            A.rowcnt[(size_t)a * m + i] = cnt;
-            A.erowcnt[(size_t)a * m + i] = ec;
-            erow[i] = ec;
-            atomicAdd(&s_tot[0], cnt);
-            atomicAdd(&s_tot[1], ec);
-        }
-    }
-    // columns (one thread per column): counts and pi0 = c_B' B^{-1} over the kept entries
+    const int *keptc = A.keptc + (size_t)a * m;
+    block_scan(A.nzc + (size_t)a * m, cstart, m, tmp);    // intermediate column starts
+    const int *irow = A.inter_row + A.inter_off[a];
+    const double *ival = A.inter_val + A.inter_off[a];
+    // per column (one thread a column): row counts, pi0 = c_B' B^{-1} (rows ascending)
     for (int c = tid; c < m; c += kPgThreads) {
-        int cnt = 0;
         double pi = 0.0;
-        for (int i = 0; i < m; ++i) {
-            const double v = D[(size_t)i * m + c];
-            if (keep_entry(touched, i, v, drop)) {
-                ++cnt;
-                pi += cbv[i] * v;
-            }
+        for (int q = cstart[c]; q < cstart[c] + keptc[c]; ++q) {
+            const int i = irow[q];
+            atomicAdd(&rowc[i], 1);
+            pi += cbv[i] * ival[q];
         }
-        A.colcnt[(size_t)a * m + c] = cnt;
         pi0[c] = pi;
+    }
+    // element rows: column row_e of B^{-1} gives element e an entry in each of its rows
+    for (int e = tid; e < k; e += kPgThreads) {
+        const int c = A.pos_row[e];
+        for (int q = cstart[c]; q < cstart[c] + keptc[c]; ++q) atomicAdd(&erow[irow[q]], 1);
     }
     __syncthreads();
     int bad = 0;
@@ -224,129 +255,75 @@ __global__ __launch_bounds__(kPgThreads) void pg_count_kernel(PgArgs A) {
         const double d = (j < n ? A.q[j] : 0.0) - s;
         if (!((bt == BT_G ? d : -d) <= 1e-7)) bad = 1;
     }
-    // B^{-1} a_{head[i0]} = e_{i0} at the probes of sparse_basis_residual (1e-8)
+    // B^{-1} a_{head[i0]} = e_{i0} at the probes of sparse_basis_residual (1e-8): the columns
+    // of B^{-1} at a's rows, scaled and accumulated
     for (int probe = 0; probe < 4; ++probe) {
         const int i0 = (int)(((long long)probe * 7919 + 13) % m), j = S.head[i0];
-        for (int i = tid; i < m; i += kPgThreads) {
-            double v = 0.0;
-            if (j >= n) {
-                const double d = D[(size_t)i * m + (j - n)];
-                if (keep_entry(touched, i, d, drop)) v = d;
-            } else {
-                for (int q = A.colptr[j]; q < A.colptr[j + 1]; ++q) {
-                    const double d = D[(size_t)i * m + A.rowidx[q]];
-                    if (keep_entry(touched, i, d, drop)) v += d * A.val[q];
-                }
-            }
-            if (!(fabs(v - (i == i0 ? 1.0 : 0.0)) <= 1e-8)) bad = 1;
+        __syncthreads();
+        for (int i = tid; i < m; i += kPgThreads) y[i] = 0.0;
+        __syncthreads();
+        const int q0 = j >= n ? 0 : A.colptr[j], q1 = j >= n ? 1 : A.colptr[j + 1];
+        for (int qa = q0; qa < q1; ++qa) {
+            const int r = j >= n ? j - n : A.rowidx[qa];
+            const double av = j >= n ? 1.0 : A.val[qa];
+            for (int q = cstart[r] + tid; q < cstart[r] + keptc[r]; q += kPgThreads) y[irow[q]] += ival[q] * av;
+            __syncthreads();   // rows are distinct within a column; columns one after another
         }
+        for (int i = tid; i < m; i += kPgThreads)
+            if (!(fabs(y[i] - (i == i0 ? 1.0 : 0.0)) <= 1e-8)) bad = 1;
     }
     if (bad) atomicOr(&s_bad, 1);
-    // ELL entry rows (sum over slots of the widest row) and selection records (every row
-    // active; rows of fixed basics twice), as prepare_elements
-    if (tid < A.R9) {
+    for (int i = tid; i < m; i += kPgThreads) {
+        A.rowcnt[(size_t)a * m + i] = rowc[i];
+        A.erowcnt[(size_t)a * m + i] = erow[i];
+        atomicAdd(&s_tot[0], rowc[i]);
+        atomicAdd(&s_tot[1], erow[i]);
+        // selection records: every row active, rows of fixed basics twice (prepare_elements)
+        atomicAdd(&s_tot[3], (1 + erow[i]) * (A.btype[S.head[i]] == BT_E ? 2 : 1));
+    }
+    if (tid < A.R9) {   // ELL entry rows: per slot of 64 rows the widest row
         int w = 0;
         for (int l = 0; l < 64 && 64 * tid + l < m; ++l) w = max(w, erow[64 * tid + l]);
         atomicAdd(&s_tot[2], w);
     }
-    for (int i = tid; i < m; i += kPgThreads)
-        atomicAdd(&s_tot[3], (1 + erow[i]) * (A.btype[S.head[i]] == BT_E ? 2 : 1));
     __syncthreads();
     if (tid < 4) A.tot[(size_t)a * 4 + tid] = s_tot[tid];
     if (tid == 0) A.valid[a] = s_bad ? 0 : 1;
 }
 
-// ---- 3. pool-strided outputs ------------------------------------------------------------
+// ---- 3. pool-strided outputs --------------------------------------------------------------
 __global__ __launch_bounds__(kPgThreads) void pg_fill_kernel(PgArgs A, PgFill F) {
     extern __shared__ double smem[];
     __shared__ int tmp[kPgThreads];
     __shared__ uint64_t bits[64];
-    __shared__ int ws[65];   // ELL slot widths, then slot offsets
+    __shared__ int ws[65];   // ELL slot offsets (entry rows)
     const int p = F.P0 + blockIdx.x, a = F.map[p];
     const int m = A.m, n = A.n, k = A.k, MP = A.MP, R9 = A.R9, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const Src S = src_of(A, a);
-    const double drop = 1e-14 * A.amax[a];
-    const double *D = A.D + (size_t)(a - A.a0) * m * m;
     double *pi0 = smem, *cbv = smem + m;
-    int *rs = reinterpret_cast<int *>(cbv + m), *cs = rs + (m + 1), *es = cs + (m + 1);
-    unsigned char *touched = reinterpret_cast<unsigned char *>(es + (m + 1)), *isb = touched + m;
-    for (int i = tid; i < m; i += kPgThreads) touched[i] = 0;
+    int *rs = reinterpret_cast<int *>(cbv + m), *cs = rs + (m + 1), *es = cs + (m + 1), *ic = es + (m + 1);
+    int *cur = ic + (m + 1), *ecur = cur + m;
+    unsigned char *isb = reinterpret_cast<unsigned char *>(ecur + m);
     for (int j = tid; j < n + m; j += kPgThreads) isb[j] = 0;
+    for (int i = tid; i < m; i += kPgThreads) { cur[i] = 0; ecur[i] = 0; }
     if (tid < 64) bits[tid] = 0;
     __syncthreads();
-    const int ne = S.K > 0 ? S.etaoff[S.K] : 0;
-    for (int e = tid; e < ne; e += kPgThreads) touched[A.eo_eidx[S.off + e]] = 1;
     for (int i = tid; i < m; i += kPgThreads) {
         const int j = S.head[i];
         isb[j] = 1;
         cbv[i] = j < n ? A.q[j] : 0.0;
         atomicOr(reinterpret_cast<unsigned long long *>(&bits[j & 63]), 1ull << (j >> 6));
     }
+    const int *keptc = A.keptc + (size_t)a * m;
     block_scan(A.rowcnt + (size_t)a * m, rs, m, tmp);
-    block_scan(A.colcnt + (size_t)a * m, cs, m, tmp);
+    block_scan(keptc, cs, m, tmp);
     block_scan(A.erowcnt + (size_t)a * m, es, m, tmp);
-    const int nb = F.off[(size_t)p * 4 + 0], eb = F.off[(size_t)p * 4 + 1];
-    // B^{-1} rows (CSR, columns ascending) and element rows (CSR, e ascending): one wave a row
-    for (int i = wv; i < m; i += kPgThreads / 64) {
-        int run = 0;
-        for (int c0 = 0; c0 < m; c0 += 64) {
-            const int c = c0 + lane;
-            const double v = c < m ? D[(size_t)i * m + c] : 0.0;
-            const bool kk = c < m && keep_entry(touched, i, v, drop);
-            const unsigned long long msk = __ballot(kk);
-            if (kk) {
-                const int at = nb + rs[i] + run + __popcll(msk & lanemask_lt(lane));
-                F.brcol[at] = c;
-                F.brval[at] = v;
-            }
-            run += __popcll(msk);
-        }
-        run = 0;
-        for (int e0 = 0; e0 < k; e0 += 64) {
-            const int e = e0 + lane;
-            const double v = e < k ? D[(size_t)i * m + A.pos_row[e]] : 0.0;
-            const bool kk = e < k && keep_entry(touched, i, v, drop);
-            const unsigned long long msk = __ballot(kk);
-            if (kk) {
-                const int at = eb + es[i] + run + __popcll(msk & lanemask_lt(lane));
-                F.ke[at] = e;
-                F.kraw[at] = v;
-            }
-            run += __popcll(msk);
-        }
-    }
-    for (int i = tid; i <= MP; i += kPgThreads) {
-        F.brptr[(size_t)p * (MP + 1) + i] = nb + rs[min(i, m)];
-        F.bcp[(size_t)p * (MP + 1) + i] = nb + cs[min(i, m)];
-    }
-    for (int i = tid; i <= m; i += kPgThreads) F.kp[(size_t)p * (m + 1) + i] = eb + es[i];
-    // B^{-1} columns (CSC, rows ascending) and pi0: one thread a column
-    for (int c = tid; c < m; c += kPgThreads) {
-        const int base = nb + cs[c];
-        int cnt = 0;
-        double pi = 0.0;
-        for (int i = 0; i < m; ++i) {
-            const double v = D[(size_t)i * m + c];
-            if (keep_entry(touched, i, v, drop)) {
-                F.bci[base + cnt] = i;
-                F.bcv[base + cnt] = v;
-                ++cnt;
-                pi += cbv[i] * v;
-            }
-        }
-        pi0[c] = pi;
-    }
-    // sliced ELL of the element rows: slot t = rows [64t, 64t + 64), width = widest row
-    if (tid < R9) {
-        int w = 0;
-        for (int l = 0; l < 64 && 64 * tid + l < m; ++l) w = max(w, es[64 * tid + l + 1] - es[64 * tid + l]);
-        ws[tid] = w;
-    }
-    __syncthreads();
-    if (tid == 0) {
+    block_scan(A.nzc + (size_t)a * m, ic, m, tmp);        // intermediate column starts
+    if (tid == 0) {   // ELL slots: widest element row of each 64 rows
         int o = F.off[(size_t)p * 4 + 2];
         for (int t = 0; t < R9; ++t) {
-            const int w = ws[t];
+            int w = 0;
+            for (int l = 0; l < 64 && 64 * t + l < m; ++l) w = max(w, es[64 * t + l + 1] - es[64 * t + l]);
             ws[t] = o;
             F.kslot[(size_t)p * (R9 + 1) + t] = o;
             o += w;
@@ -355,24 +332,64 @@ __global__ __launch_bounds__(kPgThreads) void pg_fill_kernel(PgArgs A, PgFill F)
         F.kslot[(size_t)p * (R9 + 1) + R9] = o;
     }
     __syncthreads();
-    for (int i = tid; i < 64 * R9; i += kPgThreads) {
-        const int t = i >> 6, l = i & 63, r0 = ws[t], w = ws[t + 1] - ws[t];
-        int j = 0;
-        if (i < m)
-            for (int e = 0; e < k; ++e) {
-                const double v = D[(size_t)i * m + A.pos_row[e]];
-                if (keep_entry(touched, i, v, drop)) {
-                    F.kix[(size_t)(r0 + j) * 64 + l] = e;
-                    F.kv[(size_t)(r0 + j) * 64 + l] = v;
-                    ++j;
-                }
+    const int nb = F.off[(size_t)p * 4 + 0], eb = F.off[(size_t)p * 4 + 1];
+    const int *irow = A.inter_row + A.inter_off[a];
+    const double *ival = A.inter_val + A.inter_off[a];
+    if (wv == 0) {
+        // B^{-1} rows (CSR, columns ascending): walk the columns in order, per-row cursors
+        for (int c = 0; c < m; ++c) {
+            for (int q = ic[c] + lane; q < ic[c] + keptc[c]; q += 64) {   // distinct rows
+                const int i = irow[q];
+                const int at = nb + rs[i] + cur[i]++;
+                F.brcol[at] = c;
+                F.brval[at] = ival[q];
             }
-        for (; j < w; ++j) {
-            F.kix[(size_t)(r0 + j) * 64 + l] = 0;
-            F.kv[(size_t)(r0 + j) * 64 + l] = 0.0;
+            __builtin_amdgcn_wave_barrier();
+        }
+    } else if (wv == 1) {
+        // element rows (CSR, e ascending) and their sliced ELL: walk the elements in order
+        for (int e = 0; e < k; ++e) {
+            const int c = A.pos_row[e];
+            for (int q = ic[c] + lane; q < ic[c] + keptc[c]; q += 64) {
+                const int i = irow[q];
+                const double v = ival[q];
+                const int j = ecur[i]++;
+                F.ke[eb + es[i] + j] = e;
+                F.kraw[eb + es[i] + j] = v;
+                const size_t at = ((size_t)ws[i >> 6] + j) * 64 + (i & 63);
+                F.kix[at] = e;
+                F.kv[at] = v;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    } else {
+        // B^{-1} columns (CSC, rows ascending, compacted) and pi0 (rows ascending)
+        for (int c = tid - 128; c < m; c += kPgThreads - 128) {
+            const int base = nb + cs[c];
+            double pi = 0.0;
+            for (int q = 0; q < keptc[c]; ++q) {
+                const int i = irow[ic[c] + q];
+                const double v = ival[ic[c] + q];
+                F.bci[base + q] = i;
+                F.bcv[base + q] = v;
+                pi += cbv[i] * v;
+            }
+            pi0[c] = pi;
+        }
+        // ELL padding: entries [rows of row i, slot width) of every lane (rows >= m: all)
+        for (int i = tid - 128; i < 64 * R9; i += kPgThreads - 128) {
+            const int t = i >> 6, l = i & 63, w = ws[t + 1] - ws[t];
+            for (int j = i < m ? es[i + 1] - es[i] : 0; j < w; ++j) {
+                F.kix[((size_t)ws[t] + j) * 64 + l] = 0;
+                F.kv[((size_t)ws[t] + j) * 64 + l] = 0.0;
+            }
         }
     }
-    // basis words
+    for (int i = tid; i <= MP; i += kPgThreads) {
+        F.brptr[(size_t)p * (MP + 1) + i] = nb + rs[min(i, m)];
+        F.bcp[(size_t)p * (MP + 1) + i] = nb + cs[min(i, m)];
+    }
+    for (int i = tid; i <= m; i += kPgThreads) F.kp[(size_t)p * (m + 1) + i] = eb + es[i];
     for (int i = tid; i < MP; i += kPgThreads)
         F.hb0[(size_t)p * MP + i] = i < m ? S.head[i] * 4 + A.btype[S.head[i]] : -1;
     if (tid < 64) F.basic0[(size_t)p * 64 + tid] = bits[tid];
@@ -398,32 +415,36 @@ __global__ __launch_bounds__(kPgThreads) void pg_fill_kernel(PgArgs A, PgFill F)
     }
 }
 
+static size_t ftran_lds(const PgArgs &A) {
+    return sizeof(double) * kPgWaves * A.m + sizeof(int) * (2 * A.kmax + 1 + A.m + 1) + A.m + 16;
+}
 static size_t count_lds(const PgArgs &A) {
-    return sizeof(double) * 2 * A.m + sizeof(int) * A.m + A.m + (A.n + A.m) + 16;
+    return sizeof(double) * 3 * A.m + sizeof(int) * (3 * A.m + 1) + (A.n + A.m) + 16;
 }
 static size_t fill_lds(const PgArgs &A) {
-    return sizeof(double) * 2 * A.m + sizeof(int) * 3 * (A.m + 1) + A.m + (A.n + A.m) + 16;
+    return sizeof(double) * 2 * A.m + sizeof(int) * (4 * (A.m + 1) + 2 * A.m) + (A.n + A.m) + 16;
 }
 
-hipError_t pg_launch_dense(const PgArgs &A, int nb, hipStream_t s) {
-    const size_t lds = (size_t)A.m * A.W * sizeof(double);
-    hipError_t e = hipFuncSetAttribute((const void *)pg_dense_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(pg_dense_kernel, dim3(nb), dim3(kPgThreads), lds, s, A);
+int pg_supported(int m, int n, int kmax) {
+    PgArgs A{};
+    A.m = m; A.n = n; A.kmax = kmax;
+    return ftran_lds(A) <= 64 * 1024 && count_lds(A) <= 64 * 1024 && fill_lds(A) <= 64 * 1024 && (m + 63) / 64 <= 64;
+}
+
+template <int PASS>
+static hipError_t launch_ftran(const PgArgs &A, int nb, hipStream_t s) {
+    hipLaunchKernelGGL(pg_ftran_kernel<PASS>, dim3(nb), dim3(kPgThreads), ftran_lds(A), s, A);
     return hipGetLastError();
 }
+hipError_t pg_launch_ftran(const PgArgs &A, int pass, int nb, hipStream_t s) {
+    return pass == 0 ? launch_ftran<0>(A, nb, s) : launch_ftran<1>(A, nb, s);
+}
 hipError_t pg_launch_count(const PgArgs &A, int nb, hipStream_t s) {
-    const size_t lds = count_lds(A);
-    hipError_t e = hipFuncSetAttribute((const void *)pg_count_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(pg_count_kernel, dim3(nb), dim3(kPgThreads), lds, s, A);
+    hipLaunchKernelGGL(pg_count_kernel, dim3(nb), dim3(kPgThreads), count_lds(A), s, A);
     return hipGetLastError();
 }
 hipError_t pg_launch_fill(const PgArgs &A, const PgFill &F, int np, hipStream_t s) {
-    const size_t lds = fill_lds(A);
-    hipError_t e = hipFuncSetAttribute((const void *)pg_fill_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(pg_fill_kernel, dim3(np), dim3(kPgThreads), lds, s, A, F);
+    hipLaunchKernelGGL(pg_fill_kernel, dim3(np), dim3(kPgThreads), fill_lds(A), s, A, F);
     return hipGetLastError();
 }
 

@@ -145,9 +145,11 @@ struct twosd_ctx {
     int *d_refresh_sel = nullptr;                  // refresh: scenarios to re-solve
     size_t refresh_sel_cap = 0;
     int box_epi = -1, box_first = -1, box_count = -1, box_n = -1;   // training range of sel_lo / sel_hi
-    // device pool build of a refresh (pool_gpu.hip): dense scratch, per-source counts and
+    // device pool build of a refresh (pool_gpu.hip): intermediate CSC, per-source counts and
     // checks, pool map / offsets, primary head and d0
-    double *d_pg_D = nullptr, *d_pg_amax = nullptr, *d_pg_d0p = nullptr;
+    double *d_pg_amax = nullptr, *d_pg_d0p = nullptr, *d_pg_ival = nullptr;
+    int *d_pg_irow = nullptr;
+    long long *d_pg_ioff = nullptr;
     int *d_pg_cnt = nullptr, *d_pg_tot = nullptr, *d_pg_valid = nullptr, *d_pg_head0 = nullptr;
     int *d_pg_map = nullptr, *d_pg_off = nullptr, *d_pg_pos = nullptr;
     // pinned host staging buffers of the pool upload, kept across uploads (no page faults,

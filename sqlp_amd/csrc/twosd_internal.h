@@ -73,19 +73,24 @@ struct HyperParams {
 
 // ---- device pool build of a refresh (pool_gpu.hip) ---------------------------------
 // Source a of a build: a = 0 the primary basis (start pool basis 0, no etas, head0), a >= 1
-// the eta file and head of list position a - 1 of the refresh re-solve.  B^{-1} of every
-// source is composed densely (column tiles of W in LDS), checked, counted, and then written
-// into the pool-strided arrays of upload_pool / prepare_elements at host-computed offsets.
+// the eta file and head of list position a - 1 of the refresh re-solve.  Every column of
+// B^{-1} is the start basis's column pushed through the eta file (pg_ftran_kernel, two
+// passes: max / counts, then the kept entries into an intermediate CSC), checked and counted
+// (pg_count_kernel), and written into the pool-strided arrays of upload_pool /
+// prepare_elements at host-computed offsets (pg_fill_kernel).
 struct PgArgs {
-    int m, n, MP, CH, R9, k, W, kmax, npool_old;
+    int m, n, MP, CH, R9, k, kmax, npool_old;
     const int *colptr, *rowidx; const double *val, *q; const int8_t *btype; const int *pos_row;
     const int *bcp0, *bci0; const double *bcv0;          // start pool: B^{-1} CSC (pool-strided)
     const int *eo_pb, *eo_K, *eo_off, *eo_etap, *eo_etaoff, *eo_eidx; const double *eo_evals;
     const int *head0, *heads;                            // primary head (m); heads by list position
-    double *D;                                           // dense B^{-1} of sources [a0, a0 + batch)
-    int a0;
+    int a0;                                              // first source of the launch
     double *amax;                                        // nsrc (-1: source unusable)
-    int *rowcnt, *colcnt, *erowcnt;                      // nsrc x m
+    int *nzc, *keptc;                                    // nsrc x m: nonzeros / kept entries per column
+    int *nztot;                                          // nsrc: sum of nzc
+    const long long *inter_off;                          // nsrc: intermediate CSC offsets
+    int *inter_row; double *inter_val;
+    int *rowcnt, *erowcnt;                               // nsrc x m
     int *tot;                                            // nsrc x 4: nnz, element entries, ELL rows, records
     int *valid;                                          // nsrc
 };
@@ -99,8 +104,8 @@ struct PgFill {
     int *kp, *ke; double *kraw; int *kslot, *kix; double *kv;
     int *hb0; uint64_t *basic0; int *bnnz; double *d0; int *sel_ptr;
 };
-int pg_tile_width(int m);                                // 0: m too large for the LDS tile
-hipError_t pg_launch_dense(const PgArgs &A, int nb, hipStream_t s);
+int pg_supported(int m, int n, int kmax);                // the LDS layouts fit
+hipError_t pg_launch_ftran(const PgArgs &A, int pass, int nb, hipStream_t s);
 hipError_t pg_launch_count(const PgArgs &A, int nb, hipStream_t s);
 hipError_t pg_launch_fill(const PgArgs &A, const PgFill &F, int np, hipStream_t s);
 
