@@ -260,8 +260,11 @@ def main():
         if args.pool_level1 > 0 and ctx.pool_size() > args.pool_level1:
             ctx.pool_build_candidates(rtr, xx, 0, args.refresh_train, args.pool_level1, args.pool_cands)
         pool_at["x"] = xx.copy()
-        # [training solves, re-solves, composition, upload, refresh total, candidate lists] ms
-        pool_at["last_ms"] = list(ctx.last_refresh_ms()) + [1e3 * (time.perf_counter() - t1)]
+        # ms: training solves (with eta files), basis keys + selection, pool build (device:
+        # B^-1 FTRAN + pool arrays; host path: composition), host upload (host path only),
+        # refresh total, two-level candidate lists
+        ms = list(ctx.last_refresh_ms()) + [1e3 * (time.perf_counter() - t1)]
+        pool_at["last_ms"] = dict(zip(("train", "keys", "build", "host_upload", "total", "candidates"), ms))
         return time.perf_counter() - t0
 
     heads_at = {}    # first pool bases at each x point (the pooled CPU baseline starts from the same bases)
@@ -271,7 +274,7 @@ def main():
         if rec:
             per_x[cur["xi"]]["refresh"] += t_ref
             if t_ref > 0:
-                per_x[cur["xi"]]["refresh_parts"] = [round(v, 2) for v in pool_at["last_ms"]]
+                per_x[cur["xi"]]["refresh_parts"] = {k_: round(v, 2) for k_, v in pool_at["last_ms"].items()}
             if cur["xi"] not in heads_at and not args.no_cpu and rank == 0:
                 heads_at[cur["xi"]] = np.stack([ctx.pool_get(p) for p in range(min(args.cpu_pool, ctx.pool_size()))])
         ctx.invalidate_x()     # every pass pays its per-x setup (x_B of the pool, selection data)

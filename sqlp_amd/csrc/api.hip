@@ -777,13 +777,16 @@ static const char *finish_composed(const twosd_ctx *c, PoolBasis &B) {
     return nullptr;
 }
 
-// Device build of the refreshed pool (pool_gpu.hip) from the re-solve's eta files and heads
-// (list positions 0..R-1 in c->d_eo_* / c->d_head_out): sources a = 0 (primary) .. R are
+// Device build of the refreshed pool (pool_gpu.hip) from the eta files and heads of the
+// training solves (rows = training scenarios in c->d_eo_* / c->d_head_out; sel = the
+// representatives, also in c->d_refresh_sel): sources a = 0 (primary), a
+// = 1..R (scenario sel[a - 1]) are
 // composed column by column, checked, and the sources that passed are written in order as
 // pool[0..P) -- the arrays upload_pool + prepare_elements would produce.  Returns 1, with the
 // pool unchanged, when the LDS layouts do not fit or the primary fails the device checks (the
 // caller then composes on the host).
-static int refresh_build_device(twosd_ctx *c, int R) {
+static int refresh_build_device(twosd_ctx *c, const std::vector<int> &sel) {
+    const int R = (int)sel.size();
     const HostLP &L = c->L;
     const int m = L.m, n = L.n, MP = c->MP, nsrc = R + 1;
     if (!pg_supported(m, n, c->eo_kmax)) return 1;
@@ -804,7 +807,7 @@ static int refresh_build_device(twosd_ctx *c, int R) {
     A.bcp0 = c->d_bcp; A.bci0 = c->d_bci; A.bcv0 = c->d_bcv;
     A.eo_pb = c->d_eo_pb; A.eo_K = c->d_eo_K; A.eo_off = c->d_eo_off; A.eo_etap = c->d_eo_etap;
     A.eo_etaoff = c->d_eo_etaoff; A.eo_eidx = c->d_eo_eidx; A.eo_evals = c->d_eo_evals;
-    A.head0 = c->d_pg_head0; A.heads = c->d_head_out;
+    A.head0 = c->d_pg_head0; A.heads = c->d_head_out; A.src_row = c->d_refresh_sel;
     A.a0 = 0;
     A.amax = c->d_pg_amax;
     A.nzc = c->d_pg_cnt; A.keptc = c->d_pg_cnt + (size_t)nsrc * m;
@@ -835,12 +838,12 @@ static int refresh_build_device(twosd_ctx *c, int R) {
     HIPCHK(pg_launch_ftran(A, 1, nsrc, c->stream));
     HIPCHK(pg_launch_count(A, nsrc, c->stream));
     const auto t2 = now();
-    int *h_tot = stage_buf<int>(c, 9, (size_t)5 * nsrc), *h_heads = stage_buf<int>(c, 10, (size_t)R * m);
-    if (!h_tot || !h_heads) return fail(TWOSD_E_DEVICE, "pool refresh: pinned staging allocation failed");
+    int *h_tot = stage_buf<int>(c, 9, (size_t)5 * nsrc);
+    if (!h_tot) return fail(TWOSD_E_DEVICE, "pool refresh: pinned staging allocation failed");
     int *h_valid = h_tot + (size_t)4 * nsrc;
     HIPCHK(hipMemcpyAsync(h_tot, c->d_pg_tot, sizeof(int) * 4 * nsrc, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(h_valid, c->d_pg_valid, sizeof(int) * nsrc, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(h_heads, c->d_head_out, sizeof(int) * R * m, hipMemcpyDeviceToHost, c->stream));
+
     HIPCHK(hipStreamSynchronize(c->stream));
     if (!h_valid[0]) return 1;   // the primary basis failed the device checks: host path
     // pool = the sources that passed, in order; offsets = prefix sums of their totals
@@ -881,6 +884,9 @@ static int refresh_build_device(twosd_ctx *c, int R) {
     F.P0 = 0;
     const auto t3 = now();
     HIPCHK(pg_launch_fill(A, F, P, c->stream));
+    int *h_hb = stage_buf<int>(c, 10, (size_t)P * MP);   // the pool's heads, from hb0 = 4 head + type
+    if (!h_hb) return fail(TWOSD_E_DEVICE, "pool refresh: pinned staging allocation failed");
+    HIPCHK(hipMemcpyAsync(h_hb, c->d_hb0, sizeof(int) * P * MP, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     if (dbg) {
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -893,8 +899,8 @@ static int refresh_build_device(twosd_ctx *c, int R) {
     keep.push_back(std::move(c->pool[0]));
     for (int p = 1; p < P; ++p) {
         PoolBasis B;
-        const int l = map[p] - 1;
-        B.head.assign(h_heads + (size_t)l * m, h_heads + (size_t)(l + 1) * m);
+        B.head.resize(m);
+        for (int i = 0; i < m; ++i) B.head[i] = h_hb[(size_t)p * MP + i] >> 2;
         B.dev_only = true;
         keep.push_back(std::move(B));
     }
@@ -920,9 +926,11 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
     const int m = c->L.m;
     const double *d_dv = E.d_dv + (size_t)first * c->k;
     int rc;
-    // 1. training solves at x from the current pool, basis keys
+    // 1. training solves at x from the current pool: basis keys, eta files and heads by scenario
     LpRun o;
     o.want_bkey = true;
+    o.want_etas = true;
+    o.want_head = true;
     if ((rc = run_lp_ex(c, x, d_dv, count, o))) return rc;
     const auto t1 = std::chrono::steady_clock::now();
     // 2. distinct optimal bases, most frequent first (ties: first occurrence), primary excluded
@@ -943,39 +951,30 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
     for (int a = 0; a < R; ++a) sel[a] = reps[ord[a]];
     std::vector<PoolBasis> fresh;
     bool device_built = false;
-    if (R > 0) {
-        // 3. re-solve the selected scenarios (same starts, so the same pivots) with their eta files
+    c->last_refresh_ms[1] = std::chrono::duration<double, std::milli>(t1b - t1).count();
+    c->last_refresh_ms[2] = c->last_refresh_ms[3] = 0.0;
+    if (R > 0 && !getenv("TWOSD_REFRESH_HOST")) {
+        // 3. B^{-1} of the representatives from their eta files, and the pool arrays, on the device
         if ((size_t)R > c->refresh_sel_cap) {
             if ((rc = dalloc(&c->d_refresh_sel, (size_t)R))) return rc;
             c->refresh_sel_cap = R;
         }
-        int *d_sel = c->d_refresh_sel;
-        HIPCHK(hipMemcpy(d_sel, sel.data(), sizeof(int) * R, hipMemcpyHostToDevice));
-        LpRun r;
-        r.d_list = d_sel;
-        r.nlist = R;
-        r.want_etas = true;
-        r.want_head = true;
-        rc = run_lp_ex(c, x, d_dv, count, r);
-        if (rc) return rc;
-        int dev = 1;
-        if (!getenv("TWOSD_REFRESH_HOST")) {
-            HIPCHK(hipStreamSynchronize(c->stream));
-            const auto t2 = std::chrono::steady_clock::now();
-            c->last_refresh_ms[1] = std::chrono::duration<double, std::milli>(t2 - t1).count();
-            if ((dev = refresh_build_device(c, R)) < 0) return dev;
-            c->last_refresh_ms[2] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count();
-        }
+        HIPCHK(hipMemcpyAsync(c->d_refresh_sel, sel.data(), sizeof(int) * R, hipMemcpyHostToDevice, c->stream));
+        const int dev = refresh_build_device(c, sel);
+        if (dev < 0) return dev;
         device_built = dev == 0;
+        c->last_refresh_ms[2] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1b).count();
     }
     if (R > 0 && !device_built) {
+        // 3'. host path: compose on the host threads, then upload_pool + prepare_elements
         if ((rc = ensure_host_pool(c))) return rc;   // start bases in host form
         const int kmax = c->eo_kmax;
-        std::vector<int> pb(R), K(R), off(R), etap((size_t)R * kmax), etaoff((size_t)R * (kmax + 1)), heads((size_t)R * m);
+        std::vector<int> pb(count), K(count), off(count), etap((size_t)count * kmax), etaoff((size_t)count * (kmax + 1)),
+            heads((size_t)count * m);
         int used = 0;
-        HIPCHK(hipMemcpy(pb.data(), c->d_eo_pb, sizeof(int) * R, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(K.data(), c->d_eo_K, sizeof(int) * R, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(off.data(), c->d_eo_off, sizeof(int) * R, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(pb.data(), c->d_eo_pb, sizeof(int) * count, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(K.data(), c->d_eo_K, sizeof(int) * count, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(off.data(), c->d_eo_off, sizeof(int) * count, hipMemcpyDeviceToHost));
         HIPCHK(hipMemcpy(etap.data(), c->d_eo_etap, sizeof(int) * etap.size(), hipMemcpyDeviceToHost));
         HIPCHK(hipMemcpy(etaoff.data(), c->d_eo_etaoff, sizeof(int) * etaoff.size(), hipMemcpyDeviceToHost));
         HIPCHK(hipMemcpy(heads.data(), c->d_head_out, sizeof(int) * heads.size(), hipMemcpyDeviceToHost));
@@ -988,8 +987,6 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
             HIPCHK(hipMemcpy(ev.data(), c->d_eo_evals, sizeof(double) * used, hipMemcpyDeviceToHost));
         }
         const auto t2 = std::chrono::steady_clock::now();
-        c->last_refresh_ms[1] = std::chrono::duration<double, std::milli>(t2 - t1).count();
-        // 4. compose B^{-1} of every new basis on the host threads
         fresh.resize(R);
         std::vector<char> ok(R, 0);
         const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -997,13 +994,14 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
         for (unsigned t = 0; t < nth; ++t)
             th.emplace_back([&, t]() {
                 for (int a = (int)t; a < R; a += (int)nth) {
-                    if (K[a] < 0 || pb[a] < 0 || pb[a] >= (int)c->pool.size()) continue;
+                    const int l = sel[a];   // eta-file row: the training scenario
+                    if (K[l] < 0 || pb[l] < 0 || pb[l] >= (int)c->pool.size()) continue;
                     PoolBasis &B = fresh[a];
-                    B.head.assign(heads.begin() + (size_t)a * m, heads.begin() + (size_t)(a + 1) * m);
-                    const int *eo = etaoff.data() + (size_t)a * (kmax + 1);
-                    const PoolBasis &B0 = c->pool[pb[a]];
-                    compose_binv(m, B0.rptr, B0.rcol, B0.rval, K[a], etap.data() + (size_t)a * kmax, eo, ei.data() + off[a],
-                                 ev.data() + off[a], B.rptr, B.rcol, B.rval);
+                    B.head.assign(heads.begin() + (size_t)l * m, heads.begin() + (size_t)(l + 1) * m);
+                    const int *eo = etaoff.data() + (size_t)l * (kmax + 1);
+                    const PoolBasis &B0 = c->pool[pb[l]];
+                    compose_binv(m, B0.rptr, B0.rcol, B0.rval, K[l], etap.data() + (size_t)l * kmax, eo, ei.data() + off[l],
+                                 ev.data() + off[l], B.rptr, B.rcol, B.rval);
                     ok[a] = finish_composed(c, B) == nullptr;
                 }
             });
@@ -1019,7 +1017,6 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
         std::thread([old = std::move(keep)]() mutable { old.clear(); }).detach();
     } else if (R == 0) {
         c->pool.resize(1);
-        c->last_refresh_ms[1] = c->last_refresh_ms[2] = 0.0;
     }
     const auto tb = std::chrono::steady_clock::now();
     // training box of the deltas (selection row pruning), as twosd_pool_build; cached per
@@ -1043,7 +1040,7 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
     const auto t3 = std::chrono::steady_clock::now();
     if (getenv("TWOSD_DEBUG")) {
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        fprintf(stderr, "pool_refresh: train %.2f, keys %.2f, re-solve+compose %.2f, box %.2f, upload_pool %.2f, elements %.2f ms (R=%d)\n",
+        fprintf(stderr, "pool_refresh: train %.2f, keys %.2f, build %.2f, box %.2f, upload_pool %.2f, elements %.2f ms (R=%d)\n",
                 ms(t0, t1), ms(t1, t1b), ms(t1b, tb), ms(tb, tu), ms(tu, tua), ms(tua, t3), R);
     }
     c->last_refresh_ms[0] = std::chrono::duration<double, std::milli>(t1 - t0).count();
@@ -1757,9 +1754,10 @@ int twosd::run_lp_ex(twosd_ctx *c, const double *x, const double *d_dv, int N, c
         H.obj = c->d_obj; H.pi = want_pi ? c->d_pi : nullptr; H.y = want_y ? c->d_y : nullptr;
         H.vkey = o.want_key ? c->d_vkey : nullptr;
         H.bkey = o.want_bkey ? c->d_bkey : nullptr;
-        if (list && o.want_etas) {
-            if ((size_t)NL > c->eo_rows || c->eo_kmax != kmax) {
-                const size_t rows = std::max<size_t>(NL, 256);
+        if (o.want_etas) {   // rows: list positions, or scenarios
+            const size_t need = list ? (size_t)NL : (size_t)N;
+            if (need > c->eo_rows || c->eo_kmax != kmax) {
+                const size_t rows = std::max<size_t>(need, 256);
                 if ((rc = dalloc(&c->d_eo_pb, rows)) || (rc = dalloc(&c->d_eo_K, rows)) || (rc = dalloc(&c->d_eo_off, rows)) ||
                     (rc = dalloc(&c->d_eo_etap, rows * kmax)) || (rc = dalloc(&c->d_eo_etaoff, rows * (kmax + 1))) ||
                     (rc = dalloc(&c->d_eo_eidx, rows * 4096)) || (rc = dalloc(&c->d_eo_evals, rows * 4096)))
@@ -1774,10 +1772,11 @@ int twosd::run_lp_ex(twosd_ctx *c, const double *x, const double *d_dv, int N, c
             H.eo_etaoff = c->d_eo_etaoff; H.eo_eidx = c->d_eo_eidx; H.eo_evals = c->d_eo_evals; H.eo_used = c->d_eo_used;
             H.eo_cap = (int)std::min<size_t>(c->eo_cap, INT32_MAX);
         }
-        if (list && o.want_head) {
-            if ((size_t)NL > c->head_cap) {
-                if ((rc = dalloc(&c->d_head_out, (size_t)NL * m))) return rc;
-                c->head_cap = NL;
+        if (o.want_head) {   // rows: list positions, or scenarios
+            const size_t need = list ? (size_t)NL : (size_t)N;
+            if (need > c->head_cap) {
+                if ((rc = dalloc(&c->d_head_out, need * m))) return rc;
+                c->head_cap = need;
             }
             H.head_out = c->d_head_out;
         }

@@ -706,6 +706,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             if (lane == 0) P.bkey[s] = h;
         }
         if (P.eo_K) {   // eta file of the solve (pool refresh composes B^{-1} = E_K..E_1 B_pb^{-1} from it)
+            const int erow = P.pi_by_pos ? qpos : s;
             int off = 0;
             if (lane == 0 && status == TWOSD_LP_OPTIMAL) off = atomicAdd(P.eo_used, eoff);
             off = __builtin_amdgcn_readfirstlane(__shfl(off, 0));
@@ -715,13 +716,13 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                     P.eo_eidx[off + e] = eidx[e];
                     P.eo_evals[off + e] = evals[e];
                 }
-                for (int t = lane; t < K; t += 64) P.eo_etap[(size_t)qpos * P.kmax + t] = etap[t];
-                for (int t = lane; t <= K; t += 64) P.eo_etaoff[(size_t)qpos * (P.kmax + 1) + t] = etaoff[t];
+                for (int t = lane; t < K; t += 64) P.eo_etap[(size_t)erow * P.kmax + t] = etap[t];
+                for (int t = lane; t <= K; t += 64) P.eo_etaoff[(size_t)erow * (P.kmax + 1) + t] = etaoff[t];
             }
             if (lane == 0) {
-                P.eo_K[qpos] = ok ? K : -1;
-                P.eo_off[qpos] = off;
-                P.eo_pb[qpos] = pb;
+                P.eo_K[erow] = ok ? K : -1;
+                P.eo_off[erow] = off;
+                P.eo_pb[erow] = pb;
             }
         }
         if (lane == 0) {

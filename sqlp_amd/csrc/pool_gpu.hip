@@ -44,7 +44,7 @@ __device__ inline Src src_of(const PgArgs &A, int a) {
         s.pb = 0; s.K = 0; s.off = 0; s.head = A.head0; s.etap = nullptr; s.etaoff = nullptr;
         return s;
     }
-    const int l = a - 1;
+    const int l = A.src_row[a - 1];
     s.pb = A.eo_pb[l];
     s.K = A.eo_K[l];
     s.off = A.eo_off[l];

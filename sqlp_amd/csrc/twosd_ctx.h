@@ -171,8 +171,8 @@ int run_lp(twosd_ctx *c, const double *x, const double *d_dv, int N, bool want_p
 struct LpRun {
     bool want_pi = false, want_y = false, want_key = false;
     bool want_bkey = false;       // basis keys into c->d_bkey
-    bool want_etas = false;       // list mode: eta files into c->eo (pool refresh)
-    bool want_head = false;       // list mode: final heads by list position into c->d_head_out
+    bool want_etas = false;       // eta files into c->eo (pool refresh), rows by list position / scenario
+    bool want_head = false;       // final heads into c->d_head_out, rows by list position / scenario
     const int *d_list = nullptr;  // list mode: scenarios (indices into d_dv) to solve, no selection
     int nlist = 0;
 };

@@ -73,7 +73,7 @@ struct HyperParams {
 
 // ---- device pool build of a refresh (pool_gpu.hip) ---------------------------------
 // Source a of a build: a = 0 the primary basis (start pool basis 0, no etas, head0), a >= 1
-// the eta file and head of list position a - 1 of the refresh re-solve.  Every column of
+// the eta file and head of training scenario src_row[a - 1] of the refresh.  Every column of
 // B^{-1} is the start basis's column pushed through the eta file (pg_ftran_kernel, two
 // passes: max / counts, then the kept entries into an intermediate CSC), checked and counted
 // (pg_count_kernel), and written into the pool-strided arrays of upload_pool /
@@ -83,7 +83,8 @@ struct PgArgs {
     const int *colptr, *rowidx; const double *val, *q; const int8_t *btype; const int *pos_row;
     const int *bcp0, *bci0; const double *bcv0;          // start pool: B^{-1} CSC (pool-strided)
     const int *eo_pb, *eo_K, *eo_off, *eo_etap, *eo_etaoff, *eo_eidx; const double *eo_evals;
-    const int *head0, *heads;                            // primary head (m); heads by list position
+    const int *head0, *heads;                            // primary head (m); heads (eta-file rows)
+    const int *src_row;                                  // source a >= 1: eta-file / head row src_row[a - 1]
     int a0;                                              // first source of the launch
     double *amax;                                        // nsrc (-1: source unusable)
     int *nzc, *keptc;                                    // nsrc x m: nonzeros / kept entries per column
