@@ -312,7 +312,7 @@ def main():
     barrier()
     acc = {"lp": 0.0, "dd": 0.0, "cut": 0.0, "fin": 0.0, "sel": 0.0, "flops": 0.0, "piv": 0, "pmax": 0}
     per_x = [{"piv": 0, "n": 0, "lp": 0.0, "wall": 0.0, "steps": 0, "alpha": None, "refresh": 0.0} for _ in xs]
-    cur = {"xi": 0}
+    cur = {"xi": 0, "piv": 0, "lp": 0.0}
 
     def record():
         tm = ctx.timings_us()
@@ -322,13 +322,19 @@ def main():
         acc["piv"] += ps; acc["pmax"] = max(acc["pmax"], pm)
         px = per_x[cur["xi"]]
         px["piv"] += ps; px["n"] += n_local; px["lp"] += tm[0]
+        cur["piv"] += ps; cur["lp"] += tm[0]
     t0 = time.perf_counter()
+    step_log = []    # per timed step: x index, wall ms, refresh ms, LP kernel ms, mean pivots
     for i in range(args.steps):
         cur["xi"] = i % X
+        cur["piv"] = 0; cur["lp"] = 0.0
         ts = time.perf_counter()
+        r0 = per_x[i % X]["refresh"]
         alpha = step(xs[i % X], record)
         px = per_x[i % X]
         px["wall"] += time.perf_counter() - ts; px["steps"] += 1; px["alpha"] = alpha
+        step_log.append([i % X, round(1e3 * (time.perf_counter() - ts), 2), round(1e3 * (px["refresh"] - r0), 2),
+                         round(cur["lp"] / 1e3, 2), round(cur["piv"] / max(n_local * E, 1), 3)])
     barrier()
     elapsed = time.perf_counter() - t0
     t_lp, t_dd, t_cut, t_fin, t_sel = acc["lp"], acc["dd"], acc["cut"], acc["fin"], acc["sel"]
@@ -398,6 +404,7 @@ def main():
                                "cut_partial": t_cut / K / 1e3, "cut_finalize": t_fin / K / 1e3},
         "lp_pivots_mean": piv_sum / (passes * n_local), "lp_pivots_max": piv_max,
         "x_points": x_points,
+        "steps_log": {"columns": ["x_index", "ms", "refresh_ms", "lp_kernel_ms", "lp_pivots_mean"], "rows": step_log},
         "roofline": {"kernel": "lp_hyper_kernel", "bound": "mfma",
                      "note": "fp64 peak (vector == matrix on gfx950); achieved = counted fp64 FLOPs of the executed pivot path / LP kernel time",
                      "achieved": lp_tflops, "peak": PEAK_FP64_TFS, "unit": "TFLOP/s",
