@@ -110,9 +110,11 @@ int twosd_pool_build_candidates(twosd_ctx *ctx, int epi, const double *x, int fi
  * frequent optimal bases (ties: first occurrence).  A pool's bases are optimal near the x they
  * were harvested at, so a first-stage point far from the last one (an SD candidate, the x
  * of an evaluate) gets a pool of its own.  B^{-1} of each new basis is composed from its start
- * basis and the eta file of its solve (no refactorisation).  Selection becomes flat (candidate
- * lists reset).  last_refresh_ms: [training solves, re-solves of the harvested scenarios,
- * host composition, upload of the pool's device form, total] of the last refresh. */
+ * basis and the eta file of its training solve (no refactorisation), on the device by default
+ * (TWOSD_REFRESH_HOST=1: on the host, then uploaded; same pool).  Selection becomes flat
+ * (candidate lists reset).  last_refresh_ms: [training solves, basis keys + selection, pool
+ * build (device; host path: composition), host upload (host path only), total] of the last
+ * refresh. */
 int twosd_pool_refresh(twosd_ctx *ctx, int epi, const double *x, int first, int count, int max_pool,
                        int *pool_size);
 int twosd_last_refresh_ms(twosd_ctx *ctx, double *ms5);

@@ -114,6 +114,11 @@ pool_build_candidates!(ctx::HipContext, epi::HipEpigraph, x::Vector{Float64}, co
     check(ccall((:twosd_pool_build_candidates, LIB), Cint, (Ptr{Cvoid}, Cint, Ptr{Float64}, Cint, Cint, Cint, Cint),
                 ctx.h, epi.index, x, 0, count, level1, ncand))
 
+# per-x pool (timed in the bench): rebuilt from the optimal bases of training scenarios at x
+pool_refresh!(ctx::HipContext, epi::HipEpigraph, x::Vector{Float64}, count::Integer, max_pool::Integer) =
+    (n = Ref{Cint}(0); check(ccall((:twosd_pool_refresh, LIB), Cint,
+        (Ptr{Cvoid}, Cint, Ptr{Float64}, Cint, Cint, Cint, Ref{Cint}), ctx.h, epi.index, x, 0, count, max_pool, n)); n[])
+
 # push!(::sdDualVertexSet, π)                         dual_set.jl:84-94 (the set lives on the GPU)
 struct HipDualVertexSet; ctx::HipContext; end
 function Base.push!(V::HipDualVertexSet, π::Vector{Float64})
