@@ -73,12 +73,16 @@ __global__ void cut_pk_kernel(int from, int to, int m, int k, int k4, int vcap, 
 
 // PKTc[kk][v] = coef_kk * PKT[kk][v] over rows [0, rows) x columns [0, vcap32), zero outside
 // [0, k) x [0, nv) (the LDS-DMA source of cut_argmax2_kernel; per x)
+// With base != nullptr, row k holds base[v] (-inf for v >= nv): the MFMA then adds the vertex
+// base through a constant 1 in the scenarios' delta column k.
 __global__ void cut_pktc_kernel(int nv, int k, int rows, int vcap, int vcap32, const double *__restrict__ PKT,
-                                const double *__restrict__ coef, double *__restrict__ PKTc) {
+                                const double *__restrict__ coef, const double *__restrict__ base, double *__restrict__ PKTc) {
     const size_t total = (size_t)rows * vcap32;
     for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
         const int kk = (int)(idx / vcap32), v = (int)(idx % vcap32);
-        PKTc[idx] = (kk < k && v < nv) ? coef[kk] * PKT[(size_t)kk * vcap + v] : 0.0;
+        double x = (kk < k && v < nv) ? coef[kk] * PKT[(size_t)kk * vcap + v] : 0.0;
+        if (base && kk == k) x = v < nv ? base[v] : -INFINITY;
+        PKTc[idx] = x;
     }
 }
 
@@ -117,6 +121,12 @@ __device__ __forceinline__ void row_update(RowBest &b, double s, int v, double r
         b.M = s;
     }
     // s within the band but not above M: a later (higher) index never wins
+}
+
+// the same update behind its only trigger: every action needs s > M (M = -inf takes any
+// finite s), so the common case is one compare
+__device__ __forceinline__ void row_update_fast(RowBest &b, double s, int v, double rel) {
+    if (__builtin_expect(s > b.M, 0)) row_update(b, s, v, rel);
 }
 
 template <int KB>
@@ -286,6 +296,20 @@ __global__ void __launch_bounds__(256, 2) cut_argmax_kernel(CutParams P) {
 #ifndef TWOSD_CUT_SB
 #define TWOSD_CUT_SB 1                   // scheduling barrier between the groups
 #endif
+#ifndef TWOSD_CUT_FASTRU
+#define TWOSD_CUT_FASTRU 1               // row updates behind the s > M test
+#endif
+#if TWOSD_CUT_FASTRU
+#define RU2 row_update_fast
+#else
+#define RU2 row_update
+#endif
+#ifndef TWOSD_CUT_BASEK
+#define TWOSD_CUT_BASEK 1                // vertex base as an extra k-row of the chunk (no VALU add)
+#endif
+#ifndef TWOSD_CUT_PF
+#define TWOSD_CUT_PF 0                   // read the next group's fragments before this group's MFMAs
+#endif
 constexpr int kVT2 = 32;                 // vertices per LDS chunk (two 16-vertex MFMA tiles)
 constexpr int kCutTile2 = 128;           // scenarios per block tile (4 waves x 2 x 16)
 constexpr int kLdsRow2 = 32;             // doubles per k-row of a chunk
@@ -320,6 +344,7 @@ __global__ void __launch_bounds__(256, 2) cut_argmax2_kernel(CutParams P) {
             const int sa = s0 + j, sb = s0 + 16 + j;
             a0[kb] = (sa < P.N && e < P.k) ? P.dv[(size_t)sa * P.k + e] : 0.0;
             a1[kb] = (sb < P.N && e < P.k) ? P.dv[(size_t)sb * P.k + e] : 0.0;
+            if (TWOSD_CUT_BASEK && e == P.k) a0[kb] = a1[kb] = 1.0;   // x the base row of the chunk
         }
         RowBest rb0, rb1;   // scenario s0 + j / s0 + 16 + j over this lane's vertices v0 + g + 4r (+16)
         rb0.M = -INFINITY; rb0.SV = -INFINITY; rb0.I = -1; rb0.F = 0;
@@ -337,10 +362,10 @@ __global__ void __launch_bounds__(256, 2) cut_argmax2_kernel(CutParams P) {
                 __builtin_amdgcn_global_load_lds((const void *)(P.PKTc + (size_t)kk * P.vcap32 + v0 + vv),
                                                  (__attribute__((address_space(3))) void *)&Bs[buf][i * 4 * kLdsRow2], 16, 0, 0);
             }
-            if (threadIdx.x < kVT2) preb = v0 + (int)threadIdx.x < P.nv ? P.base[v0 + threadIdx.x] : -INFINITY;
+            if (!TWOSD_CUT_BASEK && threadIdx.x < kVT2) preb = v0 + (int)threadIdx.x < P.nv ? P.base[v0 + threadIdx.x] : -INFINITY;
         };
         stage(0, 0);
-        if (threadIdx.x < kVT2) bs[0][threadIdx.x] = preb;
+        if (!TWOSD_CUT_BASEK && threadIdx.x < kVT2) bs[0][threadIdx.x] = preb;
         __syncthreads();            // chunk 0 landed (the barrier drains the DMA)
         for (int ch = 0; ch < nchunks; ++ch) {
             const int buf = ch & 1;
@@ -352,6 +377,42 @@ __global__ void __launch_bounds__(256, 2) cut_argmax2_kernel(CutParams P) {
             // fragments are read in groups of KG k-blocks ahead of their MFMAs; the scheduling
             // barrier keeps the compiler from hoisting every read of the chunk (register spills)
             constexpr int KG = TWOSD_CUT_KG;
+            if constexpr (TWOSD_CUT_PF) {
+                // software-pipelined: group k0 + KG is read while group k0 is multiplied
+                double x0[KG], x1[KG];
+#pragma unroll
+                for (int u = 0; u < KG; ++u) {
+                    x0[u] = Bs[buf][lds2(4 * u + g, j)];
+                    x1[u] = Bs[buf][lds2(4 * u + g, 16 + j)];
+                }
+#pragma unroll
+                for (int k0 = 0; k0 < KB; k0 += KG) {
+                    double y0[KG], y1[KG];
+#pragma unroll
+                    for (int u = 0; u < KG; ++u) {
+                        if (k0 + KG + u < KB) {
+                            y0[u] = Bs[buf][lds2(4 * (k0 + KG + u) + g, j)];
+                            y1[u] = Bs[buf][lds2(4 * (k0 + KG + u) + g, 16 + j)];
+                        }
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int u = 0; u < KG; ++u) {
+                        if (k0 + u < KB) {
+                            c00 = __builtin_amdgcn_mfma_f64_16x16x4f64(x0[u], a0[k0 + u], c00, 0, 0, 0);
+                            c01 = __builtin_amdgcn_mfma_f64_16x16x4f64(x0[u], a1[k0 + u], c01, 0, 0, 0);
+                            c10 = __builtin_amdgcn_mfma_f64_16x16x4f64(x1[u], a0[k0 + u], c10, 0, 0, 0);
+                            c11 = __builtin_amdgcn_mfma_f64_16x16x4f64(x1[u], a1[k0 + u], c11, 0, 0, 0);
+                        }
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int u = 0; u < KG; ++u) {
+                        x0[u] = y0[u];
+                        x1[u] = y1[u];
+                    }
+                }
+            } else {
 #pragma unroll
             for (int k0 = 0; k0 < KB; k0 += KG) {
                 double x0[KG], x1[KG];
@@ -373,23 +434,37 @@ __global__ void __launch_bounds__(256, 2) cut_argmax2_kernel(CutParams P) {
                 }
                 if (TWOSD_CUT_SB) __builtin_amdgcn_sched_barrier(0);
             }
+            }
             // C/D: register r of a tile is vertex row g + 4r, scenario column j; this lane's
             // vertices in increasing order: v0 + g + 4r, then v0 + 16 + g + 4r
+            if constexpr (TWOSD_CUT_BASEK) {   // the scores include the base (-inf past nv)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    RU2(rb0, c00[r], v0 + g + 4 * r, P.tie_rel);
+                    RU2(rb1, c01[r], v0 + g + 4 * r, P.tie_rel);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    RU2(rb0, c10[r], v0 + 16 + g + 4 * r, P.tie_rel);
+                    RU2(rb1, c11[r], v0 + 16 + g + 4 * r, P.tie_rel);
+                }
+            } else {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int va = v0 + g + 4 * r;
                 const double ba = va < P.nv ? bs[buf][g + 4 * r] : -INFINITY;
-                row_update(rb0, ba + c00[r], va, P.tie_rel);
-                row_update(rb1, ba + c01[r], va, P.tie_rel);
+                RU2(rb0, ba + c00[r], va, P.tie_rel);
+                RU2(rb1, ba + c01[r], va, P.tie_rel);
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int vb = v0 + 16 + g + 4 * r;
                 const double bb = vb < P.nv ? bs[buf][16 + g + 4 * r] : -INFINITY;
-                row_update(rb0, bb + c10[r], vb, P.tie_rel);
-                row_update(rb1, bb + c11[r], vb, P.tie_rel);
+                RU2(rb0, bb + c10[r], vb, P.tie_rel);
+                RU2(rb1, bb + c11[r], vb, P.tie_rel);
             }
-            if (ch + 1 < nchunks && threadIdx.x < kVT2) bs[buf ^ 1][threadIdx.x] = preb;
+            }
+            if (!TWOSD_CUT_BASEK && ch + 1 < nchunks && threadIdx.x < kVT2) bs[buf ^ 1][threadIdx.x] = preb;
             __syncthreads();
         }
         // combine the 4 lanes (g) of each scenario column: max M, band threshold, lowest candidate
@@ -754,8 +829,10 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     const EpiDevice &E = c->epis[epi];
     const int N = E.count, k = c->k, m = c->L.m, nv = c->dvs.size, n1 = c->n1;
     const int k4 = (std::max(k, 1) + 3) & ~3;
-    const int KB = kb_for(k4);
-    if (KB < 0) return fail(TWOSD_E_UNSUPPORTED, "k = %d random elements exceeds the cut kernel envelope (128)", k);
+    // v2 with the base row: k + 1 rows of the chunk
+    const bool base_row = cut_version() == 2 && TWOSD_CUT_BASEK;
+    const int KB = kb_for(base_row ? ((k + 1 + 3) & ~3) : k4);
+    if (KB < 0) return fail(TWOSD_E_UNSUPPORTED, "k = %d random elements exceeds the cut kernel envelope (127)", k);
     int rc;
     if ((rc = update_pk(c))) return rc;
     // host: bvec = r - T x, coef
@@ -818,7 +895,7 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
         }
         const size_t tot = (size_t)rows * vcap32;
         hipLaunchKernelGGL(cut_pktc_kernel, dim3((unsigned)std::min<size_t>(4096, (tot + 255) / 256)), dim3(256), 0, c->stream, nv, k,
-                           rows, w->pk_vcap, vcap32, w->PKT, w->coef, w->PKTc);
+                           rows, w->pk_vcap, vcap32, w->PKT, w->coef, base_row ? w->base : nullptr, w->PKTc);
         P.PKTc = w->PKTc;
         P.vcap32 = vcap32;
     }

@@ -6,7 +6,7 @@ set -e
 cd "$(dirname "$0")/../sqlp_amd/csrc"
 make -s
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../../include -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result"
-OTHERS="build/api.hip.o build/lp_hyper.hip.o build/pool_sort.hip.o build/sampler.hip.o build/dvs_kernel.hip.o build/vkey.hip.o build/host_basis.cpp.o"
+OTHERS="build/api.hip.o build/lp_hyper.hip.o build/pool_sort.hip.o build/sampler.hip.o build/dvs_kernel.hip.o build/vkey.hip.o build/pool_gpu.hip.o build/host_basis.cpp.o"
 mkdir -p build_v
 pids=()
 while [ $# -ge 2 ]; do
