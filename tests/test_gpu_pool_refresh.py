@@ -127,3 +127,46 @@ def test_pool_refresh_device_build_equals_host(monkeypatch, chain):
     assert (st_after == 0).all()
     np.testing.assert_allclose(o_after, o_ref, rtol=1e-9, atol=1e-9)
     print(f"chain {chain}: pool {P_d}, pivots {piv_d / len(vals):.2f}, refresh ms {ctx.last_refresh_ms()}")
+
+
+@pytest.mark.parametrize("name,N,train,pool", [("ssn", 4000, 2048, 256), ("lands", 2000, 512, 32),
+                                               ("transship", 2000, 1024, 64)])
+def test_pool_refresh_device_build_other_instances(monkeypatch, name, N, train, pool):
+    """Device vs host pool build on the other instances (different m, k, element rows per
+    column, fixed basics): same pool, same objectives and pivots; objectives equal the
+    primary-basis solve."""
+    from sqlp_amd import smps, twosd
+    inst = I.load(name)
+    x_ev = I.x_ev(name)
+    x2 = x_ev * 1.07 + 0.01
+    vals = I.sample(name, N, seed=31)
+    runs = []
+    for mode in ("host", "device"):
+        if mode == "host":
+            monkeypatch.setenv("TWOSD_REFRESH_HOST", "1")
+        else:
+            monkeypatch.delenv("TWOSD_REFRESH_HOST", raising=False)
+        ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+        ctx.compute_basis(x_ev, smps.mean_values(inst["sto"]))
+        tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+        twosd.add_scenarios(tr, I.sample(name, train, seed=32))
+        ctx.pool_build(tr, x_ev, 0, train, pool)
+        ev = twosd.sdEpigraph(ctx, 1.0, 0.0)
+        twosd.add_scenarios(ev, vals)
+        P = ctx.pool_refresh(tr, x2, 0, train, pool)
+        o, _, _, st = twosd.solve_batch(ev, x2, 0, N, want_pi=False)
+        runs.append((P, [ctx.pool_get(p) for p in range(P)], o, st, ctx.lp_stats()[0]))
+    (P_h, heads_h, o_h, st_h, piv_h), (P_d, heads_d, o_d, st_d, piv_d) = runs
+    assert P_h == P_d and P_d >= 1
+    for a, b in zip(heads_h, heads_d):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(st_h, st_d)
+    np.testing.assert_allclose(o_d, o_h, rtol=1e-12, atol=1e-12)
+    assert piv_d == piv_h
+    ref = twosd.SDContext(inst["sp2"], inst["sto"])
+    ref.compute_basis(x_ev, smps.mean_values(inst["sto"]))
+    o_ref, _, _, st_ref = ref.solve_values(x2, vals, want_pi=False)
+    ok = (st_ref == 0) & (st_d == 0)
+    assert ok.mean() > 0.95
+    np.testing.assert_allclose(o_d[ok], o_ref[ok], rtol=1e-9, atol=1e-7)
+    print(f"{name}: pool {P_d}, pivots {piv_d / N:.2f}")
