@@ -283,7 +283,7 @@ def main():
             if args.no_dedup:
                 twosd.solve_batch(epi_e, xx, 0, n_local, want_pi=False)
             else:
-                twosd.solve_push(epi_e, xx, 0, n_local)
+                twosd.solve_push(epi_e, xx, 0, n_local, want_obj=False)
                 if world > 1:
                     # exchange (2) at the SD volume: two new vertices per epigraph (the candidate
                     # and incumbent duals of sd_iteration!, algorithm.jl:46-54) all-gathered

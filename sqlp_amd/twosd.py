@@ -502,13 +502,16 @@ def _build_cut(epi, x, tie_rel, want_argmax):
     return sdCut(a.value, beta, wm.value), mv, ma
 
 
-def solve_push(epi: sdEpigraph, x, first, count):
-    """Device-side solve_problem! + push! of the duals (no host round trip)."""
+def solve_push(epi: sdEpigraph, x, first, count, want_obj=True):
+    """Device-side solve_problem! + push! of the duals (no host round trip).  want_obj=False
+    skips the copy of the objectives and statuses (sd_iteration! does not read them; a
+    non-optimal scenario still raises); obj and st are then None."""
     ctx = epi.ctx
-    obj = np.zeros(count)
-    st = np.zeros(count, dtype=np.int32)
+    obj = np.zeros(count) if want_obj else None
+    st = np.zeros(count, dtype=np.int32) if want_obj else None
     ns = C.c_int()
-    check(ctx.lib.twosd_solve_push(ctx.h, epi.index, ptr(_f64(x)), first, count, ptr(obj), ptr(st), C.byref(ns)))
+    check(ctx.lib.twosd_solve_push(ctx.h, epi.index, ptr(_f64(x)), first, count, ptr(obj) if want_obj else None,
+                                   ptr(st) if want_obj else None, C.byref(ns)))
     return obj, st, ns.value
 
 
