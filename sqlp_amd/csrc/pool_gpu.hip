@@ -30,8 +30,9 @@ namespace twosd {
 
 namespace {
 
-constexpr int kPgThreads = 256;
-constexpr int kPgWaves = kPgThreads / 64;
+constexpr int kPgThreads = 256;                  // count / fill kernels
+constexpr int kFtThreads = 1024;                 // FTRAN kernels: 16 waves = 16 columns at a time per source
+constexpr int kFtWaves = kFtThreads / 64;
 
 struct Src {
     int pb, K, off;
@@ -58,15 +59,16 @@ __device__ inline bool src_ok(const PgArgs &A, const Src &S) {
     return S.K >= 0 && S.K <= A.kmax && S.pb >= 0 && S.pb < A.npool_old;
 }
 
-// exclusive prefix of in[0, n) into out[0, n], out[n] = total (all threads of the block)
+// exclusive prefix of in[0, n) into out[0, n], out[n] = total (all NT threads of the block)
+template <int NT = kPgThreads>
 __device__ void block_scan(const int *in, int *out, int n, int *tmp) {
-    const int tid = threadIdx.x, per = (n + kPgThreads - 1) / kPgThreads;
+    const int tid = threadIdx.x, per = (n + NT - 1) / NT;
     const int b = min(n, tid * per), e = min(n, b + per);
     int s = 0;
     for (int i = b; i < e; ++i) s += in[i];
     tmp[tid] = s;
     __syncthreads();
-    for (int o = 1; o < kPgThreads; o <<= 1) {
+    for (int o = 1; o < NT; o <<= 1) {
         const int v = tid >= o ? tmp[tid - o] : 0;
         __syncthreads();
         tmp[tid] += v;
@@ -77,18 +79,19 @@ __device__ void block_scan(const int *in, int *out, int n, int *tmp) {
         out[i] = run;
         run += in[i];
     }
-    if (tid == kPgThreads - 1) out[n] = tmp[kPgThreads - 1];
+    if (tid == NT - 1) out[n] = tmp[NT - 1];
     __syncthreads();
 }
 
 __device__ inline unsigned long long lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
 
 // rows any eta of the source touches (compose_binv re-filters exactly these rows)
+template <int NT>
 __device__ void mark_touched(const PgArgs &A, const Src &S, unsigned char *touched) {
-    for (int i = threadIdx.x; i < A.m; i += kPgThreads) touched[i] = 0;
+    for (int i = threadIdx.x; i < A.m; i += NT) touched[i] = 0;
     __syncthreads();
     const int ne = S.K > 0 ? S.etaoff[S.K] : 0;
-    for (int e = threadIdx.x; e < ne; e += kPgThreads) touched[A.eo_eidx[S.off + e]] = 1;
+    for (int e = threadIdx.x; e < ne; e += NT) touched[A.eo_eidx[S.off + e]] = 1;
     __syncthreads();
 }
 
@@ -96,10 +99,10 @@ __device__ void mark_touched(const PgArgs &A, const Src &S, unsigned char *touch
 
 // ---- 1. FTRAN of every column of B_pb^{-1} through the eta file ----------------------------
 template <int PASS>
-__global__ __launch_bounds__(kPgThreads) void pg_ftran_kernel(PgArgs A) {
+__global__ __launch_bounds__(kFtThreads) void pg_ftran_kernel(PgArgs A) {
     extern __shared__ double smem[];
-    __shared__ int tmp[kPgThreads];
-    __shared__ double red[kPgWaves];
+    __shared__ int tmp[kFtThreads];
+    __shared__ double red[kFtWaves];
     const int a = A.a0 + blockIdx.x, m = A.m, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const Src S = src_of(A, a);
     if (!src_ok(A, S) || (PASS == 1 && !(A.amax[a] >= 0.0))) {   // eta file did not fit: unusable
@@ -107,17 +110,17 @@ __global__ __launch_bounds__(kPgThreads) void pg_ftran_kernel(PgArgs A) {
         return;
     }
     double *x = smem + (size_t)wv * m;                    // this wave's column, dense
-    int *etap = reinterpret_cast<int *>(smem + (size_t)kPgWaves * m);
+    int *etap = reinterpret_cast<int *>(smem + (size_t)kFtWaves * m);
     int *etaoff = etap + A.kmax;
     int *cstart = etaoff + A.kmax + 1;                    // PASS 1: column offsets (m + 1)
     unsigned char *touched = reinterpret_cast<unsigned char *>(cstart + m + 1);
-    for (int t = tid; t < S.K; t += kPgThreads) etap[t] = S.etap[t];
-    for (int t = tid; t <= S.K; t += kPgThreads) etaoff[t] = S.K > 0 ? S.etaoff[t] : 0;
-    mark_touched(A, S, touched);
+    for (int t = tid; t < S.K; t += kFtThreads) etap[t] = S.etap[t];
+    for (int t = tid; t <= S.K; t += kFtThreads) etaoff[t] = S.K > 0 ? S.etaoff[t] : 0;
+    mark_touched<kFtThreads>(A, S, touched);
     double drop = 0.0;
     int *nzc = A.nzc + (size_t)a * m;
     if (PASS == 1) {
-        block_scan(nzc, cstart, m, tmp);
+        block_scan<kFtThreads>(nzc, cstart, m, tmp);
         drop = 1e-14 * A.amax[a];
     }
     const int *cp = A.bcp0 + (size_t)S.pb * (A.MP + 1);
@@ -125,7 +128,7 @@ __global__ __launch_bounds__(kPgThreads) void pg_ftran_kernel(PgArgs A) {
     const double *evals = A.eo_evals + S.off;
     double amax = 0.0;
     int nzsum = 0;   // PASS 0, lane 0: nonzeros of this wave's columns
-    for (int c = wv; c < m; c += kPgWaves) {
+    for (int c = wv; c < m; c += kFtWaves) {
         for (int i = lane; i < m; i += 64) x[i] = 0.0;
         __builtin_amdgcn_wave_barrier();
         for (int q = cp[c] + lane; q < cp[c + 1]; q += 64) {
@@ -186,7 +189,7 @@ __global__ __launch_bounds__(kPgThreads) void pg_ftran_kernel(PgArgs A) {
         if (tid == 0) {   // nztot: read back by the host for the intermediate offsets
             double v = red[0];
             int t = tmp[0];
-            for (int w = 1; w < kPgWaves; ++w) {
+            for (int w = 1; w < kFtWaves; ++w) {
                 v = fmax(v, red[w]);
                 t += tmp[w];
             }
@@ -416,7 +419,7 @@ __global__ __launch_bounds__(kPgThreads) void pg_fill_kernel(PgArgs A, PgFill F)
 }
 
 static size_t ftran_lds(const PgArgs &A) {
-    return sizeof(double) * kPgWaves * A.m + sizeof(int) * (2 * A.kmax + 1 + A.m + 1) + A.m + 16;
+    return sizeof(double) * kFtWaves * A.m + sizeof(int) * (2 * A.kmax + 1 + A.m + 1) + A.m + 16;
 }
 static size_t count_lds(const PgArgs &A) {
     return sizeof(double) * 3 * A.m + sizeof(int) * (3 * A.m + 1) + (A.n + A.m) + 16;
@@ -428,12 +431,15 @@ static size_t fill_lds(const PgArgs &A) {
 int pg_supported(int m, int n, int kmax) {
     PgArgs A{};
     A.m = m; A.n = n; A.kmax = kmax;
-    return ftran_lds(A) <= 64 * 1024 && count_lds(A) <= 64 * 1024 && fill_lds(A) <= 64 * 1024 && (m + 63) / 64 <= 64;
+    return ftran_lds(A) <= 96 * 1024 && count_lds(A) <= 64 * 1024 && fill_lds(A) <= 64 * 1024 && (m + 63) / 64 <= 64;
 }
 
 template <int PASS>
 static hipError_t launch_ftran(const PgArgs &A, int nb, hipStream_t s) {
-    hipLaunchKernelGGL(pg_ftran_kernel<PASS>, dim3(nb), dim3(kPgThreads), ftran_lds(A), s, A);
+    hipError_t e = hipFuncSetAttribute((const void *)pg_ftran_kernel<PASS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)ftran_lds(A));
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(pg_ftran_kernel<PASS>, dim3(nb), dim3(kFtThreads), ftran_lds(A), s, A);
     return hipGetLastError();
 }
 hipError_t pg_launch_ftran(const PgArgs &A, int pass, int nb, hipStream_t s) {
