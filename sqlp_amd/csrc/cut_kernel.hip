@@ -725,7 +725,7 @@ static int realloc_dev(T **p, size_t n) {
 }
 
 static int kb_for(int k4) {
-    static const int KBs[] = {1, 2, 4, 6, 8, 12, 16, 24, 30, 32};
+    static const int KBs[] = {1, 2, 4, 6, 8, 12, 16, 22, 24, 30, 32};   // 22: ssn (k = 86, + base row)
     for (int kb : KBs)
         if (4 * kb >= k4) return kb;
     return -1;
@@ -770,6 +770,7 @@ static int argmax_occupancy(int KB, size_t dyn_lds) {
         case 8: return argmax_occupancy_t<8>(dyn_lds);
         case 12: return argmax_occupancy_t<12>(dyn_lds);
         case 16: return argmax_occupancy_t<16>(dyn_lds);
+        case 22: return argmax_occupancy_t<22>(dyn_lds);
         case 24: return argmax_occupancy_t<24>(dyn_lds);
         case 30: return argmax_occupancy_t<30>(dyn_lds);
         case 32: return argmax_occupancy_t<32>(dyn_lds);
@@ -786,6 +787,7 @@ static void launch_argmax(int KB, const CutParams &P, int nblocks, hipStream_t s
         case 8: launch_argmax_t<8>(P, nblocks, s); break;
         case 12: launch_argmax_t<12>(P, nblocks, s); break;
         case 16: launch_argmax_t<16>(P, nblocks, s); break;
+        case 22: launch_argmax_t<22>(P, nblocks, s); break;
         case 24: launch_argmax_t<24>(P, nblocks, s); break;
         case 30: launch_argmax_t<30>(P, nblocks, s); break;
         case 32: launch_argmax_t<32>(P, nblocks, s); break;
