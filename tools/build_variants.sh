@@ -4,9 +4,9 @@
 # into sqlp_amd/libtwosd_hip_<name>.so (select with TWOSD_LIB=<name>).
 set -e
 cd "$(dirname "$0")/../sqlp_amd/csrc"
-make -s build/api.hip.o build/pool_sort.hip.o build/sampler.hip.o build/dvs_kernel.hip.o build/cut_kernel.hip.o build/host_basis.cpp.o
+make -s build/api.hip.o build/pool_sort.hip.o build/sampler.hip.o build/dvs_kernel.hip.o build/cut_kernel.hip.o build/vkey.hip.o build/pool_gpu.hip.o build/host_basis.cpp.o
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../../include -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result"
-OTHERS="build/api.hip.o build/pool_sort.hip.o build/sampler.hip.o build/dvs_kernel.hip.o build/cut_kernel.hip.o build/host_basis.cpp.o"
+OTHERS="build/api.hip.o build/pool_sort.hip.o build/sampler.hip.o build/dvs_kernel.hip.o build/cut_kernel.hip.o build/vkey.hip.o build/pool_gpu.hip.o build/host_basis.cpp.o"
 mkdir -p build_v
 pids=()
 while [ $# -ge 2 ]; do

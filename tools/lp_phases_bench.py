@@ -3,7 +3,9 @@ scenarios, two-level basis pool).  Run with TWOSD_LIB=stamps (libtwosd_hip_stamp
 by `make -C sqlp_amd/csrc stamps`); the stamps perturb the schedule, so only the shares and
 the cycles per pivot are meaningful, never the absolute kernel time.
 
-usage: TWOSD_LIB=stamps python tools/lp_phases_bench.py [N] [pool]
+usage: TWOSD_LIB=stamps python tools/lp_phases_bench.py [N] [pool] [batch|push]
+(push: the keyed solve_push of the bench -- dual keys instead of pi, recovery for the
+representatives only; the stamps then cover the main launch and the re-solves)
 """
 import ctypes as C
 import json
@@ -42,7 +44,13 @@ def main():
     twosd.solve_batch(epi, x, 0, min(N, 4096), want_pi=False)
     st = np.zeros(10, dtype=np.uint64)
     ctx.lib.twosd_debug_stamps(ctx.h, st.ctypes.data_as(C.c_void_p), 1)
-    twosd.solve_batch(epi, x, 0, N, want_pi=True)
+    mode = sys.argv[3] if len(sys.argv) > 3 else "batch"
+    if mode == "push":
+        V = twosd.sdDualVertexSet(ctx)
+        twosd.solve_push(epi, x, 0, N, want_obj=False)
+        print(f"representatives re-solved: {ctx.last_push_reps()}, |V| = {len(V)}")
+    else:
+        twosd.solve_batch(epi, x, 0, N, want_pi=True)
     ctx.lib.twosd_debug_stamps(ctx.h, st.ctypes.data_as(C.c_void_p), 1)
     tot = float(st.sum())
     t = ctx.timings_us()
