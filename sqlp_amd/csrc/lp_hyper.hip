@@ -121,9 +121,9 @@ constexpr int EG = TWOSD_ETA_G;
 #ifndef TWOSD_HARRIS_B
 #define TWOSD_HARRIS_B 1
 #endif
-// HB = 1: the next slot's alpha~ read one slot ahead (software pipelined)
+// HB = 1: alpha~ read TWOSD_HARRIS_PF slots ahead (software pipelined; 0 = off)
 #ifndef TWOSD_HARRIS_PF
-#define TWOSD_HARRIS_PF 0
+#define TWOSD_HARRIS_PF 1
 #endif
 // unroll of the per-scenario gathers (x_B warm start, vertex recovery): loads in flight
 #ifndef TWOSD_XB_UNROLL
@@ -388,13 +388,19 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             const double sg = delta > 0 ? 1.0 : -1.0;
             double thmax = INFINITY;
             uint64_t nzm = 0, elm = 0;
-            double apf = TWOSD_HARRIS_PF ? alpha[lane] : 0.0;   // slot c + 1 read while slot c is tested
+            double apf = TWOSD_HARRIS_PF ? alpha[lane] : 0.0;   // slot c + 1 (+ 2) read while slot c is tested
+            double apf2 = (TWOSD_HARRIS_PF > 1 && C > 1) ? alpha[64 + lane] : 0.0;
 #pragma unroll
             for (int c0 = 0; c0 < C; c0 += HB) {
                 double av[HB];
                 if constexpr (TWOSD_HARRIS_PF && HB == 1) {
                     av[0] = apf;
-                    if (c0 + 1 < C) apf = alpha[64 * (c0 + 1) + lane];
+                    if (TWOSD_HARRIS_PF > 1) {
+                        apf = apf2;
+                        if (c0 + 2 < C) apf2 = alpha[64 * (c0 + 2) + lane];
+                    } else if (c0 + 1 < C) {
+                        apf = alpha[64 * (c0 + 1) + lane];
+                    }
                 } else {
 #pragma unroll
                 for (int u = 0; u < HB; ++u) av[u] = (HB == 1 || c0 + u < C) ? alpha[64 * (c0 + u) + lane] : 0.0;
@@ -425,13 +431,19 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             double bA = 0.0, bD = 0.0, bAs = 0.0;
             int bq = 0x7fffffff;
             apf = TWOSD_HARRIS_PF ? alpha[lane] : 0.0;
+            apf2 = (TWOSD_HARRIS_PF > 1 && C > 1) ? alpha[64 + lane] : 0.0;
 #pragma unroll
             for (int c0 = 0; c0 < C; c0 += HB) {
                 if (HB > 1 && !((elm >> c0) & ((1ull << HB) - 1))) continue;
                 double av[HB];
                 if constexpr (TWOSD_HARRIS_PF && HB == 1) {
                     av[0] = apf;
-                    if (c0 + 1 < C) apf = alpha[64 * (c0 + 1) + lane];
+                    if (TWOSD_HARRIS_PF > 1) {
+                        apf = apf2;
+                        if (c0 + 2 < C) apf2 = alpha[64 * (c0 + 2) + lane];
+                    } else if (c0 + 1 < C) {
+                        apf = alpha[64 * (c0 + 1) + lane];
+                    }
                 } else {
 #pragma unroll
                 for (int u = 0; u < HB; ++u) av[u] = (HB == 1 || c0 + u < C) ? alpha[64 * (c0 + u) + lane] : 0.0;
@@ -457,13 +469,19 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             const double thetaD = eq.p0 / eq.p1;
             // d_j -= thetaD * alpha~_j for every nonbasic column with alpha_j != 0
             apf = TWOSD_HARRIS_PF ? alpha[lane] : 0.0;
+            apf2 = (TWOSD_HARRIS_PF > 1 && C > 1) ? alpha[64 + lane] : 0.0;
 #pragma unroll
             for (int c0 = 0; c0 < C; c0 += HB) {
                 if (HB > 1 && !((nzm >> c0) & ((1ull << HB) - 1))) continue;
                 double av[HB];
                 if constexpr (TWOSD_HARRIS_PF && HB == 1) {
                     av[0] = apf;
-                    if (c0 + 1 < C) apf = alpha[64 * (c0 + 1) + lane];
+                    if (TWOSD_HARRIS_PF > 1) {
+                        apf = apf2;
+                        if (c0 + 2 < C) apf2 = alpha[64 * (c0 + 2) + lane];
+                    } else if (c0 + 1 < C) {
+                        apf = alpha[64 * (c0 + 1) + lane];
+                    }
                 } else {
 #pragma unroll
                 for (int u = 0; u < HB; ++u) av[u] = (HB == 1 || c0 + u < C) ? alpha[64 * (c0 + u) + lane] : 0.0;
