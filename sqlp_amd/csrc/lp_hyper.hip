@@ -129,6 +129,10 @@ constexpr int EG = TWOSD_ETA_G;
 #ifndef TWOSD_XB_UNROLL
 #define TWOSD_XB_UNROLL 2
 #endif
+// FTRAN: B0^{-1} columns of this many nonzeros of a_q loaded per round trip (1: one at a time)
+#ifndef TWOSD_FTRAN_G
+#define TWOSD_FTRAN_G 2
+#endif
 #ifndef TWOSD_REC_UNROLL
 #define TWOSD_REC_UNROLL 1
 #endif
@@ -502,6 +506,38 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             // B0^{-1} under the nonzeros of a_q, lanes over a column's entries (distinct rows)
             {
                 const int np0 = q >= n ? 0 : P.colptr[q], np1 = q >= n ? 1 : P.colptr[q + 1];
+#if TWOSD_FTRAN_G > 1
+                // the B0^{-1} columns of FG nonzeros of a_q per memory round trip (pointers and
+                // first 64 entries loaded together), applied in pw order as below
+                constexpr int FG = TWOSD_FTRAN_G;
+                for (int pw0 = np0; pw0 < np1; pw0 += FG) {
+                    int fo[FG], fn[FG], fi[FG];
+                    double fa[FG], fv[FG];
+#pragma unroll
+                    for (int g = 0; g < FG; ++g) {
+                        const int pw = pw0 + g;
+                        fo[g] = 0; fn[g] = 0; fi[g] = 0; fa[g] = 0.0; fv[g] = 0.0;
+                        if (pw < np1) {
+                            const int cc = q >= n ? q - n : P.rowidx[pw];
+                            fa[g] = q >= n ? 1.0 : P.val[pw];
+                            fo[g] = bcp[cc];
+                            fn[g] = bcp[cc + 1] - fo[g];
+                            if (lane < fn[g]) { fi[g] = P.bci[fo[g] + lane]; fv[g] = P.bcv[fo[g] + lane]; }
+                        }
+                    }
+#pragma unroll
+                    for (int g = 0; g < FG; ++g) {
+                        if (pw0 + g >= np1) break;
+                        if (lane < fn[g]) ut[fi[g]] = fma(fa[g], fv[g], ut[fi[g]]);
+                        for (int e = 64 + lane; e < fn[g]; e += 64) {
+                            const int i = P.bci[fo[g] + e];
+                            ut[i] = fma(fa[g], P.bcv[fo[g] + e], ut[i]);
+                        }
+                        nops += fn[g];
+                        h_wave_sync();
+                    }
+                }
+#else
                 for (int pw = np0; pw < np1; ++pw) {
                     const int cc = q >= n ? q - n : P.rowidx[pw];
                     const double aw = q >= n ? 1.0 : P.val[pw];
@@ -513,6 +549,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                     nops += e1 - e0;
                     h_wave_sync();
                 }
+#endif
             }
             for (int tg = 0; tg < K; tg += EG) {
                 int gi[EG], gn[EG], go[EG];

@@ -1,0 +1,8 @@
+#!/bin/bash
+# round-end session: GPU tests + smoke, then the profile session (bench, kernel trace, PMC passes)
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gputests.log 2>&1 || { tail -30 gpurun_out/gputests.log; exit 1; }
+tail -2 gpurun_out/gputests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { cat gpurun_out/smoke.log; exit 1; }
+cat gpurun_out/smoke.log
+bash tools/profile_round.sh r02
