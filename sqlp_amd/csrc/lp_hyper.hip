@@ -111,10 +111,10 @@ size_t hyper_lds_bytes(int R, int ncol, int kmax, int k) { return (size_t)kWaves
 // loads in flight per memory round trip: etas per group (BTRAN / rho / FTRAN), W rows per
 // pricing group (A/B knobs of the development builds)
 #ifndef TWOSD_ETA_G
-#define TWOSD_ETA_G 4
+#define TWOSD_ETA_G 2
 #endif
 #ifndef TWOSD_PRICE_G
-#define TWOSD_PRICE_G 8
+#define TWOSD_PRICE_G 4
 #endif
 constexpr int EG = TWOSD_ETA_G;
 // alpha~ slots read together in the Harris passes
