@@ -12,6 +12,8 @@ Pure-numpy restatement of the reference's Julia, in the reference's loop order:
   * ``argmax_procedure``    <- subprob.jl:141-169
   * ``build_sasa_cut``      <- epigraph.jl:125-146
   * ``add_cut_discount`` / ``evaluate_epigraph`` <- epigraph.jl:101-117, 177-203
+  * ``remove_cuts_by_multiplier`` <- algorithm.jl:57-72 (CUT_REMOVE_TOLERANCE algorithm.jl:23)
+  * ``sync_cuts``           <- cell.jl:139-201 (remove_cuts! + add_cut_to_master! per epigraph)
   * ``evaluate_multi_epigraph`` / ``check_improvement`` <- epigraph.jl:221-228, improvement.jl:19-49
 """
 from __future__ import annotations
@@ -179,6 +181,36 @@ def build_sasa_cut(coef: Coefficients, deltas, weights, x, V, tie_rel: float = 0
 def add_cut_discount(alpha, beta, discount, lower_bound):
     """epigraph.jl:105-106 (the rhs/coefficients add_cut_to_master! writes)."""
     return discount * alpha + (1 - discount) * lower_bound, discount * np.asarray(beta)
+
+
+CUT_REMOVE_TOLERANCE = 0.001      # algorithm.jl:23
+
+
+def remove_cuts_by_multiplier(cuts, duals, tol=CUT_REMOVE_TOLERANCE):
+    """algorithm.jl:57-72 for one epigraph: duals[j] is dual(cell.epicon_ref[i][j]); every j
+    with |dual| < tol is collected into delete_index, then deleteat!(epi.cuts, delete_index)."""
+    delete_index = []
+    for j in range(len(duals)):
+        if abs(duals[j]) < tol:
+            delete_index.append(j)
+    return [c for j, c in enumerate(cuts) if j not in delete_index]
+
+
+def sync_cuts(epis):
+    """cell.jl:198-201 -> :167-192 for every epigraph in order: its rows are removed, then each
+    cut is added with discount = weight_mark / total_scenario_weight (add_cut_to_master!,
+    epigraph.jl:101-117), then the incumbent cut with discount 1.  epis = [(cuts,
+    incumbent_cut, total_scenario_weight, lower_bound)], cuts = [(alpha, beta, weight_mark)].
+    Returns the master's epigraph rows in insertion order: (epi, alpha', beta', incumbent)."""
+    rows = []
+    for e, (cuts, inc, tw, lb) in enumerate(epis):
+        for a, b, wm in cuts:
+            na, nb = add_cut_discount(a, b, wm / tw, lb)
+            rows.append((e, na, nb, False))
+        if inc is not None:
+            na, nb = add_cut_discount(inc[0], inc[1], 1.0, lb)
+            rows.append((e, na, nb, True))
+    return rows
 
 
 def evaluate_epigraph(cuts, incumbent_cut, x, total_scenario_weight, lower_bound):

@@ -8,7 +8,9 @@
 //
 // setup_solve: revised dual simplex with an explicit dense inverse updated by rank-1
 // pivots and re-inverted every kRefactor pivots (O(m^2) per pivot).  Dantzig leaving
-// row, Harris two-pass ratio test.  Requires q >= 0 so the slack basis is dual feasible.
+// row, Harris two-pass ratio test, from the slack basis (dual feasible when q >= 0).  With
+// negative costs (baa99-20) the slack basis is not dual feasible: a dual-simplex phase on
+// max(q, 0) finds a primal-feasible basis, then a primal simplex phase on q ends optimal.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -102,15 +104,13 @@ double basis_dual_infeasibility(const HostLP &L, const std::vector<int> &head,
     return worst;
 }
 
-int setup_solve(const HostLP &L, const std::vector<double> &b, std::vector<int> &head, double &obj,
-                int &iters, std::string &err) {
+// dual simplex from the dual-feasible basis `head` (the slack basis when every q_j >= 0) to an
+// optimal basis of L at rhs b
+static int dual_simplex(const HostLP &L, const std::vector<double> &b, std::vector<int> &head, int &iters,
+                        std::string &err) {
     const int m = L.m, n = L.n;
-    for (int j = 0; j < n; ++j)
-        if (L.q[j] < 0) { err = "setup_solve: negative stage-2 cost; install a dual-feasible basis with twosd_set_basis"; return TWOSD_LP_NUMERIC; }
-    head.resize(m);
-    for (int i = 0; i < m; ++i) head[i] = n + i;
     std::vector<char> isb(n + m, 0);
-    for (int i = 0; i < m; ++i) isb[n + i] = 1;
+    for (int i = 0; i < m; ++i) isb[head[i]] = 1;
     std::vector<double> Binv, B, xB(m), pi(m), rho(m), col(m);
     auto reinvert = [&]() -> bool {
         basis_matrix(L, head, B);
@@ -131,8 +131,7 @@ int setup_solve(const HostLP &L, const std::vector<double> &b, std::vector<int> 
         }
         return true;
     };
-    if (!reinvert()) { err = "setup_solve: singular slack basis"; return TWOSD_LP_NUMERIC; }
-    iters = 0;
+    if (!reinvert()) { err = "setup_solve: singular start basis"; return TWOSD_LP_NUMERIC; }
     const int max_iter = 50 * (m + n) + 1000;
     for (;;) {
         // leaving row: largest primal infeasibility (lowest index on ties)
@@ -214,10 +213,150 @@ int setup_solve(const HostLP &L, const std::vector<double> &b, std::vector<int> 
         ++iters;
         if (iters % kRefactor == 0 && !reinvert()) { err = "setup_solve: singular basis"; return TWOSD_LP_NUMERIC; }
     }
-    if (!reinvert()) { err = "setup_solve: singular final basis"; return TWOSD_LP_NUMERIC; }
+    return TWOSD_LP_OPTIMAL;
+}
+
+// primal simplex from the primal-feasible basis `head` to an optimal basis of L at rhs b.
+// Nonbasic variables sit at 0: y_j and L slacks may increase, G slacks (upper bound 0) may
+// decrease, E slacks are fixed.  Dantzig pricing (lowest index on ties), Harris two-pass ratio
+// test; after 50 consecutive degenerate pivots the entering variable is the lowest-index
+// candidate (Bland) until a pivot makes progress.
+static int primal_simplex(const HostLP &L, const std::vector<double> &b, std::vector<int> &head, int &iters,
+                          std::string &err) {
+    const int m = L.m, n = L.n;
+    std::vector<char> isb(n + m, 0);
+    for (int i = 0; i < m; ++i) isb[head[i]] = 1;
+    std::vector<double> Binv, B, xB(m), pi(m), col(m);
+    auto reinvert = [&]() -> bool {
+        basis_matrix(L, head, B);
+        if (!dense_inverse(m, B, Binv)) return false;
+        for (int i = 0; i < m; ++i) {
+            const double *row = &Binv[(size_t)i * m];
+            double s = 0.0;
+            for (int t = 0; t < m; ++t) s += row[t] * b[t];
+            xB[i] = s;
+        }
+        return true;
+    };
+    auto duals = [&]() {
+        std::fill(pi.begin(), pi.end(), 0.0);
+        for (int i = 0; i < m; ++i) {
+            const int j = head[i];
+            const double c = j < n ? L.q[j] : 0.0;
+            if (c == 0.0) continue;
+            const double *row = &Binv[(size_t)i * m];
+            for (int t = 0; t < m; ++t) pi[t] += c * row[t];
+        }
+    };
+    if (!reinvert()) { err = "setup_solve: singular phase-1 basis"; return TWOSD_LP_NUMERIC; }
+    const int max_iter = 50 * (m + n) + 1000;
+    int degenerate = 0;
+    for (;;) {
+        duals();
+        const bool bland = degenerate >= 50;
+        int q = -1;
+        double best = 0.0, sigma = 0.0;
+        for (int j = 0; j < n + m; ++j) {
+            if (isb[j]) continue;
+            const int bt = btype_of(L, j);
+            if (bt == BT_E) continue;
+            const double d = (j < n ? L.q[j] : 0.0) - col_dot(L, j, pi.data());
+            const double gain = bt == BT_G ? d : -d;        // objective decrease per unit move
+            if (gain > kTolD && (q < 0 || (!bland && gain > best))) {
+                q = j; best = gain; sigma = bt == BT_G ? -1.0 : 1.0;
+                if (bland) break;
+            }
+        }
+        if (q < 0) break;                                   // optimal
+        if (iters >= max_iter) { err = "setup_solve: iteration limit (primal)"; return TWOSD_LP_ITER_LIMIT; }
+        std::fill(col.begin(), col.end(), 0.0);
+        if (q >= n) {
+            for (int i = 0; i < m; ++i) col[i] = Binv[(size_t)i * m + (q - n)];
+        } else {
+            for (int p = L.colptr[q]; p < L.colptr[q + 1]; ++p) {
+                const int rr = L.rowidx[p];
+                const double a = L.val[p];
+                for (int i = 0; i < m; ++i) col[i] += a * Binv[(size_t)i * m + rr];
+            }
+        }
+        // x_B(t) = x_B - t * sigma * col, t >= 0: basic y / L slacks stay >= 0, G slacks <= 0,
+        // E slacks at 0
+        auto blocks = [&](int i, double a, bool relaxed, double &ratio) -> bool {
+            const int bt = btype_of(L, head[i]);
+            const double tol = relaxed ? kTolP : 0.0;
+            if ((bt == BT_Y || bt == BT_L || bt == BT_E) && a > kTolPiv) { ratio = (xB[i] + tol) / a; return true; }
+            if ((bt == BT_G || bt == BT_E) && a < -kTolPiv) { ratio = (xB[i] - tol) / a; return true; }
+            return false;
+        };
+        double thmax = std::numeric_limits<double>::infinity();
+        for (int i = 0; i < m; ++i) {
+            double ratio;
+            if (blocks(i, sigma * col[i], true, ratio) && ratio < thmax) thmax = ratio;
+        }
+        if (thmax == std::numeric_limits<double>::infinity()) { err = "setup_solve: stage-2 LP unbounded"; return TWOSD_LP_NUMERIC; }
+        int r = -1;
+        double amax = 0.0, theta = 0.0;
+        for (int i = 0; i < m; ++i) {
+            double ratio;
+            const double a = sigma * col[i];
+            if (blocks(i, a, false, ratio) && ratio <= thmax && std::fabs(a) > amax) {
+                amax = std::fabs(a); r = i; theta = std::max(ratio, 0.0);
+            }
+        }
+        if (r < 0) { err = "setup_solve: primal ratio test failed"; return TWOSD_LP_NUMERIC; }
+        const double arq = col[r];
+        for (int i = 0; i < m; ++i) xB[i] -= theta * sigma * col[i];
+        xB[r] = theta * sigma;
+        double *rr = &Binv[(size_t)r * m];
+        for (int t = 0; t < m; ++t) rr[t] /= arq;
+        for (int i = 0; i < m; ++i) {
+            if (i == r || col[i] == 0.0) continue;
+            const double f = col[i];
+            double *ri = &Binv[(size_t)i * m];
+            for (int t = 0; t < m; ++t) ri[t] -= f * rr[t];
+        }
+        isb[head[r]] = 0;
+        isb[q] = 1;
+        head[r] = q;
+        ++iters;
+        degenerate = theta > 1e-12 ? 0 : degenerate + 1;
+        if (iters % kRefactor == 0 && !reinvert()) { err = "setup_solve: singular basis (primal)"; return TWOSD_LP_NUMERIC; }
+    }
+    return TWOSD_LP_OPTIMAL;
+}
+
+int setup_solve(const HostLP &L, const std::vector<double> &b, std::vector<int> &head, double &obj,
+                int &iters, std::string &err) {
+    const int m = L.m, n = L.n;
+    head.resize(m);
+    for (int i = 0; i < m; ++i) head[i] = n + i;
+    iters = 0;
+    bool negative = false;
+    for (int j = 0; j < n; ++j) negative |= L.q[j] < 0;
+    int st;
+    if (!negative) {
+        // q >= 0: the slack basis is dual feasible
+        st = dual_simplex(L, b, head, iters, err);
+    } else {
+        // phase 1: the dual simplex on costs max(q, 0) (slack basis dual feasible) ends at a
+        // primal-feasible basis of the same rows; phase 2: primal simplex on q from there
+        HostLP L1 = L;
+        for (double &c : L1.q) c = std::max(c, 0.0);
+        st = dual_simplex(L1, b, head, iters, err);
+        if (st == TWOSD_LP_OPTIMAL) st = primal_simplex(L, b, head, iters, err);
+    }
+    if (st != TWOSD_LP_OPTIMAL) return st;
+    std::vector<double> B, Binv;
+    basis_matrix(L, head, B);
+    if (!dense_inverse(m, B, Binv)) { err = "setup_solve: singular final basis"; return TWOSD_LP_NUMERIC; }
     obj = 0.0;
-    for (int i = 0; i < m; ++i)
-        if (head[i] < n) obj += L.q[head[i]] * xB[i];
+    for (int i = 0; i < m; ++i) {
+        if (head[i] >= n) continue;
+        double xb = 0.0;
+        const double *row = &Binv[(size_t)i * m];
+        for (int t = 0; t < m; ++t) xb += row[t] * b[t];
+        obj += L.q[head[i]] * xb;
+    }
     return TWOSD_LP_OPTIMAL;
 }
 

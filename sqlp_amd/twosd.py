@@ -23,7 +23,11 @@ from ._lib import check, ptr
 from .smps import spStageProblem, spSmpsPosition, scenario_positions
 
 MIN_SENSE = "MIN_SENSE"
-DEFAULT_TIE_REL = 1e-12
+# argmax tie rule: 0 = the reference's strict '>' (subprob.jl:156, first maximum in insertion
+# order).  tie_rel > 0 is the build's near-tie rule (lowest vertex index within
+# tie_rel * (1 + |max|) of the maximum), which makes the pick independent of summation order
+# for scores that tie in exact arithmetic; the bench passes 1e-12 explicitly.
+DEFAULT_TIE_REL = 0.0
 
 
 def _f64(a):

@@ -25,7 +25,7 @@ def _setup(name, nv_src=512, seed=3):
 
 
 @pytest.mark.parametrize("name,N", [("lands", 300), ("newsvendor", 200), ("transship", 700), ("ssn", 1500),
-                                    ("storm", 1000)])
+                                    ("storm", 1000), ("baa99-20", 800)])
 @pytest.mark.parametrize("tie_rel", [0.0, 1e-12])
 def test_cut_matches_oracle(name, N, tie_rel):
     from oracle import cpu
@@ -63,7 +63,7 @@ def test_cut_matches_oracle(name, N, tie_rel):
     np.testing.assert_allclose(cut.beta, b_ref, rtol=1e-9, atol=1e-9 * (1 + np.abs(b_ref).max()))
 
 
-@pytest.mark.parametrize("name", ["lands", "transship", "ssn", "storm"])
+@pytest.mark.parametrize("name", ["lands", "newsvendor", "transship", "ssn", "storm", "baa99-20"])
 def test_cut_golden_fixture(name):
     from sqlp_amd import twosd
     z = np.load(os.path.join(G, f"cut_{name}.npz"))

@@ -7,7 +7,9 @@ from tests import instances as I
 
 pytestmark = pytest.mark.gpu
 
-CASES = [("lands", 512), ("newsvendor", 256), ("transship", 512), ("ssn", 512), ("storm", 512)]
+# baa99-20 (the instance of the reference driver, sd_single_cut_test.jl:10) has 210 negative stage-2
+# costs: its start basis comes from the host phase-1 + primal simplex of twosd_compute_basis
+CASES = [("lands", 512), ("newsvendor", 256), ("transship", 512), ("ssn", 512), ("storm", 512), ("baa99-20", 512)]
 
 
 def _ctx(name):
@@ -18,6 +20,24 @@ def _ctx(name):
     from sqlp_amd import smps
     ctx.compute_basis(x, smps.mean_values(inst["sto"]))
     return ctx, x
+
+
+def test_lp_golden_fixture_baa99():
+    """The committed HiGHS golden vectors of baa99-20 (tests/golden/make_golden.py): objectives
+    to 1e-9 rel and strong duality of the GPU duals at the golden x and scenarios."""
+    import os
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "lp_baa99-20.npz"))
+    from sqlp_amd import smps, twosd
+    inst = I.load("baa99-20")
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    ctx.compute_basis(z["x"], smps.mean_values(inst["sto"]))
+    obj, _, pi, st = ctx.solve_values(z["x"], z["values"], want_pi=True)
+    assert (st == 0).all()
+    np.testing.assert_allclose(obj, z["obj"], rtol=1e-9, atol=1e-9)
+    b = I.rhs_of("baa99-20", z["x"], z["values"])
+    for s in range(len(obj)):
+        assert abs(pi[s] @ b[s] - obj[s]) <= 1e-9 * (1 + abs(obj[s]))
+        assert _dual_feasible(inst["osp2"], pi[s])
 
 
 def _dual_feasible(sp, pi, tol=1e-7):

@@ -122,3 +122,45 @@ def test_master_sense_max():
     assert row.sense == MAX_SENSE and row.alpha == 0.25 * 1.0 + 0.75 * 8.0
     with pytest.raises(ValueError):
         add_cut_to_master(sdMasterCuts(1, "FEASIBILITY"), c1, 0, 1.0, 0.0)
+
+
+def test_sync_and_removal_match_oracle_restatement():
+    """The product bookkeeping (sqlp_amd.cut_pool) vs the oracle's restatement of
+    algorithm.jl:57-72 and cell.jl:167-201 on random multi-epigraph cut lists: the same cuts
+    survive removal, and sync_cuts! writes the same master rows in the same order."""
+    from sqlp_amd.cut_pool import sdMasterCuts
+    from sqlp_amd.twosd import sdCut
+    rng = np.random.default_rng(4)
+    E, n1 = 3, 5
+    epis, o_epis = [], []
+    for e in range(E):
+        tw = float(rng.integers(5, 20))
+        cuts = [sdCut(float(rng.normal()), rng.normal(size=n1), float(rng.integers(1, int(tw) + 1)))
+                for _ in range(int(rng.integers(2, 7)))]
+        inc = sdCut(float(rng.normal()), rng.normal(size=n1), tw) if e != 1 else None
+        lb = float(rng.normal())
+        epis.append(_Epi(cuts, inc, tw, lb))
+        o_epis.append(([(c.alpha, c.beta, c.weight_mark) for c in cuts], None if inc is None else
+                       (inc.alpha, inc.beta, inc.weight_mark), tw, lb))
+    m = sdMasterCuts(E)
+    m.sync_cuts(epis)
+    _check_rows(m, twosd_ref.sync_cuts(o_epis))
+    # multipliers: about half below CUT_REMOVE_TOLERANCE (incl. negatives, exactly the tolerance)
+    duals = [np.where(rng.random(len(m.epicon_ref[e])) < 0.5, rng.uniform(-9e-4, 9e-4, len(m.epicon_ref[e])),
+                      rng.uniform(1e-3, 1.0, len(m.epicon_ref[e]))) for e in range(E)]
+    duals[0][0] = 1e-3                                   # |dual| == tol is kept (strict '<')
+    m.remove_cuts_by_multiplier(epis, duals)
+    o_epis = [(twosd_ref.remove_cuts_by_multiplier(c, d), inc, tw, lb) for (c, inc, tw, lb), d in zip(o_epis, duals)]
+    for epi, (c, _, _, _) in zip(epis, o_epis):
+        assert [cut.alpha for cut in epi.cuts] == [a for a, _, _ in c]
+    m.sync_cuts(epis)
+    _check_rows(m, twosd_ref.sync_cuts(o_epis))
+
+
+def _check_rows(m, o_rows):
+    epi, alpha, beta, inc = m.rows()
+    assert len(o_rows) == len(alpha)
+    for r, (e, a, b, isinc) in enumerate(o_rows):
+        assert epi[r] == e and bool(inc[r]) == isinc
+        assert alpha[r] == a
+        np.testing.assert_array_equal(beta[r], b)

@@ -43,7 +43,7 @@ def _write_lp(path, name):
 def lp_files(tmp_path_factory):
     d = tmp_path_factory.mktemp("lps")
     out = []
-    for name in ["lands", "newsvendor", "transship", "ssn"]:
+    for name in ["lands", "newsvendor", "transship", "ssn", "baa99-20"]:
         p = str(d / f"{name}.lp")
         _write_lp(p, name)
         out.append(p)
@@ -72,7 +72,10 @@ def test_host_cpp_under_asan_ubsan(lp_files):
 def test_oracle_c_under_asan_ubsan(lp_files):
     subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "sanitize"])
     exe = os.path.join(ROOT, "oracle", "build", "oracle_check")
-    r = subprocess.run([exe] + lp_files, capture_output=True, text=True, env=_env(), timeout=600)
+    # the C port starts from the slack basis, which needs q >= 0 (baa99-20 has negative costs:
+    # its setup basis is covered by host_check's phase-1 + primal simplex above)
+    files = [f for f in lp_files if not f.endswith("baa99-20.lp")]
+    r = subprocess.run([exe] + files, capture_output=True, text=True, env=_env(), timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr
-    assert r.stdout.count("batch optimal") == len(lp_files)
+    assert r.stdout.count("batch optimal") == len(files)
