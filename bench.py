@@ -178,8 +178,11 @@ def main():
     # pool size by the per-rank shard (profiles/r01/configs/pool_sweep7.jsonl): a larger pool
     # saves pivots but its per-x preparation (x_B, selection stream) is a fixed cost per step
     # and its B^-1 data competes for L2, so small shards (the N > 1 steps) prefer 16384
+    # with the per-x refresh on, the timed steps never use the setup pool (the warmup's refresh
+    # replaces it), so only the primary basis is installed
     if args.pool <= 0:
-        args.pool = 32768 if args.scenarios // max(1, args.epigraphs) // world >= 500_000 else 16384
+        args.pool = 1 if args.refresh else (32768 if args.scenarios // max(1, args.epigraphs) // world >= 500_000
+                                            else 16384)
     if args.pool_train <= 0:
         args.pool_train = 4 * args.pool
     t_pool = time.perf_counter()
@@ -247,12 +250,14 @@ def main():
     if args.refresh:
         rtr = twosd.sdEpigraph(ctx, 1.0, 0.0)
         scenarios(rtr, 0, args.refresh_train, args.seed + 4)
-    pool_at = {"x": xs[0].copy()}    # the pool was built at x_EV
+    # the pool is not at any x point yet: the first step at every x pays its refresh (the
+    # setup pool, if any, was built at x_EV from other training scenarios)
+    pool_at = {"x": None}
 
     def refresh(xx):
         """Per-x warm-start pool: rebuilt from the training scenarios' optimal bases at xx
         (timed as part of the step), two-level selection lists from the same scenarios."""
-        if rtr is None or np.array_equal(pool_at["x"], xx):
+        if rtr is None or (pool_at["x"] is not None and np.array_equal(pool_at["x"], xx)):
             return 0.0
         t0 = time.perf_counter()
         ctx.pool_refresh(rtr, xx, 0, args.refresh_train, args.refresh_pool)
@@ -307,8 +312,10 @@ def main():
         torch.cuda.synchronize(device)
 
     m = sp2.shape[0]
-    for _ in range(args.warmup):
-        step(xs[0])
+    # warmup steps cycle over the x points so that the last one is at xs[-1]: the first timed
+    # step (at xs[0]) then pays its refresh like every later one
+    for i in range(args.warmup):
+        step(xs[(i - args.warmup) % X])
     barrier()
     acc = {"lp": 0.0, "dd": 0.0, "cut": 0.0, "fin": 0.0, "sel": 0.0, "flops": 0.0, "piv": 0, "pmax": 0}
     per_x = [{"piv": 0, "n": 0, "lp": 0.0, "wall": 0.0, "steps": 0, "alpha": None, "refresh": 0.0} for _ in xs]
@@ -435,6 +442,9 @@ def main():
             out["cutgen"]["traffic_source"] = pmc["file"]
     if rank == 0 and world == 1 and args.spot > 0:
         out["parity_spot_check"] = spot_check(sp2, ctx, epi, V, xs, x_iters, positions, args)
+    if rank == 0 and world == 1 and args.spot > 0 and not args.no_dedup:
+        j = min(1, X - 1)
+        out["push_check"] = push_check(ctx, epi, V, nv, xs[j], x_iters[j], n_local, refresh)
     if rank == 0 and world == 1 and not args.no_cpu:
         vals = twosd.get_scenarios(epi, 0, min(n_local, 1 << 19))   # the CPU sample: same scenarios
         out["cpu_baseline"] = cpu_baseline(sp2, ctx, xs, x_iters, heads_at, vals, V.matrix(), args)
@@ -466,6 +476,29 @@ def sd_points(cor, tim, sp2, sto, positions, x_ev, iters, seed, device):
                 out[it] = cell.x_candidate.copy()
         c2.close()
     return [out[i] for i in iters]
+
+
+def push_check(ctx, epi, V, nv, xx, it, n, refresh):
+    """The keyed push of the timed steps vs pushing every scenario's pi (TWOSD_PUSH_ALL=1,
+    push! of dual_set.jl:84-94 for s = 1..N in order), over the whole shard at one x point with
+    the pool refreshed there: vertex count and the order-dependent fingerprint of V."""
+    from sqlp_amd import twosd
+    refresh(xx)
+    res = {"x_iteration": it, "scenarios": n}
+    for key, env in (("keyed", None), ("push_all", "1")):
+        V.truncate(nv)
+        if env:
+            os.environ["TWOSD_PUSH_ALL"] = env
+        try:
+            twosd.solve_push(epi, xx, 0, n, want_obj=False)
+        finally:
+            os.environ.pop("TWOSD_PUSH_ALL", None)
+        res[key] = {"new_vertices": len(V) - nv, "fingerprint": f"{V.fingerprint():016x}",
+                    "pushed": ctx.last_push_reps()}
+    V.truncate(nv)
+    res["identical"] = (res["keyed"]["new_vertices"] == res["push_all"]["new_vertices"] and
+                        res["keyed"]["fingerprint"] == res["push_all"]["fingerprint"])
+    return res
 
 
 def spot_check(sp2, ctx, epi, V, xs, x_iters, positions, args):
@@ -564,7 +597,7 @@ def cpu_baseline(sp2, ctx, xs, x_iters, heads_at, vals, Vmat, args):
             t_setup += time.perf_counter() - t0
             timed(lambda d: lp.solve_batch_pool(rows, base, d, nthreads=threads)[3], "pooled")
     cut_per = t_cut / max(n_cut, 1)
-    out = {"unit": "subproblems/s", "cores": threads, "kind": "port"}
+    out = {"unit": "subproblems/s", "cores": threads, "node_cpus": os.cpu_count(), "kind": "port"}
     for key, (n, t, piv) in tot.items():
         if n:
             out[key] = {"value": n / (t + cut_per * n), "scenarios": n, "lp_s": round(t, 3), "lp_pivots_mean": piv / n}

@@ -235,6 +235,15 @@ int twosd_last_timings(twosd_ctx *ctx, double *us5);
 /* Statistics of the last LP batch: sum of simplex pivots, max pivots. */
 int twosd_last_lp_stats(twosd_ctx *ctx, int64_t *pivots_sum, int *pivots_max);
 
+/* Diagnostic: pivots and status of every scenario of the last LP launch (by scenario index;
+ * after a pool refresh: its training solves). */
+int twosd_last_lp_iters(twosd_ctx *ctx, int N, int *iters, int *status);
+
+/* Pivot cap of the training solves of twosd_pool_refresh (0: the kernel's kmax).  A training
+ * scenario that needs more pivots drops out of the basis count instead of holding the launch:
+ * one wavefront per scenario, so a launch lasts as long as its slowest scenario. */
+int twosd_set_refresh_kcap(twosd_ctx *ctx, int kcap);
+
 /* Executed fp64 row operations of the last LP batch: each is one fused multiply-add over
  * a padded basis row of *row_width (= 64 * ceil(m2/64)) doubles, i.e. 2 * row_width flops
  * (used for the counted-FLOP roofline of the LP kernel). */

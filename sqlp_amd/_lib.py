@@ -68,6 +68,8 @@ SIGNATURES = [
     ("twosd_last_lp_stats", I, [P, P, P]),
     ("twosd_last_lp_ops", I, [P, P, P]),
     ("twosd_debug_stamps", I, [P, P, I]),
+    ("twosd_last_lp_iters", I, [P, I, P, P]),
+    ("twosd_set_refresh_kcap", I, [P, I]),
 ]
 
 _lib = None

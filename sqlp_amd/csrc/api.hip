@@ -861,6 +861,19 @@ static int refresh_build_device(twosd_ctx *c, const std::vector<int> &sel) {
     }
     const int P = (int)map.size();
     if ((rc = dev_reserve(c, &c->d_pg_map, (size_t)P)) || (rc = dev_reserve(c, &c->d_pg_off, (size_t)4 * P))) return rc;
+    // From here the live pool arrays are grown in place (a grown array does not keep its
+    // contents) and then overwritten: a failure past this point leaves c->pool describing
+    // arrays that no longer hold it.  The context then drops its basis, so every later solve
+    // fails cleanly (TWOSD_E_STATE) until twosd_compute_basis / twosd_set_basis installs one.
+    auto broken = [c](int code) {
+        c->has_basis = false;
+        c->prep_valid = false;
+        c->k_valid = false;
+        c->pool_l1 = c->pool_ncand = 0;
+        return code;
+    };
+    if (const char *inj = getenv("TWOSD_INJECT_FAIL"); inj && !strcmp(inj, "refresh_fill"))   // test hook
+        return broken(fail(TWOSD_E_DEVICE, "pool refresh: injected failure after the pool-array reservation"));
     HIPCHK(hipMemcpyAsync(c->d_pg_map, map.data(), sizeof(int) * P, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->d_pg_off, off.data(), sizeof(int) * 4 * P, hipMemcpyHostToDevice, c->stream));
     const size_t nz = (size_t)acc[0], kz = (size_t)acc[1], ez = (size_t)acc[2] * 64;
@@ -873,7 +886,7 @@ static int refresh_build_device(twosd_ctx *c, const std::vector<int> &sel) {
         (rc = dev_reserve(c, &c->d_hb0, (size_t)P * MP)) || (rc = dev_reserve(c, &c->d_basic0, (size_t)P * 64)) ||
         (rc = dev_reserve(c, &c->d_bnnz, (size_t)P)) || (rc = dev_reserve(c, &c->d_d0, (size_t)P * 64 * c->CH)) ||
         (rc = dev_reserve(c, &c->d_sel_ptr, (size_t)P + 1)) || (rc = reserve_selection(c, P, (int)acc[3])))
-        return rc;
+        return broken(rc);
     // (a grown array is reallocated: the start pool's CSC was read only by the FTRAN passes)
     PgFill F{};
     F.P = P; F.map = c->d_pg_map; F.off = c->d_pg_off; F.sel_total = (int)acc[3]; F.d0_primary = c->d_pg_d0p;
@@ -883,11 +896,12 @@ static int refresh_build_device(twosd_ctx *c, const std::vector<int> &sel) {
     A.a0 = 0;
     F.P0 = 0;
     const auto t3 = now();
-    HIPCHK(pg_launch_fill(A, F, P, c->stream));
+    if (pg_launch_fill(A, F, P, c->stream) != hipSuccess) return broken(fail(TWOSD_E_DEVICE, "pool refresh: fill launch failed"));
     int *h_hb = stage_buf<int>(c, 10, (size_t)P * MP);   // the pool's heads, from hb0 = 4 head + type
-    if (!h_hb) return fail(TWOSD_E_DEVICE, "pool refresh: pinned staging allocation failed");
-    HIPCHK(hipMemcpyAsync(h_hb, c->d_hb0, sizeof(int) * P * MP, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    if (!h_hb) return broken(fail(TWOSD_E_DEVICE, "pool refresh: pinned staging allocation failed"));
+    if (hipMemcpyAsync(h_hb, c->d_hb0, sizeof(int) * P * MP, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return broken(fail(TWOSD_E_DEVICE, "pool refresh: reading the built pool heads failed"));
     if (dbg) {
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         fprintf(stderr, "refresh_build_device: %d sources, ftran-0 %.2f, ftran-1+count %.2f, offsets %.2f, fill %.2f ms (%lld intermediate)\n", nsrc, ms(t0, t1),
@@ -931,6 +945,10 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
     o.want_bkey = true;
     o.want_etas = true;
     o.want_head = true;
+    // training scenarios beyond the pivot cap only drop out of the basis count (one launch
+    // lasts as long as its slowest scenario: with one scenario per wave the cap bounds it)
+    o.kcap = c->train_kcap;
+    if (const char *e = getenv("TWOSD_TRAIN_KCAP")) o.kcap = atoi(e);   // A/B knob
     if ((rc = run_lp_ex(c, x, d_dv, count, o))) return rc;
     const auto t1 = std::chrono::steady_clock::now();
     // 2. distinct optimal bases, most frequent first (ties: first occurrence), primary excluded
@@ -978,8 +996,9 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
         HIPCHK(hipMemcpy(etap.data(), c->d_eo_etap, sizeof(int) * etap.size(), hipMemcpyDeviceToHost));
         HIPCHK(hipMemcpy(etaoff.data(), c->d_eo_etaoff, sizeof(int) * etaoff.size(), hipMemcpyDeviceToHost));
         HIPCHK(hipMemcpy(heads.data(), c->d_head_out, sizeof(int) * heads.size(), hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(&used, c->d_eo_used, sizeof(int), hipMemcpyDeviceToHost));
-        used = std::min<int>(used, (int)c->eo_cap);
+        unsigned long long used64 = 0;
+        HIPCHK(hipMemcpy(&used64, c->d_eo_used, sizeof(used64), hipMemcpyDeviceToHost));
+        used = (int)std::min<unsigned long long>(used64, std::min<size_t>(c->eo_cap, INT32_MAX));
         std::vector<int> ei(std::max(used, 1));
         std::vector<double> ev(std::max(used, 1));
         if (used > 0) {
@@ -1740,6 +1759,8 @@ int twosd::run_lp_ex(twosd_ctx *c, const double *x, const double *d_dv, int N, c
         HIPCHK(hipMemsetAsync(c->d_queue, 0, sizeof(int) * kMaxQueueGroups * kQueueStride, c->stream));
         HyperParams H{};
         H.m = m; H.n = n; H.k = c->k; H.N = NL; H.kmax = kmax; H.ecap = ecap;
+        H.kcap = o.kcap > 0 ? std::min(o.kcap, kmax) : kmax;
+        H.retry = o.kcap > 0 ? 0 : 1;
         H.colptr = c->d_colptr; H.rowidx = c->d_rowidx; H.val = c->d_val; H.q = c->d_q; H.btype = c->d_btype;
         H.wr_width = c->wr_width; H.wr_col = c->d_wr_col; H.wr_val = c->d_wr_val;
         H.wr_ocol = c->d_wr_ocol; H.wr_oval = c->d_wr_oval;
@@ -1753,9 +1774,16 @@ int twosd::run_lp_ex(twosd_ctx *c, const double *x, const double *d_dv, int N, c
         if (const char *e = getenv("TWOSD_QGROUPS")) H.qgroups = std::max(1, std::min({kMaxQueueGroups, nblocks, atoi(e)}));   // A/B knob
         H.obj = c->d_obj; H.pi = want_pi ? c->d_pi : nullptr; H.y = want_y ? c->d_y : nullptr;
         H.vkey = o.want_key ? c->d_vkey : nullptr;
+        H.key_zero = 1e-12;   // = HPI_ZERO of the pi recovery (lp_hyper.hip)
+        if (const char *e = getenv("TWOSD_KEY_ZERO")) H.key_zero = atof(e);   // A/B knob
         H.bkey = o.want_bkey ? c->d_bkey : nullptr;
         if (o.want_etas) {   // rows: list positions, or scenarios
             const size_t need = list ? (size_t)NL : (size_t)N;
+            // eta-file offsets are 32-bit (eo_off, the device pool build): the arena of
+            // 4096 entries per row must stay below 2^31 entries
+            if (need * 4096 > (size_t)INT32_MAX)
+                return fail(TWOSD_E_UNSUPPORTED, "eta files of %zu solves exceed the 2^31-entry arena (at most %d)", need,
+                            INT32_MAX / 4096);
             if (need > c->eo_rows || c->eo_kmax != kmax) {
                 const size_t rows = std::max<size_t>(need, 256);
                 if ((rc = dalloc(&c->d_eo_pb, rows)) || (rc = dalloc(&c->d_eo_K, rows)) || (rc = dalloc(&c->d_eo_off, rows)) ||
@@ -1767,10 +1795,10 @@ int twosd::run_lp_ex(twosd_ctx *c, const double *x, const double *d_dv, int N, c
                 c->eo_cap = rows * 4096;
                 c->eo_kmax = kmax;
             }
-            HIPCHK(hipMemsetAsync(c->d_eo_used, 0, sizeof(int), c->stream));
+            HIPCHK(hipMemsetAsync(c->d_eo_used, 0, sizeof(unsigned long long), c->stream));
             H.eo_pb = c->d_eo_pb; H.eo_K = c->d_eo_K; H.eo_off = c->d_eo_off; H.eo_etap = c->d_eo_etap;
             H.eo_etaoff = c->d_eo_etaoff; H.eo_eidx = c->d_eo_eidx; H.eo_evals = c->d_eo_evals; H.eo_used = c->d_eo_used;
-            H.eo_cap = (int)std::min<size_t>(c->eo_cap, INT32_MAX);
+            H.eo_cap = (long long)std::min<size_t>(c->eo_cap, INT32_MAX);
         }
         if (o.want_head) {   // rows: list positions, or scenarios
             const size_t need = list ? (size_t)NL : (size_t)N;
@@ -1922,6 +1950,20 @@ extern "C" int twosd_last_lp_stats(twosd_ctx *c, int64_t *sum, int *mx) {
     return TWOSD_OK;
 }
 
+extern "C" int twosd_set_refresh_kcap(twosd_ctx *c, int kcap) {
+    if (!c || kcap < 0) return fail(TWOSD_E_ARG, "set_refresh_kcap: bad argument");
+    c->train_kcap = kcap;
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_last_lp_iters(twosd_ctx *c, int N, int *iters, int *status) {
+    if (!c || N < 0 || N > c->out_cap || !c->d_iters) return fail(TWOSD_E_ARG, "last_lp_iters: N = %d outside the last batch", N);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (iters) HIPCHK(hipMemcpy(iters, c->d_iters, sizeof(int) * N, hipMemcpyDeviceToHost));
+    if (status) HIPCHK(hipMemcpy(status, c->d_status, sizeof(int) * N, hipMemcpyDeviceToHost));
+    return TWOSD_OK;
+}
+
 extern "C" int twosd_debug_stamps(twosd_ctx *c, uint64_t *out10, int reset) {
     if (!c || !out10) return fail(TWOSD_E_ARG, "debug_stamps: NULL");
     for (int i = 0; i < 10; ++i) out10[i] = 0;
@@ -1936,6 +1978,13 @@ extern "C" int twosd_last_lp_ops(twosd_ctx *c, int64_t *row_ops, int *row_width)
     if (row_ops) *row_ops = c->last_ops_sum;
     if (row_width) *row_width = c->last_ops_width;
     return TWOSD_OK;
+}
+
+// non-optimal statuses among the scenarios of a list-mode re-solve (status is by scenario)
+__global__ void list_status_kernel(int U, const int *__restrict__ list, const int *__restrict__ st,
+                                   unsigned long long *bad) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < U; i += gridDim.x * blockDim.x)
+        if (st[list[i]] != TWOSD_LP_OPTIMAL) atomicAdd(bad, 1ull);
 }
 
 extern "C" int twosd_solve_push(twosd_ctx *c, int epi, const double *x, int first, int count, double *obj, int *status,
@@ -1985,6 +2034,16 @@ extern "C" int twosd_solve_push(twosd_ctx *c, int epi, const double *x, int firs
             r.d_list = d_list;
             r.nlist = U;
             if ((rc = run_lp_ex(c, x, d_dv, count, r))) return rc;
+            // the re-solve starts every representative from its recorded pick and repeats its
+            // optimal solve; should one ever end otherwise, its pi row must not reach V
+            HIPCHK(hipMemsetAsync(c->d_lpstats, 0, sizeof(unsigned long long), c->stream));
+            hipLaunchKernelGGL(list_status_kernel, dim3((unsigned)std::min(256, (U + 255) / 256)), dim3(256), 0, c->stream, U,
+                               d_list, c->d_status, c->d_lpstats);
+            HIPCHK(hipGetLastError());
+            unsigned long long bad = 0;
+            HIPCHK(hipMemcpyAsync(&bad, c->d_lpstats, sizeof(bad), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            if (bad) return fail(TWOSD_E_LP, "solve_push: %llu of %d re-solved representatives not optimal; nothing pushed", bad, U);
             c->t_us[0] += t_lp;   // LP kernel time of the batch: main pass + representatives
             HIPCHK(hipEventRecord(c->ev[2], c->stream));
             if ((rc = dvs_push_device(c, U, c->d_pi, nullptr))) return rc;

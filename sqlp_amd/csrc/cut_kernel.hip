@@ -15,11 +15,13 @@
 // Kernels:
 //   cut_pk_kernel      PK (|V| x k4 row-major) and PKT (k4 x vcap) gathers of new vertices
 //   cut_vbase_kernel   base[v] = pi_v . (r - T x)                (8|V|(m+1) bytes)
-//   cut_argmax_kernel  MFMA score tiles (16 scenarios x 16 vertices x 4 k per
-//                      v_mfma_f64_16x16x4f64), vertex chunks staged in LDS (k-major,
-//                      bank-conflict-free stride), running max/argmax per scenario in
-//                      registers; per-wave partial sums; h via uint64 fixed-point atomics
-//                      (exact and order independent -> identical on any rank count)
+//   cut_pktc_kernel    PKTc = coef(x) * PKT plus the base row: the chunk source of the argmax
+//   cut_argmax2_kernel MFMA score tiles (v_mfma_f64_16x16x4f64: 32 vertices x 32 scenarios
+//                      per wave and chunk), vertex chunks DMA'd into LDS, running max/argmax
+//                      per scenario in registers; per-wave partial sums; h via uint64
+//                      fixed-point atomics (exact and order independent -> identical on any
+//                      rank count); the last round's tiles split by vertex range
+//   cut_tail_merge_kernel  per-range results of the split tiles merged in vertex order
 //   cut_fixup_kernel   scenarios whose running argmax slid within the tolerance band are
 //                      re-decided by the exact two-pass rule (sequential fp64)
 //   cut_reduce_kernel  deterministic fixed-order sum of the partial slots
@@ -35,9 +37,6 @@ namespace twosd {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-constexpr int kVT = 32;            // vertices per LDS chunk (2 MFMA column tiles)
-constexpr int kCutTile = 64;       // scenarios per block tile (4 waves x one MFMA row tile of 16)
-constexpr int kLdsStride = 48;     // doubles per k-row in LDS (== 16 mod 32: conflict-free b64 reads)
 constexpr double kFix = 4611686018427387904.0;   // 2^62 fixed-point scale of p_w
 
 constexpr int kHistLds = 256;      // |V| up to this: the block histogram lives in LDS
@@ -58,6 +57,13 @@ struct CutParams {
     unsigned long long *hist;           // nv (fixed point)
     unsigned long long *hist_part;      // gridDim.x x nv block histograms (hist_lds mode)
     double *partial;       // slots x (k + 1): [sum p*val, S_0..S_{k-1}]
+    // work units of cut_argmax2_kernel: units [0, full_units) are whole scenario tiles; the
+    // tiles past them (the last, partial round of the persistent grid) are cut into tail_S
+    // vertex ranges each, and such a unit leaves its per-scenario (M, SV, I, F) in tp_* at
+    // [(s - 128 full_units) tail_S + range] for cut_tail_merge_kernel
+    int full_units, tail_S;
+    double *tp_m, *tp_sv;
+    int *tp_i, *tp_f;
 };
 
 __global__ void cut_pk_kernel(int from, int to, int m, int k, int k4, int vcap, const int *__restrict__ rows,
@@ -129,159 +135,6 @@ __device__ __forceinline__ void row_update_fast(RowBest &b, double s, int v, dou
     if (__builtin_expect(s > b.M, 0)) row_update(b, s, v, rel);
 }
 
-template <int KB>
-__global__ void __launch_bounds__(256, 2) cut_argmax_kernel(CutParams P) {
-    __shared__ double Bs[4 * KB * kLdsStride];
-    __shared__ double bs[kVT];
-    extern __shared__ unsigned long long hl[];   // nv entries when P.hist_lds
-    const int lane = threadIdx.x & 63;
-    const int wid = threadIdx.x >> 6;
-    if (P.hist_lds)
-        for (int v = threadIdx.x; v < P.nv; v += 256) hl[v] = 0ull;   // ordered before use by the chunk barriers
-    const int g = lane >> 4, j = lane & 15;
-    const int ntiles = (P.N + kCutTile - 1) / kCutTile;
-    const int nchunks = (P.nv + kVT - 1) / kVT;
-    // per-wave partial sums (lanes stride over elements)
-    double pv_sum = 0.0;
-    double Sacc[2] = {0.0, 0.0};
-
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        // this wave: scenarios s0 .. s0+15 as one 16-row MFMA A tile
-        const int s0 = tile * kCutTile + wid * 16;
-        double a0[KB];
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
-            const int e = 4 * kb + g;
-            const int sa = s0 + j;
-            a0[kb] = (sa < P.N && e < P.k) ? P.dv[(size_t)sa * P.k + e] * P.coef[e] : 0.0;
-        }
-        // lane (g, j) tracks rows g + 4r over the vertex columns j, 16 + j of every chunk
-        // (its own increasing vertex subsequence); lanes are combined once at the end
-        RowBest rb[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) { rb[r].M = -INFINITY; rb[r].SV = -INFINITY; rb[r].I = -1; rb[r].F = 0; }
-
-        // chunk staging is software-pipelined: chunk ch+1 is loaded into registers while
-        // the MFMAs of chunk ch run, then written to LDS
-        constexpr int NPRE = (4 * KB * kVT + 255) / 256;
-        double pre[NPRE];
-        double preb = -INFINITY;
-        auto load_chunk = [&](int v0) {
-#pragma unroll
-            for (int u = 0; u < NPRE; ++u) {
-                const int idx = threadIdx.x + 256 * u;
-                const int kk = idx / kVT, vv = idx % kVT;
-                const int v = v0 + vv;
-                pre[u] = (idx < 4 * KB * kVT && v < P.nv && kk < P.k4) ? P.PKT[(size_t)kk * P.vcap + v] : 0.0;
-            }
-            if (threadIdx.x < kVT) preb = v0 + (int)threadIdx.x < P.nv ? P.base[v0 + threadIdx.x] : -INFINITY;
-        };
-        load_chunk(0);
-        for (int ch = 0; ch < nchunks; ++ch) {
-            const int v0 = ch * kVT;
-            __syncthreads();
-#pragma unroll
-            for (int u = 0; u < NPRE; ++u) {
-                const int idx = threadIdx.x + 256 * u;
-                if (idx < 4 * KB * kVT) Bs[(idx / kVT) * kLdsStride + idx % kVT] = pre[u];
-            }
-            if (threadIdx.x < kVT) bs[threadIdx.x] = preb;
-            __syncthreads();
-            if (ch + 1 < nchunks) load_chunk(v0 + kVT);
-            d4 c00 = {0.0, 0.0, 0.0, 0.0}, c01 = c00;
-#pragma unroll
-            for (int kb = 0; kb < KB; ++kb) {
-                const double b0 = Bs[(4 * kb + g) * kLdsStride + j];
-                const double b1 = Bs[(4 * kb + g) * kLdsStride + 16 + j];
-                c00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[kb], b0, c00, 0, 0, 0);
-                c01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[kb], b1, c01, 0, 0, 0);
-            }
-            // C/D layout: acc[r] is row g + 4r, column j of its 16x16 tile
-            const int va = v0 + j, vb = v0 + 16 + j;
-            const double ba = va < P.nv ? bs[j] : -INFINITY, bb = vb < P.nv ? bs[16 + j] : -INFINITY;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                row_update(rb[r], ba + c00[r], va, P.tie_rel);
-                row_update(rb[r], bb + c01[r], vb, P.tie_rel);
-            }
-        }
-        // combine the 16 lanes (j) of each row: global max M, threshold M - tolf(M); the
-        // answer is the lowest lane candidate inside the band.  A lane whose max reaches
-        // the band but whose candidate does not (or that flagged) -> exact fixup.
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            double M = rb[r].M;
-#pragma unroll
-            for (int o = 8; o > 0; o >>= 1) M = fmax(M, __shfl_xor(M, o));
-            const double thr = M - tolf(M, P.tie_rel);
-            const bool reach = rb[r].M != -INFINITY && rb[r].M >= thr;
-            int it = (reach && rb[r].SV >= thr) ? rb[r].I : 0x7fffffff;
-            double st = rb[r].SV;
-            int fl = reach && (rb[r].F || !(rb[r].SV >= thr));
-#pragma unroll
-            for (int o = 8; o > 0; o >>= 1) {
-                const int i2 = __shfl_xor(it, o);
-                const double s2 = __shfl_xor(st, o);
-                fl |= __shfl_xor(fl, o);
-                if (i2 < it) { it = i2; st = s2; }
-            }
-            rb[r].I = (M == -INFINITY || it == 0x7fffffff) ? -1 : it;
-            rb[r].SV = st;
-            rb[r].F = fl;
-        }
-        // write results, accumulate partials for decided rows
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int s = s0 + g + 4 * r;
-            if (j == 0 && s < P.N) {
-                P.arg[s] = rb[r].I;
-                P.val[s] = rb[r].SV;
-                P.flag[s] = rb[r].F;
-            }
-        }
-        // partial sums over the 16 rows of this wave, branch-free so every row's loads are in
-        // flight together: an undecided row (flagged, no vertex, past N) gets p = 0 and vertex 0
-        // (adds exact zeros).  The vertex histogram goes to LDS (small |V|: no contention on a
-        // few global addresses) or global atomics; both uint64 fixed point: exact.
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-#pragma unroll
-            for (int gg = 0; gg < 4; ++gg) {
-                const int s = s0 + gg + 4 * r;
-                const int ai = __shfl(rb[r].I, gg * 16);
-                const int fl = __shfl(rb[r].F, gg * 16);
-                const double vl = __shfl(rb[r].SV, gg * 16);
-                const bool ok = s < P.N && !fl && ai >= 0;
-                const int au = ok ? ai : 0, su = min(s, P.N - 1);
-                const double p = ok ? P.w[su] * P.inv_total : 0.0;
-                if (lane == 0 && ok) {
-                    pv_sum = fma(p, vl, pv_sum);
-                    const unsigned long long hq = (unsigned long long)__double2ull_rn(p * kFix);
-                    if (P.hist_lds) __hip_atomic_fetch_add(&hl[au], hq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    else atomicAdd(&P.hist[au], hq);
-                }
-#pragma unroll
-                for (int t = 0; t < 2; ++t) {
-                    const int e = lane + 64 * t;
-                    if (e < P.k) Sacc[t] = fma(p * P.PK[(size_t)au * P.k4 + e], P.dv[(size_t)su * P.k + e], Sacc[t]);
-                }
-            }
-        }
-    }
-    if (P.hist_lds) {   // block histogram -> its own slot (summed by cut_hist_reduce_kernel)
-        __syncthreads();
-        for (int v = threadIdx.x; v < P.nv; v += 256) P.hist_part[(size_t)blockIdx.x * P.nv + v] = hl[v];
-    }
-    const int slot = blockIdx.x * 4 + wid;
-    double *out = P.partial + (size_t)slot * (P.k + 1);
-    if (lane == 0) out[0] = pv_sum;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const int e = lane + 64 * t;
-        if (e < P.k) out[1 + e] = Sacc[t];
-    }
-}
-
 // ---- v2: the score tile transposed -- MFMA A operand = the staged vertex chunk, B operand =
 // the scenario deltas -- so the C/D layout puts one SCENARIO per lane column (j) and four
 // vertices per lane (rows g + 4r): a lane tracks the running argmax of ONE scenario per A tile
@@ -330,10 +183,17 @@ __global__ void __launch_bounds__(256, 2) cut_argmax2_kernel(CutParams P) {
     const int g = lane >> 4, j = lane & 15;
     const int ntiles = (P.N + kCutTile2 - 1) / kCutTile2;
     const int nchunks = (P.nv + kVT2 - 1) / kVT2;
+    const int nunits = P.full_units + (ntiles - P.full_units) * P.tail_S;
     double pv_sum = 0.0;
     double Sacc[2] = {0.0, 0.0};   // lane (g, j): e = 4 kb + g for kb = j, j + 16
 
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    for (int unit = blockIdx.x; unit < nunits; unit += gridDim.x) {
+        // a whole tile (all vertex chunks), or vertex range `range` of a tail tile
+        const bool tail = unit >= P.full_units;
+        const int tile = tail ? P.full_units + (unit - P.full_units) / P.tail_S : unit;
+        const int range = tail ? (unit - P.full_units) % P.tail_S : 0;
+        const int c_lo = tail ? (int)((long long)nchunks * range / P.tail_S) : 0;
+        const int c_hi = tail ? (int)((long long)nchunks * (range + 1) / P.tail_S) : nchunks;
         // this wave: scenarios s0 + j (tile 0) and s0 + 16 + j (tile 1); lane (g, j) holds their
         // deltas e = 4 kb + g (the B operand: k = g, column = j)
         const int s0 = tile * kCutTile2 + wid * 32;
@@ -364,15 +224,15 @@ __global__ void __launch_bounds__(256, 2) cut_argmax2_kernel(CutParams P) {
             }
             if (!TWOSD_CUT_BASEK && threadIdx.x < kVT2) preb = v0 + (int)threadIdx.x < P.nv ? P.base[v0 + threadIdx.x] : -INFINITY;
         };
-        stage(0, 0);
+        stage(0, c_lo * kVT2);
         if (!TWOSD_CUT_BASEK && threadIdx.x < kVT2) bs[0][threadIdx.x] = preb;
-        __syncthreads();            // chunk 0 landed (the barrier drains the DMA)
-        for (int ch = 0; ch < nchunks; ++ch) {
-            const int buf = ch & 1;
+        __syncthreads();            // chunk c_lo landed (the barrier drains the DMA)
+        for (int ch = c_lo; ch < c_hi; ++ch) {
+            const int buf = (ch - c_lo) & 1;
             const int v0 = ch * kVT2;
             // chunk ch+1 into the other buffer while this one is multiplied (its readers passed
             // the last barrier)
-            if (ch + 1 < nchunks) stage(buf ^ 1, v0 + kVT2);
+            if (ch + 1 < c_hi) stage(buf ^ 1, v0 + kVT2);
             d4 c00 = {0.0, 0.0, 0.0, 0.0}, c01 = c00, c10 = c00, c11 = c00;   // c[vertex tile][scenario tile]
             // fragments are read in groups of KG k-blocks ahead of their MFMAs; the scheduling
             // barrier keeps the compiler from hoisting every read of the chunk (register spills)
@@ -464,7 +324,7 @@ __global__ void __launch_bounds__(256, 2) cut_argmax2_kernel(CutParams P) {
                 RU2(rb1, bb + c11[r], vb, P.tie_rel);
             }
             }
-            if (!TWOSD_CUT_BASEK && ch + 1 < nchunks && threadIdx.x < kVT2) bs[buf ^ 1][threadIdx.x] = preb;
+            if (!TWOSD_CUT_BASEK && ch + 1 < c_hi && threadIdx.x < kVT2) bs[buf ^ 1][threadIdx.x] = preb;
             __syncthreads();
         }
         // combine the 4 lanes (g) of each scenario column: max M, band threshold, lowest candidate
@@ -489,10 +349,25 @@ __global__ void __launch_bounds__(256, 2) cut_argmax2_kernel(CutParams P) {
             rb.I = (M == -INFINITY || it == 0x7fffffff) ? -1 : it;
             rb.SV = st;
             rb.F = fl;
+            rb.M = M;
         };
         combine(rb0);
         combine(rb1);
         const int sa = s0 + j, sb = s0 + 16 + j;
+        if (tail) {   // this vertex range's result; cut_tail_merge_kernel decides and sums
+            if (g == 0) {
+                const int t0 = P.full_units * kCutTile2;
+                if (sa < P.N) {
+                    const size_t o = (size_t)(sa - t0) * P.tail_S + range;
+                    P.tp_m[o] = rb0.M; P.tp_sv[o] = rb0.SV; P.tp_i[o] = rb0.I; P.tp_f[o] = rb0.F;
+                }
+                if (sb < P.N) {
+                    const size_t o = (size_t)(sb - t0) * P.tail_S + range;
+                    P.tp_m[o] = rb1.M; P.tp_sv[o] = rb1.SV; P.tp_i[o] = rb1.I; P.tp_f[o] = rb1.F;
+                }
+            }
+            continue;
+        }
         if (g == 0) {
             if (sa < P.N) { P.arg[sa] = rb0.I; P.val[sa] = rb0.SV; P.flag[sa] = rb0.F; }
             if (sb < P.N) { P.arg[sb] = rb1.I; P.val[sb] = rb1.SV; P.flag[sb] = rb1.F; }
@@ -560,6 +435,63 @@ __global__ void __launch_bounds__(256) cut_hist_reduce_kernel(int nb, int nv, co
     unsigned long long s = 0;
     for (int b = 0; b < nb; ++b) s += part[(size_t)b * nv + v];
     hist[v] += s;
+}
+
+// Tail scenarios: merge the per-range results in vertex order -- the same rule as `combine`
+// over the 4 lanes of a column: M = max, band threshold, lowest candidate inside the band,
+// flag when a range reaches the band but its candidate does not -- then, for a decided
+// scenario, its p * val, histogram weight and S_e terms (as cut_fixup_kernel).  One wavefront
+// per scenario, lane r = range r.
+__global__ void __launch_bounds__(256) cut_tail_merge_kernel(CutParams P, int slot0) {
+    const int lane = threadIdx.x & 63;
+    const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int nw = (gridDim.x * blockDim.x) >> 6;
+    const int t0 = P.full_units * kCutTile2, S = P.tail_S;
+    double pv_sum = 0.0, Sacc[2] = {0.0, 0.0};
+    for (int ts = gw; ts < P.N - t0; ts += nw) {
+        const int s = t0 + ts;
+        double m = -INFINITY, sv = -INFINITY;
+        int ii = -1, ff = 0;
+        if (lane < S) {
+            const size_t o = (size_t)ts * S + lane;
+            m = P.tp_m[o]; sv = P.tp_sv[o]; ii = P.tp_i[o]; ff = P.tp_f[o];
+        }
+        double M = m;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) M = fmax(M, __shfl_xor(M, o));
+        const double thr = M - tolf(M, P.tie_rel);
+        const bool reach = m != -INFINITY && m >= thr;
+        int it = (reach && ii >= 0 && sv >= thr) ? ii : 0x7fffffff;
+        double st = sv;
+        int fl = reach && (ff || ii < 0 || !(sv >= thr));
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const int i2 = __shfl_xor(it, o);
+            const double s2 = __shfl_xor(st, o);
+            fl |= __shfl_xor(fl, o);
+            if (i2 < it) { it = i2; st = s2; }
+        }
+        const int I = (M == -INFINITY || it == 0x7fffffff) ? -1 : it;
+        if (lane == 0) { P.arg[s] = I; P.val[s] = st; P.flag[s] = fl; }
+        if (fl || I < 0) continue;
+        const double p = P.w[s] * P.inv_total;
+        if (lane == 0) {
+            pv_sum = fma(p, st, pv_sum);
+            atomicAdd(&P.hist[I], (unsigned long long)__double2ull_rn(p * kFix));
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int e = lane + 64 * t;
+            if (e < P.k) Sacc[t] = fma(p * P.PK[(size_t)I * P.k4 + e], P.dv[(size_t)s * P.k + e], Sacc[t]);
+        }
+    }
+    double *out = P.partial + (size_t)(slot0 + gw) * (P.k + 1);
+    if (lane == 0) out[0] = pv_sum;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int e = lane + 64 * t;
+        if (e < P.k) out[1 + e] = Sacc[t];
+    }
 }
 
 // exact two-pass rule for flagged scenarios; one wavefront per scenario
@@ -681,6 +613,9 @@ struct CutWs {
     unsigned long long *hist = nullptr, *hist_part = nullptr;
     size_t hpart_cap = 0;
     double *part2 = nullptr;
+    double *tp_m = nullptr, *tp_sv = nullptr;
+    int *tp_i = nullptr, *tp_f = nullptr;
+    size_t tp_cap = 0;
     size_t base_cap = 0, part_cap = 0, n_cap = 0, hist_cap = 0, gpart_cap = 0, sums_cap = 0, part2_cap = 0;
     int m = 0, vec_m = 0;
     std::vector<double> h_coef, h_bvec;   // pinned-lifetime host staging for async uploads
@@ -697,6 +632,7 @@ void cut_free(twosd_ctx *c) {
     hipFree(w->PK); hipFree(w->PKT); hipFree(w->PKTc); hipFree(w->rows); hipFree(w->coef); hipFree(w->bvec); hipFree(w->base);
     hipFree(w->partial); hipFree(w->sums); hipFree(w->gpart); hipFree(w->g); hipFree(w->arg); hipFree(w->flag);
     hipFree(w->val); hipFree(w->hist); hipFree(w->part2); hipFree(w->hist_part);
+    hipFree(w->tp_m); hipFree(w->tp_sv); hipFree(w->tp_i); hipFree(w->tp_f);
     delete w;
     c->cut_ws = nullptr;
 }
@@ -731,20 +667,9 @@ static int kb_for(int k4) {
     return -1;
 }
 
-// kernel version: 2 = cut_argmax2_kernel (default), 1 = cut_argmax_kernel (TWOSD_CUT_V=1)
-static int cut_version() {
-    static const int v = getenv("TWOSD_CUT_V") ? atoi(getenv("TWOSD_CUT_V")) : 2;
-    return v == 1 ? 1 : 2;
-}
-
 template <int KB>
 static void launch_argmax_t(const CutParams &P, int nblocks, hipStream_t s) {
-    if (cut_version() == 2)
-        hipLaunchKernelGGL(cut_argmax2_kernel<KB>, dim3(nblocks), dim3(256), P.hist_lds ? sizeof(unsigned long long) * P.nv : 0,
-                           s, P);
-    else
-        hipLaunchKernelGGL(cut_argmax_kernel<KB>, dim3(nblocks), dim3(256), P.hist_lds ? sizeof(unsigned long long) * P.nv : 0,
-                           s, P);
+    hipLaunchKernelGGL(cut_argmax2_kernel<KB>, dim3(nblocks), dim3(256), P.hist_lds ? sizeof(unsigned long long) * P.nv : 0, s, P);
 }
 
 // resident blocks per CU of one instantiation (registers and LDS): the persistent grid is
@@ -753,11 +678,7 @@ static void launch_argmax_t(const CutParams &P, int nblocks, hipStream_t s) {
 template <int KB>
 static int argmax_occupancy_t(size_t dyn_lds) {
     int nb = 0;
-    if (cut_version() == 2) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cut_argmax2_kernel<KB>, 256, dyn_lds) != hipSuccess) nb = 0;
-    } else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cut_argmax_kernel<KB>, 256, dyn_lds) != hipSuccess) {
-        nb = 0;
-    }
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cut_argmax2_kernel<KB>, 256, dyn_lds) != hipSuccess) nb = 0;
     return nb;
 }
 
@@ -832,7 +753,7 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     const int N = E.count, k = c->k, m = c->L.m, nv = c->dvs.size, n1 = c->n1;
     const int k4 = (std::max(k, 1) + 3) & ~3;
     // v2 with the base row: k + 1 rows of the chunk
-    const bool base_row = cut_version() == 2 && TWOSD_CUT_BASEK;
+    const bool base_row = TWOSD_CUT_BASEK;
     const int KB = kb_for(base_row ? ((k + 1 + 3) & ~3) : k4);
     if (KB < 0) return fail(TWOSD_E_UNSUPPORTED, "k = %d random elements exceeds the cut kernel envelope (127)", k);
     int rc;
@@ -861,16 +782,41 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     }
     HIPCHK(hipMemcpyAsync(w->coef, coef.data(), sizeof(double) * k4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(w->bvec, bvec.data(), sizeof(double) * m, hipMemcpyHostToDevice, c->stream));
-    const int ntiles = (N + (cut_version() == 2 ? kCutTile2 : kCutTile) - 1) / (cut_version() == 2 ? kCutTile2 : kCutTile);
+    const int ntiles = (N + kCutTile2 - 1) / kCutTile2;
     // blocks per CU: resident occupancy of this instantiation (TWOSD_CUT_BPC overrides; the
     // |V| <= kHistLds case adds the LDS histogram, at most 2 KB)
     static const int bpc_env = getenv("TWOSD_CUT_BPC") ? atoi(getenv("TWOSD_CUT_BPC")) : 0;
     int bpc = bpc_env;
     if (bpc <= 0) bpc = argmax_occupancy(KB, sizeof(unsigned long long) * kHistLds);
     if (bpc <= 0) bpc = 2;
-    const int nblocks = std::max(1, std::min(ntiles, bpc * c->num_cus));
+    const int nchunks = (nv + kVT2 - 1) / kVT2;
+    // The persistent grid runs whole tiles round after round; the tiles past the last full
+    // round are cut into S vertex ranges (at least 4 chunks each) so that the last round is as
+    // full as the others.  S minimises the tail's length ceil(T S / B) / S in tile durations.
+    const int B = bpc * c->num_cus;
+    int full = ntiles, S = 1;
+    const bool tail_split = !getenv("TWOSD_CUT_TAIL") || atoi(getenv("TWOSD_CUT_TAIL")) != 0;   // A/B knob
+    if (tail_split && nchunks >= 8) {
+        const int T = ntiles % B;
+        double best = 1.0;
+        for (int s_ = 2; T > 0 && s_ <= std::min(64, nchunks / 4); ++s_) {
+            const double cost = (double)(((long long)T * s_ + B - 1) / B) / s_;
+            if (cost < best - 1e-9) { best = cost; S = s_; }
+        }
+        if (S > 1) full = ntiles - T;
+    }
+    const int nunits = full + (ntiles - full) * S;
+    const int nblocks = std::max(1, std::min(nunits, B));
     const int fix_blocks = std::max(1, std::min((N + 3) / 4, c->num_cus));
-    const size_t slots = (size_t)nblocks * 4 + (size_t)fix_blocks * 4;
+    const int ntail = S > 1 ? N - full * kCutTile2 : 0;
+    const int merge_blocks = ntail > 0 ? std::max(1, std::min((ntail + 3) / 4, c->num_cus)) : 0;
+    const size_t slots = (size_t)nblocks * 4 + (size_t)fix_blocks * 4 + (size_t)merge_blocks * 4;
+    if ((size_t)ntail * S > w->tp_cap) {
+        if ((rc = realloc_dev(&w->tp_m, (size_t)ntail * S)) || (rc = realloc_dev(&w->tp_sv, (size_t)ntail * S)) ||
+            (rc = realloc_dev(&w->tp_i, (size_t)ntail * S)) || (rc = realloc_dev(&w->tp_f, (size_t)ntail * S)))
+            return rc;
+        w->tp_cap = (size_t)ntail * S;
+    }
     if (slots * (k + 1) > w->part_cap) {
         if ((rc = realloc_dev(&w->partial, slots * (k + 1)))) return rc;
         w->part_cap = slots * (k + 1);
@@ -889,7 +835,7 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     P.hist_part = w->hist_part;
     P.tie_rel = tie_rel; P.inv_total = 1.0 / total_weight;
     P.dv = E.d_dv; P.w = E.d_w; P.coef = w->coef; P.PK = w->PK; P.PKT = w->PKT; P.base = w->base;
-    if (cut_version() == 2) {
+    {
         const int vcap32 = (nv + 31) & ~31, rows = 4 * KB;
         if ((size_t)rows * vcap32 > w->pktc_cap) {
             if ((rc = realloc_dev(&w->PKTc, (size_t)rows * vcap32))) return rc;
@@ -902,10 +848,14 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
         P.vcap32 = vcap32;
     }
     P.arg = w->arg; P.val = w->val; P.flag = w->flag; P.hist = d_hist; P.partial = w->partial;
+    P.full_units = full; P.tail_S = S;
+    P.tp_m = w->tp_m; P.tp_sv = w->tp_sv; P.tp_i = w->tp_i; P.tp_f = w->tp_f;
     launch_argmax(KB, P, nblocks, c->stream);
     if (P.hist_lds)
         hipLaunchKernelGGL(cut_hist_reduce_kernel, dim3((nv + 255) / 256), dim3(256), 0, c->stream, nblocks, nv, w->hist_part,
                            d_hist);
+    if (merge_blocks)
+        hipLaunchKernelGGL(cut_tail_merge_kernel, dim3(merge_blocks), dim3(256), 0, c->stream, P, nblocks * 4 + fix_blocks * 4);
     hipLaunchKernelGGL(cut_fixup_kernel, dim3(fix_blocks), dim3(256), 0, c->stream, P, nblocks * 4);
     if ((size_t)(k + 1) * kReduceBlocks > w->part2_cap) {
         if ((rc = realloc_dev(&w->part2, (size_t)(k + 1) * kReduceBlocks))) return rc;

@@ -265,7 +265,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             const int r = lr.idx;
             STAMP(1)
             if (lr.key == 0.0) break;
-            if (K >= P.kmax) { status = TWOSD_LP_ITER_LIMIT; break; }
+            if (K >= P.kcap) { status = TWOSD_LP_ITER_LIMIT; break; }
             const double delta = lr.p0;
 
             // ---- 2. BTRAN: u = e_r' E_K..E_1 (u dense in LDS), rho = u' B0^{-1}
@@ -664,7 +664,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             h_wave_sync();
             STAMP(8)
         }
-        if (status == TWOSD_LP_OPTIMAL || pb == 0) break;
+        if (status == TWOSD_LP_OPTIMAL || pb == 0 || !P.retry) break;
         pb = 0;
         }   // attempt
 
@@ -681,8 +681,10 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             if (P.vkey) {
                 // key of the dual: pi_i = -d_{n+i} is the reduced cost of row i's slack, kept
                 // current in registers by every pivot (fixed E-row slacks included).  Components
-                // at or below 1e-9 (1 + max) are snapped to zero and the rest rounded to 24
-                // significant bits; the key is the order-independent sum of mix64(row, bits).
+                // at or below key_zero (1 + max) are snapped to zero -- the threshold of the exact
+                // recovery below (HPI_ZERO), so a component the recovered pi keeps also separates
+                // the keys -- and the rest rounded to 24 significant bits; the key is the
+                // order-independent sum of mix64(row, bits).
                 // Scenarios with equal keys have duals equal to ~2^-23 relative -- the same vertex
                 // up to rounding noise, so their exactly recovered pi push as equal vectors
                 // (16-bit rule, dual_set.jl:24-53).  A vertex split over two keys only costs one
@@ -694,7 +696,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                     if (j >= n && j < ncol) pm = fmax(pm, fabs(d[c]));
                 }
                 pm = wmax(pm);
-                const double zt = 1e-9 * (1.0 + pm);
+                const double zt = P.key_zero * (1.0 + pm);
                 unsigned long long h = 0;
 #pragma unroll
                 for (int c = 0; c < C; ++c) {
@@ -788,10 +790,13 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         }
         if (P.eo_K) {   // eta file of the solve (pool refresh composes B^{-1} = E_K..E_1 B_pb^{-1} from it)
             const int erow = P.pi_by_pos ? qpos : s;
-            int off = 0;
-            if (lane == 0 && status == TWOSD_LP_OPTIMAL) off = atomicAdd(P.eo_used, eoff);
-            off = __builtin_amdgcn_readfirstlane(__shfl(off, 0));
-            const bool ok = status == TWOSD_LP_OPTIMAL && off + eoff <= P.eo_cap;
+            // 64-bit claim counter: it keeps counting past the arena (a scenario that does not
+            // fit gets K = -1) but cannot wrap into a valid offset; eo_cap <= INT32_MAX
+            unsigned long long off64 = 0;
+            if (lane == 0 && status == TWOSD_LP_OPTIMAL) off64 = atomicAdd(P.eo_used, (unsigned long long)eoff);
+            off64 = __shfl(off64, 0);
+            const bool ok = status == TWOSD_LP_OPTIMAL && off64 + (unsigned long long)eoff <= (unsigned long long)P.eo_cap;
+            const int off = ok ? (int)off64 : 0;
             if (ok) {
                 for (int e = lane; e < eoff; e += 64) {
                     P.eo_eidx[off + e] = eidx[e];

@@ -36,6 +36,7 @@ struct twosd_ctx {
     hipEvent_t ev[8] = {};
     int num_cus = 256;
     int kmax_override = 0;
+    int train_kcap = 0;           // pivot cap of the refresh training solves (0: kmax)
     double t_us[5] = {0, 0, 0, 0, 0};   // LP kernel, dedup, cut partial, cut finalize, pool select
     // template
     bool has_template = false, has_basis = false;
@@ -137,7 +138,8 @@ struct twosd_ctx {
     size_t vkey_cap = 0, bkey_cap = 0;
     // eta-file output of a pool refresh (list positions x kmax / kmax + 1, shared entry arena)
     int *d_eo_pb = nullptr, *d_eo_K = nullptr, *d_eo_off = nullptr, *d_eo_etap = nullptr, *d_eo_etaoff = nullptr;
-    int *d_eo_eidx = nullptr, *d_eo_used = nullptr;
+    int *d_eo_eidx = nullptr;
+    unsigned long long *d_eo_used = nullptr;
     double *d_eo_evals = nullptr;
     size_t eo_rows = 0, eo_cap = 0;
     int eo_kmax = 0;
@@ -175,6 +177,7 @@ struct LpRun {
     bool want_head = false;       // final heads into c->d_head_out, rows by list position / scenario
     const int *d_list = nullptr;  // list mode: scenarios (indices into d_dv) to solve, no selection
     int nlist = 0;
+    int kcap = 0;                 // > 0: pivot cap below kmax, no retry from the primary basis (refresh training)
 };
 int run_lp_ex(twosd_ctx *c, const double *x, const double *d_dv, int N, const LpRun &o);
 // vkey.hip

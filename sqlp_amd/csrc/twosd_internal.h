@@ -25,6 +25,8 @@ constexpr int kQueueStride = 32;   // queue heads one 128-B line apart
 constexpr int kMaxQueueGroups = 64;
 struct HyperParams {
     int m, n, k, N, kmax, ecap;
+    int kcap;                                           // pivot cap (<= kmax; beyond: TWOSD_LP_ITER_LIMIT)
+    int retry;                                          // a pool start ending non-optimal is retried from pool[0]
     const int *colptr, *rowidx; const double *val;      // W CSC
     const double *q; const int8_t *btype;
     int wr_width;                                       // W by rows as row-ELL (columns ascending, width
@@ -60,6 +62,7 @@ struct HyperParams {
     // maintained slack reduced costs, 24 significant bits); with pi == y == nullptr the vertex
     // recovery is skipped
     unsigned long long *vkey;                           // N (nullable)
+    double key_zero;                                    // key components <= key_zero (1 + max) snap to 0
     int pi_by_pos;                                      // pi / head row = queue position instead of scenario
     // basis key (pool refresh): sum of mix64(j) over the basic columns of the optimal basis
     unsigned long long *bkey;                           // N (nullable)
@@ -68,7 +71,7 @@ struct HyperParams {
     // and the eta entries, appended at an atomically claimed offset of a shared arena
     int *eo_pb, *eo_K, *eo_off, *eo_etap, *eo_etaoff;   // nullable (eo_K == nullptr: off)
     int *eo_eidx; double *eo_evals;
-    int *eo_used; int eo_cap;
+    unsigned long long *eo_used; long long eo_cap;      // claim counter (64-bit); arena entries (<= INT32_MAX)
 };
 
 // ---- device pool build of a refresh (pool_gpu.hip) ---------------------------------

@@ -165,6 +165,17 @@ class SDContext:
         check(self.lib.twosd_pool_refresh(self.h, epi.index, ptr(_f64(x)), first, count, max_pool, C.byref(n)))
         return n.value
 
+    def set_refresh_kcap(self, kcap: int):
+        """Pivot cap of the refresh's training solves (0: none below kmax)."""
+        check(self.lib.twosd_set_refresh_kcap(self.h, int(kcap)))
+
+    def last_lp_iters(self, N):
+        """(pivots, status) of the first N scenarios of the last LP launch."""
+        it = np.zeros(N, dtype=np.int32)
+        st = np.zeros(N, dtype=np.int32)
+        check(self.lib.twosd_last_lp_iters(self.h, int(N), ptr(it), ptr(st)))
+        return it, st
+
     def last_refresh_ms(self):
         """[training solves, re-solves, host composition, upload, total] of the last refresh."""
         out = np.zeros(5)

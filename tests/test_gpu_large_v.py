@@ -79,3 +79,30 @@ def test_large_vertex_set_cut_ssn():
     ma = _check(ctx, x, V, vals, w, 1e-12)
     assert ma.max() >= 16384                            # picks among the added vertices
     _check(ctx, x, V, vals, w, 0.0)
+
+
+@pytest.mark.parametrize("name,N,nsrc", [("ssn", 100_000, 12000), ("storm", 70_000, 16384)])
+def test_tail_split_equals_whole_tiles(name, N, nsrc, monkeypatch):
+    """The last round of the cut's persistent grid cut into vertex ranges (cut_tail_merge_kernel)
+    decides every scenario as the whole-tile pass does: identical argmax, max_val, alpha/beta
+    (TWOSD_CUT_TAIL=0 turns the split off)."""
+    from sqlp_amd import smps, twosd
+    inst = I.load(name)
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    x = I.x_ev(name)
+    ctx.compute_basis(x, smps.mean_values(inst["sto"]))
+    V = twosd.sdDualVertexSet(ctx)
+    _, _, pis, st = ctx.solve_values(x, I.sample(name, nsrc, 3), want_pi=True)
+    V.push_batch(pis[st == 0])
+    assert len(V) >= 512
+    epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(epi, I.sample(name, N, 17), np.random.default_rng(2).uniform(0.5, 1.5, N))
+    res = []
+    for tail in ("1", "0"):
+        monkeypatch.setenv("TWOSD_CUT_TAIL", tail)
+        res.append(twosd._build_cut(epi, x, 1e-12, want_argmax=True))
+    (c1, mv1, ma1), (c0, mv0, ma0) = res
+    np.testing.assert_array_equal(ma1, ma0)
+    np.testing.assert_array_equal(mv1, mv0)
+    assert c1.alpha == pytest.approx(c0.alpha, rel=1e-13, abs=1e-13)
+    np.testing.assert_allclose(c1.beta, c0.beta, rtol=1e-13, atol=1e-13)

@@ -170,3 +170,37 @@ def test_pool_refresh_device_build_other_instances(monkeypatch, name, N, train, 
     assert ok.mean() > 0.95
     np.testing.assert_allclose(o_d[ok], o_ref[ok], rtol=1e-9, atol=1e-7)
     print(f"{name}: pool {P_d}, pivots {piv_d / N:.2f}")
+
+
+def test_refresh_failure_leaves_context_refusing(monkeypatch):
+    """A device pool build that fails after the live pool arrays were grown (injected here,
+    TWOSD_INJECT_FAIL=refresh_fill) leaves no pool pointing at stale arrays: the refresh raises,
+    every later solve is refused (TWOSD_E_STATE) until a basis is installed again, and then the
+    context solves as before."""
+    from sqlp_amd import smps, twosd
+    from sqlp_amd._lib import TwoSDError
+    inst = I.load("storm")
+    x = I.x_ev("storm")
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    mean = smps.mean_values(inst["sto"])
+    ctx.compute_basis(x, mean)
+    vals = I.sample("storm", 256, seed=3)
+    ref, _, _, st = ctx.solve_values(x, vals)
+    assert (st == 0).all()
+    tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(tr, I.sample("storm", 2048, seed=11))
+    monkeypatch.setenv("TWOSD_INJECT_FAIL", "refresh_fill")
+    with pytest.raises(TwoSDError) as e:
+        ctx.pool_refresh(tr, x, 0, 2048, 512)
+    assert e.value.code == -2
+    monkeypatch.delenv("TWOSD_INJECT_FAIL")
+    with pytest.raises(TwoSDError) as e:
+        ctx.solve_values(x, vals)
+    assert e.value.code == -3
+    ctx.compute_basis(x, mean)
+    obj, _, _, st = ctx.solve_values(x, vals)
+    assert (st == 0).all()
+    np.testing.assert_array_equal(obj, ref)
+    assert ctx.pool_refresh(tr, x, 0, 2048, 512) > 1        # and refreshes again
+    obj, _, _, st = ctx.solve_values(x, vals)
+    np.testing.assert_allclose(obj, ref, rtol=1e-9, atol=1e-9)

@@ -70,3 +70,59 @@ def test_keyed_push_nonoptimal_refused():
     assert len(V) == 0
     twosd.solve_push(epi, x, 0, 2)
     assert len(V) >= 1 and ctx.last_push_reps() <= 2
+
+
+def _sd_candidate(name, iters, seed=11):
+    """x_candidate after `iters` sd_iteration! steps (host master + GPU hot path) from x_EV: a
+    first-stage point of the kind the bench times, away from where any pool was trained."""
+    from sqlp_amd import master, smps, twosd
+    inst = I.load(name)
+    sp1 = smps.get_smps_stage_template(inst["cor"], inst["tim"], 1)
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    x0 = I.x_ev(name)
+    ctx.compute_basis(x0, smps.mean_values(inst["sto"]))
+    cell = master.sdCell(sp1, ctx)
+    cell.bind_epigraph(twosd.sdEpigraph(ctx, 1.0, 0.0))
+    cell.x_candidate = x0.copy()
+    cell.x_incumbent = x0.copy()
+    for it in range(iters):
+        master.sd_iteration(cell, [I.sample(name, 1, seed + it)[0]])
+    x = cell.x_candidate.copy()
+    ctx.close()
+    return x
+
+
+def test_keyed_push_equals_push_all_at_scale(monkeypatch):
+    """The keyed push at bench scale: storm, 262,144 scenarios, at an SD candidate (not x_EV),
+    from a 4096-basis pool refreshed at that x (as every timed bench step): the ordered vertex
+    set is bit-identical to pushing every scenario's pi (dual_set.jl:84-94)."""
+    from sqlp_amd import smps, twosd
+    inst = I.load("storm")
+    x = _sd_candidate("storm", 4)
+    assert np.linalg.norm(x - I.x_ev("storm")) > 1e-3 * np.linalg.norm(I.x_ev("storm"))
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    ctx.compute_basis(I.x_ev("storm"), smps.mean_values(inst["sto"]))
+    ctx.set_distributions(inst["sto"])
+    tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_sampled_scenarios(tr, 16384, 4242)
+    ctx.pool_refresh(tr, x, 0, 16384, 4096)
+    assert ctx.pool_size() > 1000
+    N = 262144
+    epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_sampled_scenarios(epi, N, 777)
+    V = twosd.sdDualVertexSet(ctx)
+    runs = []
+    for mode in (None, "1"):
+        if mode:
+            monkeypatch.setenv("TWOSD_PUSH_ALL", mode)
+        else:
+            monkeypatch.delenv("TWOSD_PUSH_ALL", raising=False)
+        V.clear()
+        obj, st, ns = twosd.solve_push(epi, x, 0, N)
+        assert (st == 0).all()
+        runs.append((obj, len(V), V.fingerprint(), ctx.last_push_reps()))
+    (o_key, n_key, f_key, r_key), (o_all, n_all, f_all, r_all) = runs
+    np.testing.assert_array_equal(o_key, o_all)
+    assert r_all == N and r_key < N // 4
+    assert (n_key, f_key) == (n_all, f_all), (n_key, n_all)
+    print(f"storm {N} at SD candidate 4: |V| = {n_key}, representatives re-solved {r_key}")
