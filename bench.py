@@ -105,7 +105,11 @@ def main():
     ap.add_argument("--refresh-train", type=int, default=0,
                     help="training scenarios of a pool refresh (0: 4 x the refresh pool)")
     ap.add_argument("--refresh-pool", type=int, default=0,
-                    help="pool size after a refresh (0: by the per-rank shard, 4096 per 1M scenarios, at least 512)")
+                    help="pool size after a refresh (0: 4096 per 1M scenarios of the refreshing ranks, at least 512)")
+    ap.add_argument("--refresh-dist", type=int, default=1,
+                    help="N > 1: 1 = the ranks split the refresh (each trains on 1/N of the training scenarios and "
+                         "composes its share of the pool, packs all-gathered: sqlp_amd.dist.refresh_sharded); "
+                         "0 = every rank refreshes alone from all training scenarios with a pool sized by its shard")
     ap.add_argument("--cpu-pool", type=int, default=128, help="bases of the pooled CPU baseline (0: off)")
     ap.add_argument("--pool", type=int, default=0,
                     help="warm-start basis pool size (1 = primary basis only; 0 = by the per-rank shard: "
@@ -241,15 +245,20 @@ def main():
     X = len(xs)
     # refresh size by the per-rank shard: the refresh is a fixed cost per step (training solves,
     # B^-1 composition, upload grow with the pool), so a smaller shard takes a smaller pool
+    # a distributed refresh builds one pool for all ranks, so it is sized by the whole batch
+    dist_refresh = world > 1 and args.refresh_dist == 1
     if args.refresh_pool <= 0:
-        args.refresh_pool = max(512, min(4096, int(4096 * n_local * E / 1_000_000) // 256 * 256))
+        scope = N if dist_refresh else n_local * E
+        args.refresh_pool = max(512, min(4096, int(4096 * scope / 1_000_000) // 256 * 256))
     if args.refresh_train <= 0:
         args.refresh_train = 4 * args.refresh_pool
-    # pool refresh training scenarios (stream seed + 4, identical on every rank)
+    # pool refresh training scenarios (stream seed + 4; every rank holds all of them, or with
+    # the distributed refresh its contiguous slice)
     rtr = None
+    t_lo, t_hi = sdist.shard_range(args.refresh_train, rank, world) if dist_refresh else (0, args.refresh_train)
     if args.refresh:
         rtr = twosd.sdEpigraph(ctx, 1.0, 0.0)
-        scenarios(rtr, 0, args.refresh_train, args.seed + 4)
+        scenarios(rtr, t_lo, t_hi, args.seed + 4)
     # the pool is not at any x point yet: the first step at every x pays its refresh (the
     # setup pool, if any, was built at x_EV from other training scenarios)
     pool_at = {"x": None}
@@ -260,6 +269,12 @@ def main():
         if rtr is None or (pool_at["x"] is not None and np.array_equal(pool_at["x"], xx)):
             return 0.0
         t0 = time.perf_counter()
+        if dist_refresh:
+            _, ms = sdist.refresh_sharded(ctx, rtr, xx, 0, t_hi - t_lo, args.refresh_pool, args.pool_level1,
+                                          args.pool_cands, device)
+            pool_at["x"] = xx.copy()
+            pool_at["last_ms"] = ms
+            return time.perf_counter() - t0
         ctx.pool_refresh(rtr, xx, 0, args.refresh_train, args.refresh_pool)
         t1 = time.perf_counter()
         if args.pool_level1 > 0 and ctx.pool_size() > args.pool_level1:
@@ -402,7 +417,8 @@ def main():
                                "LP solve + dual dedup + build_sasa_cut per step",
                    "instance": name, "scenarios": N, "epigraphs": E, "vertices": nv, "k": k, "m2": m,
                    "basis_pool": pool_size, "pool_build_s": round(t_pool, 3),
-                   "pool_refresh": ({"train": args.refresh_train, "pool": args.refresh_pool} if args.refresh else None),
+                   "pool_refresh": ({"train": args.refresh_train, "pool": args.refresh_pool,
+                                     "distributed": dist_refresh} if args.refresh else None),
                    "pool_selection": (f"two-level: {args.pool_level1} + {args.pool_cands} candidates"
                                       if args.pool_level1 > 0 and pool_size > args.pool_level1 else "flat"),
                    "x_points": X,

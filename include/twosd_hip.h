@@ -118,6 +118,33 @@ int twosd_pool_build_candidates(twosd_ctx *ctx, int epi, const double *x, int fi
 int twosd_pool_refresh(twosd_ctx *ctx, int epi, const double *x, int first, int count, int max_pool,
                        int *pool_size);
 int twosd_last_refresh_ms(twosd_ctx *ctx, double *ms5);
+
+/* Distributed refresh (one rank per GPU, the pool replicated; no reference counterpart: the
+ * reference is single-process).  The twosd_pool_refresh of all ranks' training scenarios, split:
+ *   1. twosd_refresh_train: solve this rank's training slice [first, first+count) of epi at x;
+ *      *n_bases = its distinct optimal bases; box_lo/box_hi[k] (nullable) = the slice's delta box.
+ *      twosd_refresh_train_bases: their 64-bit keys, counts and first scenarios (ascending).
+ *   2. the caller all-gathers (keys, counts, first scenarios) and selects, identically on every
+ *      rank, the max_pool - 1 most frequent bases (ties: first occurrence in rank order), each
+ *      owned by the rank of its first occurrence.
+ *   3. twosd_refresh_build_local: compose B^{-1} of the n_own bases this rank owns (its first
+ *      scenarios reps[], in selection order) into a pack of *pack_bytes bytes;
+ *      twosd_refresh_pack copies it to a caller DEVICE buffer for the all-gather.
+ *   4. twosd_refresh_assemble: from the G gathered packs (DEVICE, `stride` bytes apart, rank
+ *      order), the pool = primary + the sources order[0, R) (source ids: 1 + the rank-major
+ *      position of a base among all packs), with the union box_lo/box_hi[k] of the slices.
+ * Selection becomes flat; twosd_pool_candidate_picks / twosd_pool_set_candidates split the
+ * two-level candidate lists the same way (picks of each rank's slice, lists from all picks). */
+int twosd_refresh_train(twosd_ctx *ctx, int epi, const double *x, int first, int count, int *n_bases, double *box_lo,
+                        double *box_hi);
+int twosd_refresh_train_bases(twosd_ctx *ctx, uint64_t *keys, int *counts, int *reps);
+int twosd_refresh_build_local(twosd_ctx *ctx, int n_own, const int *reps, int64_t *pack_bytes);
+int twosd_refresh_pack(twosd_ctx *ctx, void *d_dst);
+int twosd_refresh_assemble(twosd_ctx *ctx, int G, const void *d_packs, int64_t stride, int R, const int *order,
+                           const double *box_lo, const double *box_hi, int *pool_size);
+int twosd_pool_candidate_picks(twosd_ctx *ctx, int epi, const double *x, int first, int count, int level1, int *p1,
+                               int *pf);
+int twosd_pool_set_candidates(twosd_ctx *ctx, int level1, int ncand, int n, const int *p1, const int *pf);
 int twosd_pool_size(twosd_ctx *ctx, int *size);
 int twosd_pool_get(twosd_ctx *ctx, int p, int *head);
 /* Pool basis each scenario of the last LP batch started from (first N of it; 0 = the
@@ -239,9 +266,11 @@ int twosd_last_lp_stats(twosd_ctx *ctx, int64_t *pivots_sum, int *pivots_max);
  * after a pool refresh: its training solves). */
 int twosd_last_lp_iters(twosd_ctx *ctx, int N, int *iters, int *status);
 
-/* Pivot cap of the training solves of twosd_pool_refresh (0: the kernel's kmax).  A training
- * scenario that needs more pivots drops out of the basis count instead of holding the launch:
- * one wavefront per scenario, so a launch lasts as long as its slowest scenario. */
+/* Pivot cap of the training solves of a pool refresh: > 0 explicit, 0 auto (default: 4 x the
+ * mean pivots of the last batch of >= 4096 scenarios, at least 32; none before such a batch),
+ * < 0 none (the kernel's kmax).  A training scenario that needs more pivots drops out of the
+ * basis count instead of holding the launch: one wavefront per scenario, so a launch lasts as
+ * long as its slowest scenario. */
 int twosd_set_refresh_kcap(twosd_ctx *ctx, int kcap);
 
 /* Executed fp64 row operations of the last LP batch: each is one fused multiply-add over

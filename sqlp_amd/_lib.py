@@ -70,6 +70,13 @@ SIGNATURES = [
     ("twosd_debug_stamps", I, [P, P, I]),
     ("twosd_last_lp_iters", I, [P, I, P, P]),
     ("twosd_set_refresh_kcap", I, [P, I]),
+    ("twosd_refresh_train", I, [P, I, P, I, I, P, P, P]),
+    ("twosd_refresh_train_bases", I, [P, P, P, P]),
+    ("twosd_refresh_build_local", I, [P, I, P, P]),
+    ("twosd_refresh_pack", I, [P, P]),
+    ("twosd_refresh_assemble", I, [P, I, P, C.c_int64, I, P, P, P, P]),
+    ("twosd_pool_candidate_picks", I, [P, I, P, I, I, I, P, P]),
+    ("twosd_pool_set_candidates", I, [P, I, I, I, P, P]),
 ]
 
 _lib = None

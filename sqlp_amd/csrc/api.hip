@@ -239,6 +239,10 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_eo_eidx); dfree(c->d_eo_evals); dfree(c->d_eo_used); c->eo_rows = c->eo_cap = 0; c->eo_kmax = 0;
     dfree(c->d_pg_ival); dfree(c->d_pg_irow); dfree(c->d_pg_ioff); dfree(c->d_pg_amax); dfree(c->d_pg_d0p); dfree(c->d_pg_cnt); dfree(c->d_pg_tot);
     dfree(c->d_pg_valid); dfree(c->d_pg_head0); dfree(c->d_pg_map); dfree(c->d_pg_off); dfree(c->d_pg_pos);
+    dfree(c->d_rt_pack); dfree(c->d_gs_heads); dfree(c->d_gs_cnt); dfree(c->d_gs_tot); dfree(c->d_gs_valid);
+    dfree(c->d_gs_irow); dfree(c->d_gs_ioff); dfree(c->d_gs_ival);
+    if (c->d_gs_seg) { hipFree(c->d_gs_seg); c->d_gs_seg = nullptr; c->gs_seg_cap = 0; }
+    c->rt_epi = -1; c->rt_nown = -1;
     c->has_template = c->has_basis = false;
 }
 
@@ -778,18 +782,20 @@ static const char *finish_composed(const twosd_ctx *c, PoolBasis &B) {
 }
 
 // Device build of the refreshed pool (pool_gpu.hip) from the eta files and heads of the
-// training solves (rows = training scenarios in c->d_eo_* / c->d_head_out; sel = the
-// representatives, also in c->d_refresh_sel): sources a = 0 (primary), a
-// = 1..R (scenario sel[a - 1]) are
-// composed column by column, checked, and the sources that passed are written in order as
-// pool[0..P) -- the arrays upload_pool + prepare_elements would produce.  Returns 1, with the
-// pool unchanged, when the LDS layouts do not fit or the primary fails the device checks (the
-// caller then composes on the host).
-static int refresh_build_device(twosd_ctx *c, const std::vector<int> &sel) {
-    const int R = (int)sel.size();
+// training solves (rows = training scenarios in c->d_eo_* / c->d_head_out; the representatives
+// in c->d_refresh_sel).  Two phases:
+//   pg_compute   sources a = 0 (primary), a = 1..R (eta-file row d_refresh_sel[a - 1]) composed
+//                column by column into an intermediate CSC and checked (d_pg_* arrays);
+//   pg_assemble  the sources listed in `order` that passed the checks become pool[0..P), in
+//                that order: the arrays upload_pool + prepare_elements would produce.
+// The single-GPU refresh runs both on one source table; the distributed refresh
+// (twosd_refresh_*) runs pg_compute on each rank's own representatives and pg_assemble on the
+// table all ranks gathered.
+
+// workspace + PgArgs of a compute over nsrc sources (the template and start-pool fields)
+static int pg_args(twosd_ctx *c, int nsrc, PgArgs &A) {
     const HostLP &L = c->L;
-    const int m = L.m, n = L.n, MP = c->MP, nsrc = R + 1;
-    if (!pg_supported(m, n, c->eo_kmax)) return 1;
+    const int m = L.m;
     int rc;
     if ((rc = dev_reserve(c, &c->d_pg_pos, (size_t)std::max(c->k, 1))) || (rc = dev_reserve(c, &c->d_pg_amax, (size_t)nsrc)) ||
         (rc = dev_reserve(c, &c->d_pg_cnt, (size_t)4 * nsrc * m)) || (rc = dev_reserve(c, &c->d_pg_tot, (size_t)5 * nsrc)) ||
@@ -799,8 +805,8 @@ static int refresh_build_device(twosd_ctx *c, const std::vector<int> &sel) {
     HIPCHK(hipMemcpyAsync(c->d_pg_head0, c->head0.data(), sizeof(int) * m, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->d_pg_d0p, c->d_d0, sizeof(double) * 64 * c->CH, hipMemcpyDeviceToDevice, c->stream));
     if (c->k) HIPCHK(hipMemcpyAsync(c->d_pg_pos, c->pos_row.data(), sizeof(int) * c->k, hipMemcpyHostToDevice, c->stream));
-    PgArgs A{};
-    A.m = m; A.n = n; A.MP = MP; A.CH = c->CH; A.R9 = c->R; A.k = c->k; A.kmax = c->eo_kmax;
+    A = PgArgs{};
+    A.m = m; A.n = L.n; A.MP = c->MP; A.CH = c->CH; A.R9 = c->R; A.k = c->k; A.kmax = c->eo_kmax;
     A.npool_old = (int)c->pool.size();
     A.colptr = c->d_colptr; A.rowidx = c->d_rowidx; A.val = c->d_val; A.q = c->d_q; A.btype = c->d_btype;
     A.pos_row = c->d_pg_pos;
@@ -813,14 +819,16 @@ static int refresh_build_device(twosd_ctx *c, const std::vector<int> &sel) {
     A.nzc = c->d_pg_cnt; A.keptc = c->d_pg_cnt + (size_t)nsrc * m;
     A.rowcnt = c->d_pg_cnt + (size_t)2 * nsrc * m; A.erowcnt = c->d_pg_cnt + (size_t)3 * nsrc * m;
     A.tot = c->d_pg_tot; A.nztot = c->d_pg_tot + (size_t)4 * nsrc; A.valid = c->d_pg_valid;
-    const bool dbg = getenv("TWOSD_DEBUG") != nullptr;
-    auto now = [&]() {
-        if (dbg) hipStreamSynchronize(c->stream);
-        return std::chrono::steady_clock::now();
-    };
-    const auto t0 = now();
+    return TWOSD_OK;
+}
+
+// compute phase over sources [0, nsrc): FTRAN passes + counts and checks; the per-source
+// totals (4 each), nonzero counts and validity are read back into h_tot / h_nz / h_valid
+// (pinned staging), the intermediate offsets prefixed into A.inter_off
+static int pg_compute(twosd_ctx *c, int nsrc, PgArgs &A, int **h_tot, int **h_valid, long long *inz_out, bool dbg) {
+    int rc;
+    if ((rc = pg_args(c, nsrc, A))) return rc;
     HIPCHK(pg_launch_ftran(A, 0, nsrc, c->stream));
-    // intermediate CSC offsets from the nonzero counts
     int *h_nz = stage_buf<int>(c, 11, (size_t)nsrc);
     long long *h_ioff = stage_buf<long long>(c, 12, (size_t)nsrc);
     if (!h_nz || !h_ioff) return fail(TWOSD_E_DEVICE, "pool refresh: pinned staging allocation failed");
@@ -834,22 +842,30 @@ static int refresh_build_device(twosd_ctx *c, const std::vector<int> &sel) {
     if ((rc = dev_reserve(c, &c->d_pg_irow, (size_t)inz)) || (rc = dev_reserve(c, &c->d_pg_ival, (size_t)inz))) return rc;
     HIPCHK(hipMemcpyAsync(c->d_pg_ioff, h_ioff, sizeof(long long) * nsrc, hipMemcpyHostToDevice, c->stream));
     A.inter_off = c->d_pg_ioff; A.inter_row = c->d_pg_irow; A.inter_val = c->d_pg_ival;
-    const auto t1 = now();
     HIPCHK(pg_launch_ftran(A, 1, nsrc, c->stream));
     HIPCHK(pg_launch_count(A, nsrc, c->stream));
-    const auto t2 = now();
-    int *h_tot = stage_buf<int>(c, 9, (size_t)5 * nsrc);
-    if (!h_tot) return fail(TWOSD_E_DEVICE, "pool refresh: pinned staging allocation failed");
-    int *h_valid = h_tot + (size_t)4 * nsrc;
-    HIPCHK(hipMemcpyAsync(h_tot, c->d_pg_tot, sizeof(int) * 4 * nsrc, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(h_valid, c->d_pg_valid, sizeof(int) * nsrc, hipMemcpyDeviceToHost, c->stream));
-
+    int *ht = stage_buf<int>(c, 9, (size_t)5 * nsrc);
+    if (!ht) return fail(TWOSD_E_DEVICE, "pool refresh: pinned staging allocation failed");
+    HIPCHK(hipMemcpyAsync(ht, c->d_pg_tot, sizeof(int) * 4 * nsrc, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(ht + (size_t)4 * nsrc, c->d_pg_valid, sizeof(int) * nsrc, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    if (!h_valid[0]) return 1;   // the primary basis failed the device checks: host path
-    // pool = the sources that passed, in order; offsets = prefix sums of their totals
+    if (dbg) fprintf(stderr, "pg_compute: %d sources, %lld intermediate entries\n", nsrc, inz);
+    *h_tot = ht;
+    *h_valid = ht + (size_t)4 * nsrc;
+    *inz_out = inz;
+    return TWOSD_OK;
+}
+
+// assemble phase: pool = the sources of `order` (order[0] = 0, the primary) that passed, in
+// order; A describes the source table (compute output or the gathered table)
+static int pg_assemble(twosd_ctx *c, PgArgs &A, const int *h_tot, const int *h_valid, const std::vector<int> &order) {
+    const HostLP &L = c->L;
+    const int m = L.m, MP = c->MP;
+    int rc;
+    if (order.empty() || order[0] != 0 || !h_valid[0]) return 1;   // the primary failed the device checks: host path
     std::vector<int> map, off;
     std::vector<int64_t> acc(4, 0);
-    for (int a = 0; a < nsrc; ++a) {
+    for (int a : order) {
         if (!h_valid[a]) continue;
         map.push_back(a);
         for (int f = 0; f < 4; ++f) {
@@ -893,20 +909,13 @@ static int refresh_build_device(twosd_ctx *c, const std::vector<int> &sel) {
     F.brptr = c->d_brptr; F.brcol = c->d_brcol; F.brval = c->d_brval; F.bcp = c->d_bcp; F.bci = c->d_bci; F.bcv = c->d_bcv;
     F.kp = c->d_kp; F.ke = c->d_ke; F.kraw = c->d_kraw; F.kslot = c->d_kslot; F.kix = c->d_kix; F.kv = c->d_kv;
     F.hb0 = c->d_hb0; F.basic0 = c->d_basic0; F.bnnz = c->d_bnnz; F.d0 = c->d_d0; F.sel_ptr = c->d_sel_ptr;
-    A.a0 = 0;
     F.P0 = 0;
-    const auto t3 = now();
     if (pg_launch_fill(A, F, P, c->stream) != hipSuccess) return broken(fail(TWOSD_E_DEVICE, "pool refresh: fill launch failed"));
     int *h_hb = stage_buf<int>(c, 10, (size_t)P * MP);   // the pool's heads, from hb0 = 4 head + type
     if (!h_hb) return broken(fail(TWOSD_E_DEVICE, "pool refresh: pinned staging allocation failed"));
     if (hipMemcpyAsync(h_hb, c->d_hb0, sizeof(int) * P * MP, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
         return broken(fail(TWOSD_E_DEVICE, "pool refresh: reading the built pool heads failed"));
-    if (dbg) {
-        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        fprintf(stderr, "refresh_build_device: %d sources, ftran-0 %.2f, ftran-1+count %.2f, offsets %.2f, fill %.2f ms (%lld intermediate)\n", nsrc, ms(t0, t1),
-                ms(t1, t2), ms(t2, t3), ms(t3, std::chrono::steady_clock::now()), inz);
-    }
     // host pool: the primary keeps its host forms; the new bases carry their heads
     std::vector<PoolBasis> keep;
     keep.reserve(P);
@@ -925,6 +934,33 @@ static int refresh_build_device(twosd_ctx *c, const std::vector<int> &sel) {
     c->k_valid = true;
     c->pool_l1 = c->pool_ncand = 0;
     return TWOSD_OK;
+}
+
+// Returns 1, with the pool unchanged, when the LDS layouts do not fit or the primary fails the
+// device checks (the caller then composes on the host).
+static int refresh_build_device(twosd_ctx *c, const std::vector<int> &sel) {
+    const int R = (int)sel.size();
+    if (!pg_supported(c->L.m, c->L.n, c->eo_kmax)) return 1;
+    const bool dbg = getenv("TWOSD_DEBUG") != nullptr;
+    PgArgs A;
+    int *h_tot = nullptr, *h_valid = nullptr;
+    long long inz = 0;
+    int rc;
+    if ((rc = pg_compute(c, R + 1, A, &h_tot, &h_valid, &inz, dbg))) return rc;
+    std::vector<int> order(R + 1);
+    for (int a = 0; a <= R; ++a) order[a] = a;
+    return pg_assemble(c, A, h_tot, h_valid, order);
+}
+
+// pivot cap of the training solves of a refresh.  One wavefront solves one scenario, so a
+// training launch lasts as long as its slowest scenario; the scenarios far from the current
+// pool (tens of pivots) mostly end at rare bases.  Auto: 4 x the mean pivots of the last large
+// batch, at least 32 (storm: 32-44; ssn, ~33 pivots a solve: ~130); none before any batch.
+static int train_kcap(const twosd_ctx *c) {
+    if (const char *e = getenv("TWOSD_TRAIN_KCAP")) return atoi(e);   // A/B knob
+    if (c->train_kcap > 0) return c->train_kcap;
+    if (c->train_kcap < 0 || c->piv_mean_ref <= 0.0) return 0;
+    return std::max(32, (int)std::ceil(4.0 * c->piv_mean_ref));
 }
 
 extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int first, int count, int max_pool,
@@ -947,8 +983,7 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
     o.want_head = true;
     // training scenarios beyond the pivot cap only drop out of the basis count (one launch
     // lasts as long as its slowest scenario: with one scenario per wave the cap bounds it)
-    o.kcap = c->train_kcap;
-    if (const char *e = getenv("TWOSD_TRAIN_KCAP")) o.kcap = atoi(e);   // A/B knob
+    o.kcap = train_kcap(c);
     if ((rc = run_lp_ex(c, x, d_dv, count, o))) return rc;
     const auto t1 = std::chrono::steady_clock::now();
     // 2. distinct optimal bases, most frequent first (ties: first occurrence), primary excluded
@@ -1069,6 +1104,293 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
     return TWOSD_OK;
 }
 
+// ---- distributed pool refresh -------------------------------------------------------------
+// The refresh of twosd_pool_refresh split over the ranks (one process per GPU, the pool
+// replicated): each rank solves its slice of the training scenarios (twosd_refresh_train), the
+// ranks exchange the distinct optimal bases with their counts and pick the same most frequent
+// max_pool - 1 (the caller's selection, sqlp_amd/dist.py), each rank composes the B^{-1} of the
+// picked bases whose first occurrence it holds (twosd_refresh_build_local -> a pack of the
+// intermediate CSC, counts and heads), the packs are all-gathered, and every rank assembles the
+// same pool from the gathered table (twosd_refresh_assemble).  With the training scenarios
+// split contiguously the pool equals the single-rank refresh of all of them, bit for bit.
+
+// pack: 8-byte aligned sections of n sources with nz intermediate entries
+struct RtPack {
+    size_t heads, cnt, tot, nztot, valid, irow, ival, bytes;
+};
+static inline size_t al8(size_t b) { return (b + 7) & ~(size_t)7; }
+static RtPack rt_layout(long long n, long long nz, int m) {
+    RtPack L{};
+    size_t o = 32;   // header: n, nz, bytes, m (int64)
+    L.heads = o; o = al8(o + sizeof(int) * (size_t)n * m);
+    L.cnt = o; o = al8(o + sizeof(int) * 4 * (size_t)n * m);
+    L.tot = o; o = al8(o + sizeof(int) * 4 * (size_t)n);
+    L.nztot = o; o = al8(o + sizeof(int) * (size_t)n);
+    L.valid = o; o = al8(o + sizeof(int) * (size_t)n);
+    L.irow = o; o = al8(o + sizeof(int) * (size_t)nz);
+    L.ival = o; o = al8(o + sizeof(double) * (size_t)nz);
+    L.bytes = o;
+    return L;
+}
+
+// rows src_row[j] of the training heads -> out row j
+__global__ void rt_heads_kernel(int n, int m, const int *__restrict__ heads, const int *__restrict__ src_row, int *__restrict__ out) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)n * m; i += (size_t)gridDim.x * blockDim.x)
+        out[i] = heads[(size_t)src_row[i / m] * m + i % m];
+}
+
+// batched copy: segment blockIdx.y = (src, dst, 4-byte words)
+struct CopySeg { const int *src; int *dst; long long words; };
+__global__ void rt_copy_kernel(const CopySeg *__restrict__ seg) {
+    const CopySeg S = seg[blockIdx.y];
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < S.words; i += (long long)gridDim.x * blockDim.x)
+        S.dst[i] = S.src[i];
+}
+static int rt_copy(twosd_ctx *c, const std::vector<CopySeg> &segs) {
+    if (segs.empty()) return TWOSD_OK;
+    CopySeg *h = stage_buf<CopySeg>(c, 13, segs.size());
+    if (!h) return fail(TWOSD_E_DEVICE, "refresh: pinned staging allocation failed");
+    std::copy(segs.begin(), segs.end(), h);
+    if (!c->d_gs_seg || c->gs_seg_cap < segs.size()) {
+        if (c->d_gs_seg) hipFree(c->d_gs_seg);
+        c->d_gs_seg = nullptr;
+        c->gs_seg_cap = 0;
+        HIPCHK(hipMalloc(&c->d_gs_seg, sizeof(CopySeg) * std::max<size_t>(segs.size(), 64)));
+        c->gs_seg_cap = std::max<size_t>(segs.size(), 64);
+    }
+    HIPCHK(hipMemcpyAsync(c->d_gs_seg, h, sizeof(CopySeg) * segs.size(), hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(rt_copy_kernel, dim3(64, (unsigned)segs.size()), dim3(256), 0, c->stream, (const CopySeg *)c->d_gs_seg);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));   // the staging buffer is reused by the next call
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_refresh_train(twosd_ctx *c, int epi, const double *x, int first, int count, int *n_bases,
+                                   double *box_lo, double *box_hi) {
+    if (!c || !c->has_basis) return fail(TWOSD_E_STATE, "refresh_train: no primary basis");
+    if (epi < 0 || epi >= (int)c->epis.size()) return fail(TWOSD_E_ARG, "refresh_train: epigraph %d does not exist", epi);
+    const EpiDevice &E = c->epis[epi];
+    if (first < 0 || count < 1 || first + count > E.count || (c->n1 > 0 && !x) || !n_bases)
+        return fail(TWOSD_E_ARG, "refresh_train: bad arguments");
+    if (c->CH <= 0) return fail(TWOSD_E_UNSUPPORTED, "refresh_train: needs the hypersparse LP kernel");
+    HIPCHK(hipSetDevice(c->device));
+    const auto t0 = std::chrono::steady_clock::now();
+    const double *d_dv = E.d_dv + (size_t)first * c->k;
+    int rc;
+    LpRun o;   // as twosd_pool_refresh step 1
+    o.want_bkey = true;
+    o.want_etas = true;
+    o.want_head = true;
+    o.kcap = train_kcap(c);
+    if ((rc = run_lp_ex(c, x, d_dv, count, o))) return rc;
+    const auto t1 = std::chrono::steady_clock::now();
+    const int *d_list = nullptr, *d_counts = nullptr;
+    int U = 0;
+    if ((rc = vkey_first_occurrences(c, count, c->d_bkey, c->d_status, &d_list, &U, &d_counts))) return rc;
+    c->rt_reps.resize(U);
+    c->rt_counts.resize(U);
+    c->rt_keys.resize(U);
+    std::vector<unsigned long long> bk(count);
+    if (U > 0) {
+        HIPCHK(hipMemcpy(c->rt_reps.data(), d_list, sizeof(int) * U, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(c->rt_counts.data(), d_counts, sizeof(int) * U, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(bk.data(), c->d_bkey, sizeof(unsigned long long) * count, hipMemcpyDeviceToHost));
+        for (int a = 0; a < U; ++a) c->rt_keys[a] = bk[c->rt_reps[a]];
+    }
+    // training box of the slice (cached per training range, as the single-rank refresh)
+    if (c->k > 0 && !(c->rt_epi == epi && c->rt_first == first && c->rt_count == count && c->rt_n == E.count)) {
+        std::vector<double> dv((size_t)count * c->k);
+        HIPCHK(hipMemcpy(dv.data(), d_dv, sizeof(double) * dv.size(), hipMemcpyDeviceToHost));
+        c->rt_lo.assign(c->k, INFINITY);
+        c->rt_hi.assign(c->k, -INFINITY);
+        for (int s2 = 0; s2 < count; ++s2)
+            for (int e = 0; e < c->k; ++e) {
+                c->rt_lo[e] = std::min(c->rt_lo[e], dv[(size_t)s2 * c->k + e]);
+                c->rt_hi[e] = std::max(c->rt_hi[e], dv[(size_t)s2 * c->k + e]);
+            }
+        c->rt_epi = epi; c->rt_first = first; c->rt_count = count; c->rt_n = E.count;
+    }
+    if (box_lo) std::copy(c->rt_lo.begin(), c->rt_lo.end(), box_lo);
+    if (box_hi) std::copy(c->rt_hi.begin(), c->rt_hi.end(), box_hi);
+    c->rt_nown = -1;
+    c->last_refresh_ms[0] = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    c->last_refresh_ms[1] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+    *n_bases = U;
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_refresh_train_bases(twosd_ctx *c, uint64_t *keys, int *counts, int *reps) {
+    if (!c || c->rt_epi < 0) return fail(TWOSD_E_STATE, "refresh_train_bases: no training solve (twosd_refresh_train)");
+    const size_t U = c->rt_keys.size();
+    if (keys) std::copy(c->rt_keys.begin(), c->rt_keys.end(), keys);
+    if (counts) std::copy(c->rt_counts.begin(), c->rt_counts.end(), counts);
+    if (reps) std::copy(c->rt_reps.begin(), c->rt_reps.begin() + U, reps);
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_refresh_build_local(twosd_ctx *c, int n_own, const int *reps, int64_t *pack_bytes) {
+    if (!c || c->rt_epi < 0) return fail(TWOSD_E_STATE, "refresh_build_local: no training solve (twosd_refresh_train)");
+    if (n_own < 0 || (n_own > 0 && !reps) || !pack_bytes) return fail(TWOSD_E_ARG, "refresh_build_local: bad arguments");
+    for (int j = 0; j < n_own; ++j)
+        if (reps[j] < 0 || reps[j] >= c->rt_count) return fail(TWOSD_E_ARG, "refresh_build_local: representative %d outside the slice", reps[j]);
+    if (!pg_supported(c->L.m, c->L.n, c->eo_kmax))
+        return fail(TWOSD_E_UNSUPPORTED, "refresh_build_local: the device pool build does not fit this template");
+    HIPCHK(hipSetDevice(c->device));
+    const auto t0 = std::chrono::steady_clock::now();
+    const int m = c->L.m;
+    int rc;
+    if ((size_t)std::max(n_own, 1) > c->refresh_sel_cap) {
+        if ((rc = dalloc(&c->d_refresh_sel, (size_t)std::max(n_own, 1)))) return rc;
+        c->refresh_sel_cap = std::max(n_own, 1);
+    }
+    if (n_own) HIPCHK(hipMemcpyAsync(c->d_refresh_sel, reps, sizeof(int) * n_own, hipMemcpyHostToDevice, c->stream));
+    PgArgs A;
+    int *h_tot = nullptr, *h_valid = nullptr;
+    long long inz = 0;
+    const int nsrc = n_own + 1;
+    if ((rc = pg_compute(c, nsrc, A, &h_tot, &h_valid, &inz, getenv("TWOSD_DEBUG") != nullptr))) return rc;
+    const long long *h_ioff = static_cast<const long long *>(c->stage[12]);
+    const long long nz0 = n_own ? h_ioff[1] : inz;
+    const RtPack L = rt_layout(n_own, inz - nz0, m);
+    if ((rc = dev_reserve(c, &c->d_rt_pack, L.bytes))) return rc;
+    long long *hdr = stage_buf<long long>(c, 14, 4);
+    if (!hdr) return fail(TWOSD_E_DEVICE, "refresh: pinned staging allocation failed");
+    hdr[0] = n_own; hdr[1] = inz - nz0; hdr[2] = (long long)L.bytes; hdr[3] = m;
+    HIPCHK(hipMemcpyAsync(c->d_rt_pack, hdr, 32, hipMemcpyHostToDevice, c->stream));
+    char *P = c->d_rt_pack;
+    if (n_own) {
+        hipLaunchKernelGGL(rt_heads_kernel, dim3(std::min(1024, (n_own * m + 255) / 256)), dim3(256), 0, c->stream, n_own, m,
+                           c->d_head_out, c->d_refresh_sel, reinterpret_cast<int *>(P + L.heads));
+        HIPCHK(hipGetLastError());
+    }
+    std::vector<CopySeg> seg;
+    auto add = [&](const void *src, void *dst, size_t bytes) {
+        if (bytes) seg.push_back({static_cast<const int *>(src), static_cast<int *>(dst), (long long)(bytes / 4)});
+    };
+    const size_t nm = (size_t)n_own * m;
+    for (int f = 0; f < 4; ++f)   // nzc, keptc, rowcnt, erowcnt: rows 1..n_own of each
+        add(c->d_pg_cnt + (size_t)f * nsrc * m + m, P + L.cnt + sizeof(int) * f * nm, sizeof(int) * nm);
+    add(c->d_pg_tot + 4, P + L.tot, sizeof(int) * 4 * n_own);
+    add(c->d_pg_tot + (size_t)4 * nsrc + 1, P + L.nztot, sizeof(int) * n_own);
+    add(c->d_pg_valid + 1, P + L.valid, sizeof(int) * n_own);
+    add(c->d_pg_irow + nz0, P + L.irow, sizeof(int) * (inz - nz0));
+    add(c->d_pg_ival + nz0, P + L.ival, sizeof(double) * (inz - nz0));
+    if ((rc = rt_copy(c, seg))) return rc;
+    c->rt_nz0 = nz0;
+    c->rt_nsrc_local = nsrc;
+    c->rt_nown = n_own;
+    c->last_refresh_ms[2] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    *pack_bytes = (int64_t)L.bytes;
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_refresh_pack(twosd_ctx *c, void *d_dst) {
+    if (!c || c->rt_nown < 0 || !d_dst) return fail(TWOSD_E_STATE, "refresh_pack: no local build (twosd_refresh_build_local)");
+    HIPCHK(hipSetDevice(c->device));
+    const RtPack L = rt_layout(c->rt_nown, 0, c->L.m);
+    long long bytes = 0;
+    HIPCHK(hipMemcpy(&bytes, c->d_rt_pack + 16, sizeof(bytes), hipMemcpyDeviceToHost));
+    (void)L;
+    HIPCHK(hipMemcpyAsync(d_dst, c->d_rt_pack, (size_t)bytes, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_refresh_assemble(twosd_ctx *c, int G, const void *d_packs, int64_t stride, int R, const int *order,
+                                      const double *box_lo, const double *box_hi, int *pool_size) {
+    if (!c || c->rt_nown < 0) return fail(TWOSD_E_STATE, "refresh_assemble: no local build (twosd_refresh_build_local)");
+    if (G < 1 || !d_packs || stride < 32 || (stride & 7) || R < 0 || (R > 0 && !order) || (c->k > 0 && (!box_lo || !box_hi)))
+        return fail(TWOSD_E_ARG, "refresh_assemble: bad arguments");
+    HIPCHK(hipSetDevice(c->device));
+    const auto t0 = std::chrono::steady_clock::now();
+    const int m = c->L.m;
+    int rc;
+    const char *packs = static_cast<const char *>(d_packs);
+    std::vector<long long> hdr((size_t)4 * G);
+    HIPCHK(hipMemcpy2D(hdr.data(), 32, packs, (size_t)stride, 32, G, hipMemcpyDeviceToHost));
+    std::vector<long long> an(G + 1, 1), zn(G + 1, c->rt_nz0);
+    for (int r = 0; r < G; ++r) {
+        if (hdr[4 * r] < 0 || hdr[4 * r + 3] != m || hdr[4 * r + 2] > stride)
+            return fail(TWOSD_E_ARG, "refresh_assemble: pack %d is not a pack of this template", r);
+        an[r + 1] = an[r] + hdr[4 * r];
+        zn[r + 1] = zn[r] + hdr[4 * r + 1];
+    }
+    const long long nsrc = an[G], nzg = zn[G];
+    if (nsrc > INT32_MAX / std::max(m, 1)) return fail(TWOSD_E_UNSUPPORTED, "refresh_assemble: too many sources");
+    for (int i = 0; i < R; ++i)
+        if (order[i] < 1 || order[i] >= nsrc) return fail(TWOSD_E_ARG, "refresh_assemble: source %d outside [1, %lld)", order[i], nsrc);
+    if ((rc = dev_reserve(c, &c->d_gs_heads, (size_t)std::max<long long>(nsrc - 1, 1) * m)) ||
+        (rc = dev_reserve(c, &c->d_gs_cnt, (size_t)4 * nsrc * m)) || (rc = dev_reserve(c, &c->d_gs_tot, (size_t)5 * nsrc)) ||
+        (rc = dev_reserve(c, &c->d_gs_valid, (size_t)nsrc)) || (rc = dev_reserve(c, &c->d_gs_ioff, (size_t)nsrc)) ||
+        (rc = dev_reserve(c, &c->d_gs_irow, (size_t)nzg)) || (rc = dev_reserve(c, &c->d_gs_ival, (size_t)nzg)))
+        return rc;
+    // the table: source 0 = this rank's primary (local compute row 0), then every rank's pack
+    std::vector<CopySeg> seg;
+    auto add = [&](const void *src, void *dst, size_t bytes) {
+        if (bytes) seg.push_back({static_cast<const int *>(src), static_cast<int *>(dst), (long long)(bytes / 4)});
+    };
+    const size_t nl = (size_t)c->rt_nsrc_local;
+    for (int f = 0; f < 4; ++f) add(c->d_pg_cnt + f * nl * m, c->d_gs_cnt + (size_t)f * nsrc * m, sizeof(int) * m);
+    add(c->d_pg_tot, c->d_gs_tot, sizeof(int) * 4);
+    add(c->d_pg_tot + 4 * nl, c->d_gs_tot + 4 * nsrc, sizeof(int));
+    add(c->d_pg_valid, c->d_gs_valid, sizeof(int));
+    add(c->d_pg_irow, c->d_gs_irow, sizeof(int) * c->rt_nz0);
+    add(c->d_pg_ival, c->d_gs_ival, sizeof(double) * c->rt_nz0);
+    for (int r = 0; r < G; ++r) {
+        const long long n = hdr[4 * r], nz = hdr[4 * r + 1], a = an[r];
+        const RtPack L = rt_layout(n, nz, m);
+        const char *P = packs + (size_t)r * stride;
+        const size_t nm = (size_t)n * m;
+        add(P + L.heads, c->d_gs_heads + (size_t)(a - 1) * m, sizeof(int) * nm);
+        for (int f = 0; f < 4; ++f) add(P + L.cnt + sizeof(int) * f * nm, c->d_gs_cnt + (size_t)f * nsrc * m + (size_t)a * m, sizeof(int) * nm);
+        add(P + L.tot, c->d_gs_tot + 4 * a, sizeof(int) * 4 * n);
+        add(P + L.nztot, c->d_gs_tot + 4 * nsrc + a, sizeof(int) * n);
+        add(P + L.valid, c->d_gs_valid + a, sizeof(int) * n);
+        add(P + L.irow, c->d_gs_irow + zn[r], sizeof(int) * nz);
+        add(P + L.ival, c->d_gs_ival + zn[r], sizeof(double) * nz);
+    }
+    if ((rc = rt_copy(c, seg))) return rc;
+    int *h_tot = stage_buf<int>(c, 9, (size_t)6 * nsrc);
+    long long *h_ioff = stage_buf<long long>(c, 12, (size_t)nsrc);
+    if (!h_tot || !h_ioff) return fail(TWOSD_E_DEVICE, "refresh: pinned staging allocation failed");
+    int *h_nz = h_tot + 4 * nsrc, *h_valid = h_tot + 5 * nsrc;
+    HIPCHK(hipMemcpyAsync(h_tot, c->d_gs_tot, sizeof(int) * 5 * nsrc, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(h_valid, c->d_gs_valid, sizeof(int) * nsrc, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    long long z = 0;
+    for (long long a = 0; a < nsrc; ++a) {
+        h_ioff[a] = z;
+        z += h_nz[a];
+    }
+    if (z != nzg) return fail(TWOSD_E_ARG, "refresh_assemble: packs inconsistent (%lld vs %lld entries)", z, nzg);
+    HIPCHK(hipMemcpyAsync(c->d_gs_ioff, h_ioff, sizeof(long long) * nsrc, hipMemcpyHostToDevice, c->stream));
+    // source table of the gathered build (template fields as the local compute)
+    PgArgs A;
+    if ((rc = pg_args(c, c->rt_nsrc_local, A))) return rc;
+    A.nzc = c->d_gs_cnt; A.keptc = c->d_gs_cnt + (size_t)nsrc * m;
+    A.rowcnt = c->d_gs_cnt + (size_t)2 * nsrc * m; A.erowcnt = c->d_gs_cnt + (size_t)3 * nsrc * m;
+    A.tot = c->d_gs_tot; A.nztot = c->d_gs_tot + 4 * nsrc; A.valid = c->d_gs_valid;
+    A.inter_off = c->d_gs_ioff; A.inter_row = c->d_gs_irow; A.inter_val = c->d_gs_ival;
+    A.gheads = c->d_gs_heads;
+    std::vector<int> ord(R + 1);
+    ord[0] = 0;
+    std::copy(order, order + R, ord.begin() + 1);
+    if ((rc = pg_assemble(c, A, h_tot, h_valid, ord)) != 0)
+        return rc < 0 ? rc : fail(TWOSD_E_STATE, "refresh_assemble: the primary basis failed the device checks");
+    // selection box: the union of the ranks' training boxes
+    if (c->k > 0) {
+        c->sel_lo.assign(box_lo, box_lo + c->k);
+        c->sel_hi.assign(box_hi, box_hi + c->k);
+        c->box_epi = -1;   // not the single-rank cache
+    }
+    c->rt_nown = -1;
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c->last_refresh_ms[3] = ms;
+    c->last_refresh_ms[4] = c->last_refresh_ms[0] + c->last_refresh_ms[1] + c->last_refresh_ms[2] + ms;
+    if (pool_size) *pool_size = (int)c->pool.size();
+    return TWOSD_OK;
+}
+
 extern "C" int twosd_last_refresh_ms(twosd_ctx *c, double *ms5) {
     if (!c || !ms5) return fail(TWOSD_E_ARG, "last_refresh_ms: NULL");
     for (int i = 0; i < 5; ++i) ms5[i] = c->last_refresh_ms[i];
@@ -1080,6 +1402,79 @@ extern "C" int twosd_last_refresh_ms(twosd_ctx *c, double *ms5) {
 // level 1 = pool[0, level1) (the most frequent bases); the candidates of a level-1 basis p are
 // the ncand bases that the flat selection over the whole pool picks most often for training
 // scenarios whose level-1 pick is p (ties: lower index).  level1 = 0 back to flat selection.
+// flat and level-1 picks of training scenarios [first, first + count) of epi at x
+static int candidate_picks(twosd_ctx *c, const EpiDevice &E, const double *x, int first, int count, int level1,
+                           int *p1, int *pf) {
+    int rc;
+    if ((rc = prepare_x(c, x))) return rc;
+    int *d_p = nullptr;
+    if ((rc = dalloc(&d_p, (size_t)count))) return rc;
+    const double *dv = E.d_dv + (size_t)first * c->k;
+    auto picks = [&](int np, int *out) {   // selection runs on c->stream
+        int r = select_pool(c, dv, count, d_p, np);
+        if (!r && (hipStreamSynchronize(c->stream) != hipSuccess ||
+                   hipMemcpy(out, d_p, sizeof(int) * count, hipMemcpyDeviceToHost) != hipSuccess))
+            r = fail(TWOSD_E_DEVICE, "pool candidates: selection failed");
+        return r;
+    };
+    rc = picks(level1, p1);
+    if (!rc) rc = picks((int)c->pool.size(), pf);
+    hipFree(d_p);
+    return rc;
+}
+
+// candidate lists from the picks of the training scenarios (any order): the ncand bases the flat
+// selection picks most often among the scenarios of each level-1 pick (ties: lower index)
+static int set_candidates(twosd_ctx *c, int level1, int ncand, int n, const int *p1, const int *pf) {
+    std::vector<std::map<int, int>> freq(level1);
+    for (int s = 0; s < n; ++s)
+        if (pf[s] != p1[s] && p1[s] >= 0 && p1[s] < level1) ++freq[p1[s]][pf[s]];
+    std::vector<int> cand((size_t)level1 * ncand, -1);
+    for (int p = 0; p < level1; ++p) {
+        std::vector<std::pair<int, int>> v;   // (-count, basis)
+        for (auto &kv : freq[p]) v.push_back({-kv.second, kv.first});
+        std::sort(v.begin(), v.end());
+        for (int i = 0; i < (int)v.size() && i < ncand; ++i) cand[(size_t)p * ncand + i] = v[i].second;
+    }
+    if (getenv("TWOSD_DEBUG")) {
+        int diff = 0, filled = 0;
+        for (int s = 0; s < n; ++s) diff += pf[s] != p1[s];
+        for (int v : cand) filled += v >= 0;
+        fprintf(stderr, "pool candidates: P=%zu level1=%d: %d of %d training picks change, %d candidate slots filled\n",
+                c->pool.size(), level1, diff, n, filled);
+    }
+    int rc;
+    if ((rc = upload(&c->d_cand, cand))) return rc;
+    c->pool_l1 = level1;
+    c->pool_ncand = ncand;
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_pool_candidate_picks(twosd_ctx *c, int epi, const double *x, int first, int count, int level1, int *p1,
+                                          int *pf) {
+    if (!c || !c->has_basis) return fail(TWOSD_E_STATE, "pool_candidate_picks: no primary basis");
+    if (epi < 0 || epi >= (int)c->epis.size()) return fail(TWOSD_E_ARG, "pool_candidate_picks: epigraph %d does not exist", epi);
+    const EpiDevice &E = c->epis[epi];
+    const int P = (int)c->pool.size();
+    if (first < 0 || count < 1 || first + count > E.count || level1 < 1 || level1 >= P || !p1 || !pf || (c->n1 > 0 && !x) ||
+        c->CH <= 0)
+        return fail(TWOSD_E_ARG, "pool_candidate_picks: bad arguments");
+    HIPCHK(hipSetDevice(c->device));
+    c->pool_l1 = c->pool_ncand = 0;   // the flat pick runs over the whole pool
+    return candidate_picks(c, E, x, first, count, level1, p1, pf);
+}
+
+extern "C" int twosd_pool_set_candidates(twosd_ctx *c, int level1, int ncand, int n, const int *p1, const int *pf) {
+    if (!c || !c->has_basis) return fail(TWOSD_E_STATE, "pool_set_candidates: no primary basis");
+    const int P = (int)c->pool.size();
+    if (level1 < 1 || level1 >= P || ncand < 1 || ncand > 256 || n < 0 || (n > 0 && (!p1 || !pf)))
+        return fail(TWOSD_E_ARG, "pool_set_candidates: bad arguments");
+    for (int s = 0; s < n; ++s)
+        if (p1[s] < 0 || p1[s] >= P || pf[s] < 0 || pf[s] >= P) return fail(TWOSD_E_ARG, "pool_set_candidates: pick outside the pool");
+    HIPCHK(hipSetDevice(c->device));
+    return set_candidates(c, level1, ncand, n, p1, pf);
+}
+
 extern "C" int twosd_pool_build_candidates(twosd_ctx *c, int epi, const double *x, int first, int count, int level1,
                                            int ncand) {
     if (!c || !c->has_basis) return fail(TWOSD_E_STATE, "pool_build_candidates: no primary basis");
@@ -1091,44 +1486,10 @@ extern "C" int twosd_pool_build_candidates(twosd_ctx *c, int epi, const double *
     c->pool_l1 = c->pool_ncand = 0;
     if (level1 == 0 || ncand == 0 || level1 >= P || P < 2 || c->CH <= 0) return TWOSD_OK;   // flat selection
     HIPCHK(hipSetDevice(c->device));
-    int rc;
-    if ((rc = prepare_x(c, x))) return rc;
-    int *d_p = nullptr;
-    if ((rc = dalloc(&d_p, (size_t)count))) return rc;
-    const double *dv = E.d_dv + (size_t)first * c->k;
     std::vector<int> p1(count), pf(count);
-    auto picks = [&](int np, std::vector<int> &out) {   // selection runs on c->stream
-        int r = select_pool(c, dv, count, d_p, np);
-        if (!r && (hipStreamSynchronize(c->stream) != hipSuccess ||
-                   hipMemcpy(out.data(), d_p, sizeof(int) * count, hipMemcpyDeviceToHost) != hipSuccess))
-            r = fail(TWOSD_E_DEVICE, "pool_build_candidates: selection failed");
-        return r;
-    };
-    rc = picks(level1, p1);
-    if (!rc) rc = picks(P, pf);
-    hipFree(d_p);
-    if (rc) return rc;
-    std::vector<std::map<int, int>> freq(level1);
-    for (int s = 0; s < count; ++s)
-        if (pf[s] != p1[s] && p1[s] >= 0 && p1[s] < level1) ++freq[p1[s]][pf[s]];
-    std::vector<int> cand((size_t)level1 * ncand, -1);
-    for (int p = 0; p < level1; ++p) {
-        std::vector<std::pair<int, int>> v;   // (-count, basis)
-        for (auto &kv : freq[p]) v.push_back({-kv.second, kv.first});
-        std::sort(v.begin(), v.end());
-        for (int i = 0; i < (int)v.size() && i < ncand; ++i) cand[(size_t)p * ncand + i] = v[i].second;
-    }
-    if (getenv("TWOSD_DEBUG")) {
-        int diff = 0, filled = 0;
-        for (int s = 0; s < count; ++s) diff += pf[s] != p1[s];
-        for (int v : cand) filled += v >= 0;
-        fprintf(stderr, "pool_build_candidates: P=%d level1=%d: %d of %d training picks change, %d candidate slots filled\n", P,
-                level1, diff, count, filled);
-    }
-    if ((rc = upload(&c->d_cand, cand))) return rc;
-    c->pool_l1 = level1;
-    c->pool_ncand = ncand;
-    return TWOSD_OK;
+    int rc;
+    if ((rc = candidate_picks(c, E, x, first, count, level1, p1.data(), pf.data()))) return rc;
+    return set_candidates(c, level1, ncand, count, p1.data(), pf.data());
 }
 
 extern "C" int twosd_last_pool_picks(twosd_ctx *c, int N, int *picks) {
@@ -1899,6 +2260,7 @@ static int copy_lp_outputs(twosd_ctx *c, int N, double *obj, double *pi, double 
     if (y) HIPCHK(hipMemcpy(y, c->d_y, sizeof(double) * N * c->L.n, hipMemcpyDeviceToHost));
     if (status) HIPCHK(hipMemcpy(status, c->d_status, sizeof(int) * N, hipMemcpyDeviceToHost));
     c->last_pivots_sum = (int64_t)stv[0]; c->last_ops_sum = (int64_t)stv[1]; c->last_pivots_max = (int)stv[2];
+    if (N >= 4096) c->piv_mean_ref = (double)stv[0] / N;
     const long long bad = (long long)stv[3];
     if (bad) return fail(TWOSD_E_LP, "%lld of %d scenario LPs not optimal (see status[])", bad, N);
     return TWOSD_OK;
@@ -1951,7 +2313,7 @@ extern "C" int twosd_last_lp_stats(twosd_ctx *c, int64_t *sum, int *mx) {
 }
 
 extern "C" int twosd_set_refresh_kcap(twosd_ctx *c, int kcap) {
-    if (!c || kcap < 0) return fail(TWOSD_E_ARG, "set_refresh_kcap: bad argument");
+    if (!c) return fail(TWOSD_E_ARG, "set_refresh_kcap: NULL");
     c->train_kcap = kcap;
     return TWOSD_OK;
 }

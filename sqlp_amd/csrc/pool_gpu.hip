@@ -302,7 +302,9 @@ __global__ __launch_bounds__(kPgThreads) void pg_fill_kernel(PgArgs A, PgFill F)
     __shared__ int ws[65];   // ELL slot offsets (entry rows)
     const int p = F.P0 + blockIdx.x, a = F.map[p];
     const int m = A.m, n = A.n, k = A.k, MP = A.MP, R9 = A.R9, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const Src S = src_of(A, a);
+    // a gathered source table (distributed refresh) carries its heads; otherwise the head row
+    // of the source's training scenario
+    const int *shead = a == 0 ? A.head0 : (A.gheads ? A.gheads + (size_t)(a - 1) * m : src_of(A, a).head);
     double *pi0 = smem, *cbv = smem + m;
     int *rs = reinterpret_cast<int *>(cbv + m), *cs = rs + (m + 1), *es = cs + (m + 1), *ic = es + (m + 1);
     int *cur = ic + (m + 1), *ecur = cur + m;
@@ -312,7 +314,7 @@ __global__ __launch_bounds__(kPgThreads) void pg_fill_kernel(PgArgs A, PgFill F)
     if (tid < 64) bits[tid] = 0;
     __syncthreads();
     for (int i = tid; i < m; i += kPgThreads) {
-        const int j = S.head[i];
+        const int j = shead[i];
         isb[j] = 1;
         cbv[i] = j < n ? A.q[j] : 0.0;
         atomicOr(reinterpret_cast<unsigned long long *>(&bits[j & 63]), 1ull << (j >> 6));
@@ -394,7 +396,7 @@ __global__ __launch_bounds__(kPgThreads) void pg_fill_kernel(PgArgs A, PgFill F)
     }
     for (int i = tid; i <= m; i += kPgThreads) F.kp[(size_t)p * (m + 1) + i] = eb + es[i];
     for (int i = tid; i < MP; i += kPgThreads)
-        F.hb0[(size_t)p * MP + i] = i < m ? S.head[i] * 4 + A.btype[S.head[i]] : -1;
+        F.hb0[(size_t)p * MP + i] = i < m ? shead[i] * 4 + A.btype[shead[i]] : -1;
     if (tid < 64) F.basic0[(size_t)p * 64 + tid] = bits[tid];
     if (tid == 0) {
         F.bnnz[p] = rs[m];

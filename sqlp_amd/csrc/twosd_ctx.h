@@ -36,7 +36,8 @@ struct twosd_ctx {
     hipEvent_t ev[8] = {};
     int num_cus = 256;
     int kmax_override = 0;
-    int train_kcap = 0;           // pivot cap of the refresh training solves (0: kmax)
+    int train_kcap = 0;           // pivot cap of the refresh training solves (> 0; 0: auto; < 0: none)
+    double piv_mean_ref = 0.0;    // mean pivots of the last large batch solve (the auto cap's scale)
     double t_us[5] = {0, 0, 0, 0, 0};   // LP kernel, dedup, cut partial, cut finalize, pool select
     // template
     bool has_template = false, has_basis = false;
@@ -154,6 +155,20 @@ struct twosd_ctx {
     long long *d_pg_ioff = nullptr;
     int *d_pg_cnt = nullptr, *d_pg_tot = nullptr, *d_pg_valid = nullptr, *d_pg_head0 = nullptr;
     int *d_pg_map = nullptr, *d_pg_off = nullptr, *d_pg_pos = nullptr;
+    // distributed refresh (twosd_refresh_*): this rank's training keys, its pack of built
+    // sources, and the source table gathered from all ranks
+    std::vector<unsigned long long> rt_keys;
+    std::vector<int> rt_counts, rt_reps;
+    std::vector<double> rt_lo, rt_hi;     // training box of this rank's slice
+    int rt_epi = -1, rt_first = -1, rt_count = -1, rt_n = -1, rt_nown = -1;
+    long long rt_nz0 = 0;                 // intermediate entries of the primary (local source 0)
+    int rt_nsrc_local = 0;
+    char *d_rt_pack = nullptr;
+    int *d_gs_heads = nullptr, *d_gs_cnt = nullptr, *d_gs_tot = nullptr, *d_gs_valid = nullptr, *d_gs_irow = nullptr;
+    long long *d_gs_ioff = nullptr;
+    double *d_gs_ival = nullptr;
+    void *d_gs_seg = nullptr;             // copy-segment list of the gather unpack
+    size_t gs_seg_cap = 0;
     // pinned host staging buffers of the pool upload, kept across uploads (no page faults,
     // no unmapping per refresh, page-locked copies)
     void *stage[16] = {};

@@ -88,6 +88,8 @@ struct PgArgs {
     const int *eo_pb, *eo_K, *eo_off, *eo_etap, *eo_etaoff, *eo_eidx; const double *eo_evals;
     const int *head0, *heads;                            // primary head (m); heads (eta-file rows)
     const int *src_row;                                  // source a >= 1: eta-file / head row src_row[a - 1]
+    const int *gheads;                                   // fill only (nullable): head of source a >= 1 at
+                                                         //   gheads + (a - 1) m (a gathered source table)
     int a0;                                              // first source of the launch
     double *amax;                                        // nsrc (-1: source unusable)
     int *nzc, *keptc;                                    // nsrc x m: nonzeros / kept entries per column

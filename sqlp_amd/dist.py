@@ -174,6 +174,120 @@ def push_sharded(V, pis_local: np.ndarray) -> int:
     return len(V)
 
 
+def select_refresh_bases(keys, counts, reps, rank_of, max_pool):
+    """Global selection of a distributed pool refresh, identical on every rank.  keys / counts /
+    reps / rank_of: the distinct optimal bases of every rank's training slice, concatenated in
+    rank order (within a rank ascending by first scenario, as twosd_refresh_train lists them).
+    A basis seen by several ranks counts the sum of their counts and belongs to the rank of its
+    first occurrence.  The max_pool - 1 most frequent, ties by first occurrence in (rank,
+    scenario) order -- the single-rank refresh's stable sort over all training scenarios.
+    Returns (owner rank, owner's first scenario) of the picks, in pool order."""
+    keys = np.asarray(keys, dtype=np.uint64)
+    if keys.size == 0 or max_pool <= 1:
+        return np.zeros(0, dtype=np.int64), np.zeros(0, dtype=np.int64)
+    _, first, inv = np.unique(keys, return_index=True, return_inverse=True)
+    tot = np.bincount(inv.reshape(-1), weights=np.asarray(counts, dtype=np.float64)).astype(np.int64)
+    order = np.lexsort((first, -tot))[: max_pool - 1]          # by -count, then first occurrence
+    pick = first[order]
+    return np.asarray(rank_of)[pick].astype(np.int64), np.asarray(reps)[pick].astype(np.int64)
+
+
+def _allgather_1d(arr: np.ndarray, device=None):
+    """Rank-order concatenation of every rank's 1-D array (variable lengths) and the length of
+    each part.  Host arrays; over RCCL they travel as device tensors."""
+    G = dist.get_world_size()
+    t = torch.from_numpy(np.ascontiguousarray(arr))
+    nccl = dist.get_backend() == "nccl"
+    if nccl:
+        t = t.to(device)
+    n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
+    ns = [torch.zeros_like(n) for _ in range(G)]
+    dist.all_gather(ns, n)
+    ns = [int(v.item()) for v in ns]
+    pad = torch.zeros(max(max(ns), 1), dtype=t.dtype, device=t.device)
+    pad[: t.numel()] = t
+    bufs = [torch.zeros_like(pad) for _ in range(G)]
+    dist.all_gather(bufs, pad)
+    return np.concatenate([b[:k].cpu().numpy() for b, k in zip(bufs, ns)]), ns
+
+
+def refresh_sharded(ctx, train_epi, x, first, count, max_pool, level1=0, ncand=0, device=None):
+    """twosd_pool_refresh of the training scenarios of every rank (this rank: [first,
+    first + count) of train_epi, the ranks' slices contiguous in rank order) -- the same pool on
+    every rank, equal to one rank refreshing from all of them:
+      1. each rank solves its slice (twosd_refresh_train);
+      2. exchange 1: all-gather of the distinct bases (key, count, first scenario) and of the
+         delta boxes; select_refresh_bases on every rank;
+      3. each rank composes the picks it owns (twosd_refresh_build_local);
+      4. exchange 2: all-gather of the packs (one all_gather_into_tensor of device buffers,
+         padded to the largest pack); every rank assembles the pool (twosd_refresh_assemble);
+      5. the two-level candidate lists from every rank's picks (exchange 3: the picks).
+    Returns (pool size, phase milliseconds)."""
+    import time
+    rank, G = world()
+    t = [time.perf_counter()]
+    keys, counts, reps, lo, hi = ctx.refresh_train(train_epi, x, first, count)
+    t.append(time.perf_counter())
+    if G == 1:
+        all_keys, all_counts, all_reps, ns = keys, counts, reps, [len(keys)]
+        box_lo, box_hi = lo, hi
+    else:
+        all_keys, ns = _allgather_1d(keys.view(np.int64), device)
+        all_keys = all_keys.view(np.uint64)
+        all_counts, _ = _allgather_1d(counts.astype(np.int64), device)
+        all_reps, _ = _allgather_1d(reps.astype(np.int64), device)
+        boxes, _ = _allgather_1d(np.concatenate([lo, hi]), device)
+        boxes = boxes.reshape(G, 2, -1)
+        box_lo, box_hi = boxes[:, 0].min(axis=0), boxes[:, 1].max(axis=0)
+    rank_of = np.repeat(np.arange(G), ns)
+    owner, orep = select_refresh_bases(all_keys, all_counts, all_reps, rank_of, max_pool)
+    mine = orep[owner == rank]
+    # source id of a pick: 1 + its position among all packs (rank-major, selection order)
+    n_own = np.bincount(owner, minlength=G) if owner.size else np.zeros(G, dtype=np.int64)
+    base = 1 + np.concatenate([[0], np.cumsum(n_own)[:-1]])
+    pos = np.zeros(owner.size, dtype=np.int64)
+    seen = np.zeros(G, dtype=np.int64)
+    for i, r in enumerate(owner):
+        pos[i] = base[r] + seen[r]
+        seen[r] += 1
+    t.append(time.perf_counter())
+    nbytes = ctx.refresh_build_local(mine)
+    t.append(time.perf_counter())
+    if G == 1:
+        buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        torch.cuda.synchronize(device)
+        ctx.refresh_pack(buf.data_ptr())
+        size = ctx.refresh_assemble(1, buf.data_ptr(), nbytes, pos, box_lo, box_hi)
+    else:
+        mx = torch.tensor([nbytes], dtype=torch.int64, device=device if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        stride = (int(mx.item()) + 255) // 256 * 256
+        buf = torch.empty(stride, dtype=torch.uint8, device=device)
+        torch.cuda.synchronize(device)
+        ctx.refresh_pack(buf.data_ptr())
+        if dist.get_backend() == "nccl":
+            out = torch.empty(G * stride, dtype=torch.uint8, device=device)
+            dist.all_gather_into_tensor(out, buf)
+            torch.cuda.synchronize(device)
+        else:   # gloo (tests, rehearsal): through host memory
+            parts = [torch.empty(stride, dtype=torch.uint8) for _ in range(G)]
+            dist.all_gather(parts, buf.cpu())
+            out = torch.cat(parts).to(device)
+            torch.cuda.synchronize(device)
+        size = ctx.refresh_assemble(G, out.data_ptr(), stride, pos, box_lo, box_hi)
+    t.append(time.perf_counter())
+    if level1 > 0 and ncand > 0 and size > level1:
+        p1, pf = ctx.pool_candidate_picks(train_epi, x, first, count, level1)
+        if G > 1:
+            p1, _ = _allgather_1d(p1.astype(np.int64), device)
+            pf, _ = _allgather_1d(pf.astype(np.int64), device)
+        ctx.pool_set_candidates(level1, ncand, p1, pf)
+    t.append(time.perf_counter())
+    ms = dict(zip(("train", "select", "build", "exchange_assemble", "candidates"),
+                  (1e3 * (b - a) for a, b in zip(t[:-1], t[1:]))))
+    return size, ms
+
+
 def finalize_from_partials(hist: np.ndarray, sums: np.ndarray, V: np.ndarray, r: np.ndarray, T: np.ndarray,
                            cols: np.ndarray):
     """Host restatement of twosd_cut_finalize (used by the gloo tests): g = sum_v h_v pi_v,

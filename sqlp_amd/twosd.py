@@ -165,6 +165,51 @@ class SDContext:
         check(self.lib.twosd_pool_refresh(self.h, epi.index, ptr(_f64(x)), first, count, max_pool, C.byref(n)))
         return n.value
 
+    # -- distributed refresh (twosd_refresh_*; driven by sqlp_amd.dist.refresh_sharded) --------
+    def refresh_train(self, epi, x, first, count):
+        """Training solves of this rank's slice; returns (keys u64, counts, first scenarios, box
+        lo, box hi) of its distinct optimal bases."""
+        U = C.c_int()
+        lo = np.zeros(max(self.k, 1))
+        hi = np.zeros(max(self.k, 1))
+        check(self.lib.twosd_refresh_train(self.h, epi.index, ptr(_f64(x)), int(first), int(count), C.byref(U),
+                                           ptr(lo), ptr(hi)))
+        keys = np.zeros(U.value, dtype=np.uint64)
+        counts = np.zeros(U.value, dtype=np.int32)
+        reps = np.zeros(U.value, dtype=np.int32)
+        check(self.lib.twosd_refresh_train_bases(self.h, ptr(keys), ptr(counts), ptr(reps)))
+        return keys, counts, reps, lo[:self.k], hi[:self.k]
+
+    def refresh_build_local(self, reps) -> int:
+        """Compose the bases this rank owns (first scenarios `reps`, selection order); returns the
+        pack size in bytes."""
+        reps = np.ascontiguousarray(reps, dtype=np.int32)
+        nb = C.c_int64()
+        check(self.lib.twosd_refresh_build_local(self.h, len(reps), ptr(reps), C.byref(nb)))
+        return nb.value
+
+    def refresh_pack(self, d_dst: int):
+        check(self.lib.twosd_refresh_pack(self.h, C.c_void_p(d_dst)))
+
+    def refresh_assemble(self, G, d_packs: int, stride: int, order, box_lo, box_hi) -> int:
+        order = np.ascontiguousarray(order, dtype=np.int32)
+        n = C.c_int()
+        check(self.lib.twosd_refresh_assemble(self.h, int(G), C.c_void_p(d_packs), C.c_int64(stride), len(order),
+                                              ptr(order), ptr(_f64(box_lo)), ptr(_f64(box_hi)), C.byref(n)))
+        return n.value
+
+    def pool_candidate_picks(self, epi, x, first, count, level1):
+        p1 = np.zeros(count, dtype=np.int32)
+        pf = np.zeros(count, dtype=np.int32)
+        check(self.lib.twosd_pool_candidate_picks(self.h, epi.index, ptr(_f64(x)), int(first), int(count), int(level1),
+                                                  ptr(p1), ptr(pf)))
+        return p1, pf
+
+    def pool_set_candidates(self, level1, ncand, p1, pf):
+        p1 = np.ascontiguousarray(p1, dtype=np.int32)
+        pf = np.ascontiguousarray(pf, dtype=np.int32)
+        check(self.lib.twosd_pool_set_candidates(self.h, int(level1), int(ncand), len(p1), ptr(p1), ptr(pf)))
+
     def set_refresh_kcap(self, kcap: int):
         """Pivot cap of the refresh's training solves (0: none below kmax)."""
         check(self.lib.twosd_set_refresh_kcap(self.h, int(kcap)))

@@ -138,3 +138,85 @@ def _mismatch_worker(rank, world, port, out):
             out[rank] = "raised"
     finally:
         dist.destroy_process_group()
+
+
+# ---- distributed pool refresh (sqlp_amd.dist.refresh_sharded) ------------------------------
+R_TRAIN = 4096
+R_POOL = 512
+R_EVAL = 3000
+
+
+def _refresh_x():
+    from tests.test_gpu_pool_refresh import _sd_x
+    return _sd_x(3)
+
+
+def _storm_ctx():
+    from sqlp_amd import smps, twosd
+    inst = I.load("storm")
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    ctx.compute_basis(I.x_ev("storm"), smps.mean_values(inst["sto"]))
+    ctx.set_distributions(inst["sto"])
+    return ctx
+
+
+def _pool_state(ctx, x):
+    from sqlp_amd import twosd
+    heads = np.stack([ctx.pool_get(p) for p in range(ctx.pool_size())])
+    ev = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_sampled_scenarios(ev, R_EVAL, 99)
+    obj, _, _, st = twosd.solve_batch(ev, x, 0, R_EVAL, want_pi=False)
+    return heads, obj, st, ctx.last_pool_picks(R_EVAL), ctx.lp_stats()[0]
+
+
+def _refresh_worker(rank, world, port, x, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from sqlp_amd import dist as sdist
+        from sqlp_amd import twosd
+        ctx = _storm_ctx()
+        lo, hi = sdist.shard_range(R_TRAIN, rank, world)
+        tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+        twosd.add_sampled_scenarios(tr, hi - lo, 4242, first_index=lo)
+        size, ms = sdist.refresh_sharded(ctx, tr, x, 0, hi - lo, R_POOL, 128, 160, torch.device("cuda", 0))
+        heads, obj, st, picks, piv = _pool_state(ctx, x)
+        out[rank] = dict(size=size, heads=heads, obj=obj, st=st, picks=picks, piv=piv, ms=ms)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_refresh_sharded_equals_single_rank():
+    """Two ranks on cuda:0 (gloo) refresh the pool from their halves of the training scenarios
+    (train, exchange the distinct bases, compose the owned picks, all-gather the packs,
+    assemble, candidate lists from both ranks' picks): both hold the pool one rank builds from
+    all training scenarios with twosd_pool_refresh + twosd_pool_build_candidates -- the same
+    bases in the same order -- and the next solve is bit-identical (objectives, pool picks,
+    pivots)."""
+    import torch.multiprocessing as mp
+    from sqlp_amd import twosd
+    x = _refresh_x()
+    port = _free_port()
+    with mp.get_context("spawn").Manager() as mgr:
+        out = mgr.dict()
+        mp.start_processes(_refresh_worker, args=(2, port, x, out), nprocs=2, join=True, start_method="spawn")
+        res = dict(out)
+    ctx = _storm_ctx()
+    tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_sampled_scenarios(tr, R_TRAIN, 4242)
+    size = ctx.pool_refresh(tr, x, 0, R_TRAIN, R_POOL)
+    ctx.pool_build_candidates(tr, x, 0, R_TRAIN, 128, 160)
+    heads, obj, st, picks, piv = _pool_state(ctx, x)
+    assert size > 128 and (st == 0).all()
+    for r in (0, 1):
+        o = res[r]
+        assert o["size"] == size
+        np.testing.assert_array_equal(o["heads"], heads)
+        np.testing.assert_array_equal(o["st"], st)
+        np.testing.assert_array_equal(o["obj"], obj)
+        np.testing.assert_array_equal(o["picks"], picks)
+        assert o["piv"] == piv
+    print(f"refresh_sharded: pool {size}, phases (rank 0) {res[0]['ms']}")

@@ -1,0 +1,160 @@
+"""Per-rank step of the N-GPU bench (strong scaling of the storm 1M batch), emulated on ONE GPU:
+G contexts in one process, one per emulated rank, each with its own 1/G scenario shard and its
+1/G slice of the refresh training scenarios.  Every phase of a rank runs alone on the GPU, in
+sequence: the distributed refresh (twosd_refresh_train, the global selection, the local
+composition, the assembly from the gathered packs, the candidate picks), then solve_push and
+the cut over the rank's shard.  The all-gathers travel by device copies here; their xGMI time is
+estimated as bytes / (link_gbs) per peer pack (each GPU receives the G-1 other packs over its G-1
+point-to-point links in parallel) and added -- it is the one number not measured.
+
+Per-rank step = the rank's own phases + the exchange estimate; reported per x point and as the
+max over ranks, next to N = 1 (one context holding everything, the bench's single-GPU step).
+Usage (GPU box): python tools/shard_emulate.py [G] [scenarios] [steps]
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+LINK_GBS = 153.0 * 0.5       # xGMI link, half of the per-link figure (RCCL efficiency assumed)
+
+
+def main():
+    import torch
+    torch.cuda.init()
+    dev = torch.device("cuda", 0)
+    import bench
+    from sqlp_amd import dist as sdist
+    from sqlp_amd import smps, twosd
+    G = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    N = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
+    steps = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+    seed = 20250219
+    POOL, TRAIN, L1, NC, NV = 4096, 16384, 128, 160, 4096
+    d = os.path.join(ROOT, "data", "smps", "storm")
+    cor, tim, sto = smps.load_smps(d, "storm")
+    sp2 = smps.get_smps_stage_template(cor, tim, 2)
+    with open(os.path.join(ROOT, "tests", "golden", "ev_x.json")) as f:
+        x0 = np.array(json.load(f)["storm"]["x"])
+    positions = list(sto.indep.keys())
+    xs = bench.sd_points(cor, tim, sp2, sto, positions, x0, [0, 4, 12, 30], seed + 7, dev)
+    ranks = []
+    for r in range(G):
+        ctx = twosd.SDContext(sp2, sto)
+        ctx.compute_basis(x0, smps.mean_values(sto, positions))
+        ctx.set_distributions(sto)
+        lo, hi = sdist.shard_range(N, r, G)
+        epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
+        twosd.add_sampled_scenarios(epi, hi - lo, seed, first_index=lo)
+        tlo, thi = sdist.shard_range(TRAIN, r, G)
+        tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+        twosd.add_sampled_scenarios(tr, thi - tlo, seed + 4, first_index=tlo)
+        V = twosd.sdDualVertexSet(ctx)
+        ranks.append(dict(ctx=ctx, epi=epi, tr=tr, n=hi - lo, nt=thi - tlo, V=V))
+    # |V| pool (identical on every rank): duals of stream seed + 1
+    src = twosd.sdEpigraph(ranks[0]["ctx"], 1.0, 0.0)
+    twosd.add_sampled_scenarios(src, 1 << 18, seed + 1)
+    V0 = twosd.sdDualVertexSet(ranks[0]["ctx"])
+    at = 0
+    while len(V0) < NV and at < (1 << 18):     # as bench.py
+        _, _, pis, st = twosd.solve_batch(src, x0, at, 16384, want_pi=True)
+        V0.push_batch(pis[st == 0])
+        at += 16384
+    V0.truncate(min(NV, len(V0)))
+    Vm = V0.matrix()
+    for rk in ranks[1:]:
+        rk["V"].push_batch(Vm)
+    nv = len(V0)
+
+    def refresh(xx):
+        """the distributed refresh, phase by phase per rank; returns per-rank ms and pack bytes"""
+        ms = [dict() for _ in range(G)]
+        lists = []
+        for r, rk in enumerate(ranks):
+            t = time.perf_counter()
+            k, c, f, lo_, hi_ = rk["ctx"].refresh_train(rk["tr"], xx, 0, rk["nt"])
+            ms[r]["train"] = 1e3 * (time.perf_counter() - t)
+            lists.append((k, c, f, lo_, hi_))
+        t = time.perf_counter()
+        kk = np.concatenate([l[0] for l in lists])
+        cc = np.concatenate([l[1] for l in lists]).astype(np.int64)
+        ff = np.concatenate([l[2] for l in lists]).astype(np.int64)
+        rk_of = np.concatenate([np.full(len(l[0]), r) for r, l in enumerate(lists)])
+        owner, orep = sdist.select_refresh_bases(kk, cc, ff, rk_of, POOL)
+        box_lo = np.min([l[3] for l in lists], axis=0)
+        box_hi = np.max([l[4] for l in lists], axis=0)
+        n_own = np.bincount(owner, minlength=G)
+        base = 1 + np.concatenate([[0], np.cumsum(n_own)[:-1]])
+        pos = np.zeros(owner.size, dtype=np.int64)
+        seen = np.zeros(G, dtype=np.int64)
+        for i, o in enumerate(owner):
+            pos[i] = base[o] + seen[o]
+            seen[o] += 1
+        t_sel = 1e3 * (time.perf_counter() - t)
+        nbytes = []
+        for r, rk in enumerate(ranks):
+            ms[r]["select"] = t_sel
+            t = time.perf_counter()
+            nbytes.append(rk["ctx"].refresh_build_local(orep[owner == r]))
+            ms[r]["build"] = 1e3 * (time.perf_counter() - t)
+        stride = (max(nbytes) + 255) // 256 * 256
+        out = torch.empty(G * stride, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        for r, rk in enumerate(ranks):
+            rk["ctx"].refresh_pack(out[r * stride:].data_ptr())
+        for r, rk in enumerate(ranks):
+            t = time.perf_counter()
+            rk["ctx"].refresh_assemble(G, out.data_ptr(), stride, pos, box_lo, box_hi)
+            ms[r]["assemble"] = 1e3 * (time.perf_counter() - t)
+        picks = []
+        for r, rk in enumerate(ranks):
+            t = time.perf_counter()
+            picks.append(rk["ctx"].pool_candidate_picks(rk["tr"], xx, 0, rk["nt"], L1))
+            ms[r]["picks"] = 1e3 * (time.perf_counter() - t)
+        p1 = np.concatenate([p[0] for p in picks])
+        pf = np.concatenate([p[1] for p in picks])
+        for r, rk in enumerate(ranks):
+            t = time.perf_counter()
+            rk["ctx"].pool_set_candidates(L1, NC, p1, pf)
+            ms[r]["cand_lists"] = 1e3 * (time.perf_counter() - t)
+            # exchanges: basis lists (tiny), packs, picks (tiny) -- estimated
+            ms[r]["xgmi_est"] = 1e3 * (max(nbytes[q] for q in range(G) if q != r) if G > 1 else 0) / (LINK_GBS * 1e9) + 0.1
+        return ms, nbytes, int(ranks[0]["ctx"].pool_size())
+
+    def solve_cut(rk, xx):
+        t = time.perf_counter()
+        rk["ctx"].invalidate_x()
+        twosd.solve_push(rk["epi"], xx, 0, rk["n"], want_obj=False)
+        rk["V"].truncate(nv)
+        piv = rk["ctx"].lp_stats()[0] / rk["n"]
+        twosd.build_sasa_cut(rk["epi"], xx, rk["V"], 1e-12)
+        return 1e3 * (time.perf_counter() - t), piv
+
+    refresh(xs[-1])       # warmup: the pool at the last x point
+    rows = []
+    for i in range(steps):
+        xx = xs[i % len(xs)]
+        ms, nbytes, P = refresh(xx)
+        per = []
+        for r, rk in enumerate(ranks):
+            t_sc, piv = solve_cut(rk, xx)
+            ms[r]["solve_cut"] = t_sc
+            per.append((sum(ms[r].values()), piv))
+        worst = max(range(G), key=lambda r: per[r][0])
+        rows.append((i % len(xs), per[worst][0], np.mean([p[0] for p in per]), np.mean([p[1] for p in per]), P,
+                     {k: round(v, 2) for k, v in ms[worst].items()}, max(nbytes)))
+        print(f"x{rows[-1][0]}: per-rank step max {rows[-1][1]:.2f} ms (mean {rows[-1][2]:.2f}), pivots {rows[-1][3]:.2f}, "
+              f"pool {P}, pack {max(nbytes) / 1e6:.1f} MB, slowest rank {rows[-1][5]}", flush=True)
+    step_ms = float(np.mean([r[1] for r in rows]))
+    print(json.dumps({"G": G, "scenarios": N, "per_rank_step_ms": step_ms,
+                      "subproblems_per_s_projected": N / (step_ms * 1e-3),
+                      "note": f"emulated on one GPU; xGMI all-gather estimated at {LINK_GBS} GB/s per link"}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -24,7 +24,8 @@ def main():
     N = int(sys.argv[1]) if len(sys.argv) > 1 else 125000
     T = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
     P = int(sys.argv[3]) if len(sys.argv) > 3 else 512
-    caps = [int(v) for v in sys.argv[4:]] or [0, 96, 64, 48, 32]
+    # cap: an explicit pivot cap, "none" (kmax) or "auto" (4 x the last batch's mean, >= 32)
+    caps = sys.argv[4:] or ["none", "auto", "48", "32", "24"]
     d = os.path.join(ROOT, "data", "smps", "storm")
     cor, tim, sto = smps.load_smps(d, "storm")
     sp2 = smps.get_smps_stage_template(cor, tim, 2)
@@ -40,9 +41,9 @@ def main():
     epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
     twosd.add_sampled_scenarios(epi, N, 20250219)
     for cap in caps:
-        ctx.set_refresh_kcap(0)
+        ctx.set_refresh_kcap(-1)
         ctx.pool_refresh(tr, xs[-1], 0, T, P)
-        ctx.set_refresh_kcap(cap)
+        ctx.set_refresh_kcap({"none": -1, "auto": 0}.get(cap) if cap in ("none", "auto") else int(cap))
         rows = []
         for xx in xs:
             t0 = time.perf_counter()
