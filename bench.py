@@ -297,7 +297,10 @@ def main():
                 per_x[cur["xi"]]["refresh_parts"] = {k_: round(v, 2) for k_, v in pool_at["last_ms"].items()}
             if cur["xi"] not in heads_at and not args.no_cpu and rank == 0:
                 heads_at[cur["xi"]] = np.stack([ctx.pool_get(p) for p in range(min(args.cpu_pool, ctx.pool_size()))])
-        ctx.invalidate_x()     # every pass pays its per-x setup (x_B of the pool, selection data)
+        # every pass pays its per-x setup (x_B of the pool, selection data): a step that refreshed
+        # paid it inside the refresh (the candidate lists select at this x, with this pool)
+        if t_ref == 0.0:
+            ctx.invalidate_x()
         alpha = 0.0
         for epi_e, tw in zip(epis, total_weights):
             if args.no_dedup:

@@ -137,6 +137,23 @@ static T *stage_buf(twosd_ctx *c, int slot, size_t n) {
     return static_cast<T *>(c->stage[slot]);
 }
 
+// head of pool basis p (materialised from c->pool_hb for a device-built basis on first use: a
+// refresh of 4096 bases would otherwise spend ~2 ms building host heads nobody reads)
+static const std::vector<int> &head_of(twosd_ctx *c, int p) {
+    PoolBasis &B = c->pool[p];
+    if (B.hb_row >= 0) {
+        const int m = c->L.m;
+        const int *r = c->pool_hb + (size_t)B.hb_row * c->MP;
+        B.head.resize(m);
+        for (int i = 0; i < m; ++i) B.head[i] = r[i] >> 2;
+        B.hb_row = -1;
+    }
+    return B.head;
+}
+static void materialize_heads(twosd_ctx *c) {
+    for (int p = 0; p < (int)c->pool.size(); ++p) head_of(c, p);
+}
+
 // f(i) for i in [0, n) on up to 16 host threads (per-basis pool preparation: independent work)
 template <typename F>
 static void parallel_for(int n, F f) {
@@ -243,6 +260,7 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_gs_irow); dfree(c->d_gs_ioff); dfree(c->d_gs_ival);
     if (c->d_gs_seg) { hipFree(c->d_gs_seg); c->d_gs_seg = nullptr; c->gs_seg_cap = 0; }
     c->rt_epi = -1; c->rt_nown = -1;
+    if (c->pool_hb) { hipHostFree(c->pool_hb); c->pool_hb = nullptr; c->pool_hb_cap = 0; }
     c->has_template = c->has_basis = false;
 }
 
@@ -460,6 +478,7 @@ static void pi0_from_rows(const twosd_ctx *c, PoolBasis &B) {
 // host CSR rows and pi0 of the bases a device refresh built (dev_only), read back from the
 // pool arrays: upload_pool, prepare_elements and the host compose work on the host forms
 static int ensure_host_pool(twosd_ctx *c) {
+    materialize_heads(c);
     const int P = (int)c->pool.size(), MP = c->MP, m = c->L.m;
     int last = -1;
     for (int p = 0; p < P; ++p)
@@ -598,6 +617,7 @@ static bool same_basis(const std::vector<int> &a, const std::vector<int> &b) {
 
 // append a basis to the pool; returns 1 if added, 0 if already present, < 0 on error
 static int pool_add(twosd_ctx *c, const std::vector<int> &head, bool upload_now) {
+    materialize_heads(c);
     for (const PoolBasis &B : c->pool)
         if (same_basis(B.head, head)) return 0;
     PoolBasis pb;
@@ -655,7 +675,8 @@ extern "C" int twosd_pool_size(twosd_ctx *c, int *size) {
 
 extern "C" int twosd_pool_get(twosd_ctx *c, int p, int *head) {
     if (!c || !head || p < 0 || p >= (int)c->pool.size()) return fail(TWOSD_E_ARG, "pool_get: basis %d of %zu", p, c ? c->pool.size() : 0);
-    std::copy(c->pool[p].head.begin(), c->pool[p].head.end(), head);
+    const std::vector<int> &h = head_of(c, p);
+    std::copy(h.begin(), h.end(), head);
     return TWOSD_OK;
 }
 
@@ -708,6 +729,7 @@ extern "C" int twosd_pool_build(twosd_ctx *c, int epi, const double *x, int firs
         HIPCHK(hipMemcpy(heads.data(), c->d_head_out, sizeof(int) * heads.size(), hipMemcpyDeviceToHost));
         HIPCHK(hipMemcpy(st.data(), c->d_status, sizeof(int) * nh, hipMemcpyDeviceToHost));
         std::map<std::vector<int>, std::pair<int, int>> freq;   // sorted head -> (count, first scenario)
+        materialize_heads(c);
         for (const PoolBasis &B : c->pool) {
             std::vector<int> key(B.head);
             std::sort(key.begin(), key.end());
@@ -876,6 +898,8 @@ static int pg_assemble(twosd_ctx *c, PgArgs &A, const int *h_tot, const int *h_v
             return fail(TWOSD_E_UNSUPPORTED, "basis pool too large (> 2^31 entries)");
     }
     const int P = (int)map.size();
+    const bool dbg = getenv("TWOSD_DEBUG") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     if ((rc = dev_reserve(c, &c->d_pg_map, (size_t)P)) || (rc = dev_reserve(c, &c->d_pg_off, (size_t)4 * P))) return rc;
     // From here the live pool arrays are grown in place (a grown array does not keep its
     // contents) and then overwritten: a failure past this point leaves c->pool describing
@@ -911,21 +935,28 @@ static int pg_assemble(twosd_ctx *c, PgArgs &A, const int *h_tot, const int *h_v
     F.hb0 = c->d_hb0; F.basic0 = c->d_basic0; F.bnnz = c->d_bnnz; F.d0 = c->d_d0; F.sel_ptr = c->d_sel_ptr;
     F.P0 = 0;
     if (pg_launch_fill(A, F, P, c->stream) != hipSuccess) return broken(fail(TWOSD_E_DEVICE, "pool refresh: fill launch failed"));
-    int *h_hb = stage_buf<int>(c, 10, (size_t)P * MP);   // the pool's heads, from hb0 = 4 head + type
-    if (!h_hb) return broken(fail(TWOSD_E_DEVICE, "pool refresh: pinned staging allocation failed"));
-    if (hipMemcpyAsync(h_hb, c->d_hb0, sizeof(int) * P * MP, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+    // the pool's heads (hb0 = 4 head + type) into a pinned buffer of their own; a host head is
+    // materialised from it on first use (head_of)
+    // (the old pool's bases that refer to the buffer are dropped below; only the primary,
+    // a host basis, is kept)
+    if ((size_t)P * MP > c->pool_hb_cap) {
+        if (c->pool_hb) hipHostFree(c->pool_hb);
+        c->pool_hb = nullptr;
+        c->pool_hb_cap = 0;
+        if (hipHostMalloc((void **)&c->pool_hb, sizeof(int) * (size_t)P * MP * 5 / 4) != hipSuccess)
+            return broken(fail(TWOSD_E_DEVICE, "pool refresh: pinned allocation of the pool heads failed"));
+        c->pool_hb_cap = (size_t)P * MP * 5 / 4;
+    }
+    if (hipMemcpyAsync(c->pool_hb, c->d_hb0, sizeof(int) * P * MP, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
         return broken(fail(TWOSD_E_DEVICE, "pool refresh: reading the built pool heads failed"));
-    // host pool: the primary keeps its host forms; the new bases carry their heads
-    std::vector<PoolBasis> keep;
-    keep.reserve(P);
-    keep.push_back(std::move(c->pool[0]));
+    const auto t1 = std::chrono::steady_clock::now();
+    // host pool: the primary keeps its host forms; the new bases refer to their head rows
+    std::vector<PoolBasis> keep(P);
+    keep[0] = std::move(c->pool[0]);
     for (int p = 1; p < P; ++p) {
-        PoolBasis B;
-        B.head.resize(m);
-        for (int i = 0; i < m; ++i) B.head[i] = h_hb[(size_t)p * MP + i] >> 2;
-        B.dev_only = true;
-        keep.push_back(std::move(B));
+        keep[p].hb_row = p;
+        keep[p].dev_only = true;
     }
     c->pool.swap(keep);
     std::thread([old = std::move(keep)]() mutable { old.clear(); }).detach();
@@ -933,6 +964,11 @@ static int pg_assemble(twosd_ctx *c, PgArgs &A, const int *h_tot, const int *h_v
     c->prep_valid = false;
     c->k_valid = true;
     c->pool_l1 = c->pool_ncand = 0;
+    if (dbg) {
+        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        fprintf(stderr, "pg_assemble: P=%d fill + heads %.2f ms, host pool %.2f ms\n", P, ms(t0, t1),
+                ms(t1, std::chrono::steady_clock::now()));
+    }
     return TWOSD_OK;
 }
 
@@ -954,13 +990,15 @@ static int refresh_build_device(twosd_ctx *c, const std::vector<int> &sel) {
 
 // pivot cap of the training solves of a refresh.  One wavefront solves one scenario, so a
 // training launch lasts as long as its slowest scenario; the scenarios far from the current
-// pool (tens of pivots) mostly end at rare bases.  Auto: 4 x the mean pivots of the last large
-// batch, at least 32 (storm: 32-44; ssn, ~33 pivots a solve: ~130); none before any batch.
+// pool (tens of pivots) mostly end at rare bases.  Auto: 3 x the mean pivots of the last large
+// batch, at least 32 (storm: 32-33; ssn, ~33 pivots a solve: ~100); none before any batch.
+// Storm 1M, 4096-basis pool (profiles/r03/train_kcap_1M.txt): cap 32 vs none -- refresh
+// 18.3 vs 25.6 ms, and the next solve 86.6 vs 108.5 ms (fewer pivots from the capped pool).
 static int train_kcap(const twosd_ctx *c) {
     if (const char *e = getenv("TWOSD_TRAIN_KCAP")) return atoi(e);   // A/B knob
     if (c->train_kcap > 0) return c->train_kcap;
     if (c->train_kcap < 0 || c->piv_mean_ref <= 0.0) return 0;
-    return std::max(32, (int)std::ceil(4.0 * c->piv_mean_ref));
+    return std::max(32, (int)std::ceil(3.0 * c->piv_mean_ref));
 }
 
 extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int first, int count, int max_pool,
@@ -1350,6 +1388,10 @@ extern "C" int twosd_refresh_assemble(twosd_ctx *c, int G, const void *d_packs, 
         add(P + L.ival, c->d_gs_ival + zn[r], sizeof(double) * nz);
     }
     if ((rc = rt_copy(c, seg))) return rc;
+    const auto t_copy = std::chrono::steady_clock::now();
+    if (getenv("TWOSD_DEBUG"))
+        fprintf(stderr, "refresh_assemble: %lld sources, %lld entries, unpack %.2f ms\n", nsrc, nzg,
+                std::chrono::duration<double, std::milli>(t_copy - t0).count());
     int *h_tot = stage_buf<int>(c, 9, (size_t)6 * nsrc);
     long long *h_ioff = stage_buf<long long>(c, 12, (size_t)nsrc);
     if (!h_tot || !h_ioff) return fail(TWOSD_E_DEVICE, "refresh: pinned staging allocation failed");
@@ -1426,15 +1468,27 @@ static int candidate_picks(twosd_ctx *c, const EpiDevice &E, const double *x, in
 // candidate lists from the picks of the training scenarios (any order): the ncand bases the flat
 // selection picks most often among the scenarios of each level-1 pick (ties: lower index)
 static int set_candidates(twosd_ctx *c, int level1, int ncand, int n, const int *p1, const int *pf) {
-    std::vector<std::map<int, int>> freq(level1);
+    // (level-1 pick, flat pick) pairs that differ, sorted, then counted by runs
+    std::vector<long long> pr;
+    pr.reserve(n);
+    const long long P = (long long)c->pool.size();
     for (int s = 0; s < n; ++s)
-        if (pf[s] != p1[s] && p1[s] >= 0 && p1[s] < level1) ++freq[p1[s]][pf[s]];
+        if (pf[s] != p1[s] && p1[s] >= 0 && p1[s] < level1) pr.push_back((long long)p1[s] * P + pf[s]);
+    std::sort(pr.begin(), pr.end());
     std::vector<int> cand((size_t)level1 * ncand, -1);
-    for (int p = 0; p < level1; ++p) {
-        std::vector<std::pair<int, int>> v;   // (-count, basis)
-        for (auto &kv : freq[p]) v.push_back({-kv.second, kv.first});
-        std::sort(v.begin(), v.end());
-        for (int i = 0; i < (int)v.size() && i < ncand; ++i) cand[(size_t)p * ncand + i] = v[i].second;
+    std::vector<std::pair<int, int>> v;   // (-count, basis) of one level-1 pick
+    for (size_t a = 0; a < pr.size();) {
+        const long long p = pr[a] / P;
+        v.clear();
+        while (a < pr.size() && pr[a] / P == p) {
+            size_t b = a;
+            while (b < pr.size() && pr[b] == pr[a]) ++b;
+            v.push_back({-(int)(b - a), (int)(pr[a] % P)});
+            a = b;
+        }
+        const size_t nk = std::min<size_t>(v.size(), ncand);
+        std::partial_sort(v.begin(), v.begin() + nk, v.end());
+        for (size_t i = 0; i < nk; ++i) cand[(size_t)p * ncand + i] = v[i].second;
     }
     if (getenv("TWOSD_DEBUG")) {
         int diff = 0, filled = 0;

@@ -26,6 +26,7 @@ struct PoolBasis {
     std::vector<double> rval;
     bool dev_only = false;        // built on the device (refresh): rptr / rcol / rval / pi0 are
                                   // fetched from the pool arrays when the host needs them
+    int hb_row = -1;              // >= 0: head not materialised yet; row of c->pool_hb (4 head + type)
 };
 
 }  // namespace twosd
@@ -171,6 +172,8 @@ struct twosd_ctx {
     size_t gs_seg_cap = 0;
     // pinned host staging buffers of the pool upload, kept across uploads (no page faults,
     // no unmapping per refresh, page-locked copies)
+    int *pool_hb = nullptr;       // pinned: the heads of the last device-built pool (P x MP, 4 head + type)
+    size_t pool_hb_cap = 0;
     void *stage[16] = {};
     size_t stage_bytes[16] = {};
     std::map<const void *, size_t> dcap;   // element capacity of grow-only device arrays (by member address)

@@ -192,6 +192,20 @@ def select_refresh_bases(keys, counts, reps, rank_of, max_pool):
     return np.asarray(rank_of)[pick].astype(np.int64), np.asarray(reps)[pick].astype(np.int64)
 
 
+def pack_positions(owner, G):
+    """Source id of every pick in the gathered table: 1 + its position among all packs, packs
+    in rank order, each pack in selection order (the primary is source 0)."""
+    owner = np.asarray(owner, dtype=np.int64)
+    if owner.size == 0:
+        return np.zeros(0, dtype=np.int64)
+    n_own = np.bincount(owner, minlength=G)
+    base = 1 + np.concatenate([[0], np.cumsum(n_own)[:-1]])
+    order = np.argsort(owner, kind="stable")
+    rank_in = np.empty(owner.size, dtype=np.int64)
+    rank_in[order] = np.arange(owner.size) - np.repeat(np.cumsum(n_own) - n_own, n_own)
+    return base[owner] + rank_in
+
+
 def _allgather_1d(arr: np.ndarray, device=None):
     """Rank-order concatenation of every rank's 1-D array (variable lengths) and the length of
     each part.  Host arrays; over RCCL they travel as device tensors."""
@@ -242,14 +256,7 @@ def refresh_sharded(ctx, train_epi, x, first, count, max_pool, level1=0, ncand=0
     rank_of = np.repeat(np.arange(G), ns)
     owner, orep = select_refresh_bases(all_keys, all_counts, all_reps, rank_of, max_pool)
     mine = orep[owner == rank]
-    # source id of a pick: 1 + its position among all packs (rank-major, selection order)
-    n_own = np.bincount(owner, minlength=G) if owner.size else np.zeros(G, dtype=np.int64)
-    base = 1 + np.concatenate([[0], np.cumsum(n_own)[:-1]])
-    pos = np.zeros(owner.size, dtype=np.int64)
-    seen = np.zeros(G, dtype=np.int64)
-    for i, r in enumerate(owner):
-        pos[i] = base[r] + seen[r]
-        seen[r] += 1
+    pos = pack_positions(owner, G)
     t.append(time.perf_counter())
     nbytes = ctx.refresh_build_local(mine)
     t.append(time.perf_counter())

@@ -88,13 +88,7 @@ def main():
         owner, orep = sdist.select_refresh_bases(kk, cc, ff, rk_of, POOL)
         box_lo = np.min([l[3] for l in lists], axis=0)
         box_hi = np.max([l[4] for l in lists], axis=0)
-        n_own = np.bincount(owner, minlength=G)
-        base = 1 + np.concatenate([[0], np.cumsum(n_own)[:-1]])
-        pos = np.zeros(owner.size, dtype=np.int64)
-        seen = np.zeros(G, dtype=np.int64)
-        for i, o in enumerate(owner):
-            pos[i] = base[o] + seen[o]
-            seen[o] += 1
+        pos = sdist.pack_positions(owner, G)
         t_sel = 1e3 * (time.perf_counter() - t)
         nbytes = []
         for r, rk in enumerate(ranks):
@@ -127,8 +121,7 @@ def main():
         return ms, nbytes, int(ranks[0]["ctx"].pool_size())
 
     def solve_cut(rk, xx):
-        t = time.perf_counter()
-        rk["ctx"].invalidate_x()
+        t = time.perf_counter()      # the refresh prepared x (its candidate picks): no invalidate
         twosd.solve_push(rk["epi"], xx, 0, rk["n"], want_obj=False)
         rk["V"].truncate(nv)
         piv = rk["ctx"].lp_stats()[0] / rk["n"]
