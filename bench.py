@@ -247,9 +247,13 @@ def main():
     # B^-1 composition, upload grow with the pool), so a smaller shard takes a smaller pool
     # a distributed refresh builds one pool for all ranks, so it is sized by the whole batch
     dist_refresh = world > 1 and args.refresh_dist == 1
+    # pool size by the shard: 4096 per 1M scenarios on one rank, at least 512; the distributed
+    # refresh builds twice that (at least 1024): its training and composition are split over the
+    # ranks (profiles/r03/shard_emulate_pool*.txt: at N = 8, 1024-4096 bases all give a
+    # 31-35 ms per-rank step, 1024 the least)
     if args.refresh_pool <= 0:
-        scope = N if dist_refresh else n_local * E
-        args.refresh_pool = max(512, min(4096, int(4096 * scope / 1_000_000) // 256 * 256))
+        scope = 2 * n_local * E if dist_refresh else n_local * E
+        args.refresh_pool = max(1024 if dist_refresh else 512, min(4096, int(4096 * scope / 1_000_000) // 256 * 256))
     if args.refresh_train <= 0:
         args.refresh_train = 4 * args.refresh_pool
     # pool refresh training scenarios (stream seed + 4; every rank holds all of them, or with

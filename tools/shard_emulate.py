@@ -9,7 +9,7 @@ point-to-point links in parallel) and added -- it is the one number not measured
 
 Per-rank step = the rank's own phases + the exchange estimate; reported per x point and as the
 max over ranks, next to N = 1 (one context holding everything, the bench's single-GPU step).
-Usage (GPU box): python tools/shard_emulate.py [G] [scenarios] [steps]
+Usage (GPU box): python tools/shard_emulate.py [G] [scenarios] [steps] [pool] [training scenarios]
 """
 import json
 import os
@@ -34,8 +34,10 @@ def main():
     G = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     N = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+    POOL = int(sys.argv[4]) if len(sys.argv) > 4 else 4096
+    TRAIN = int(sys.argv[5]) if len(sys.argv) > 5 else 4 * POOL
     seed = 20250219
-    POOL, TRAIN, L1, NC, NV = 4096, 16384, 128, 160, 4096
+    L1, NC, NV = 128, 160, 4096
     d = os.path.join(ROOT, "data", "smps", "storm")
     cor, tim, sto = smps.load_smps(d, "storm")
     sp2 = smps.get_smps_stage_template(cor, tim, 2)
@@ -144,7 +146,7 @@ def main():
         print(f"x{rows[-1][0]}: per-rank step max {rows[-1][1]:.2f} ms (mean {rows[-1][2]:.2f}), pivots {rows[-1][3]:.2f}, "
               f"pool {P}, pack {max(nbytes) / 1e6:.1f} MB, slowest rank {rows[-1][5]}", flush=True)
     step_ms = float(np.mean([r[1] for r in rows]))
-    print(json.dumps({"G": G, "scenarios": N, "per_rank_step_ms": step_ms,
+    print(json.dumps({"G": G, "scenarios": N, "pool": POOL, "train": TRAIN, "per_rank_step_ms": step_ms,
                       "subproblems_per_s_projected": N / (step_ms * 1e-3),
                       "note": f"emulated on one GPU; xGMI all-gather estimated at {LINK_GBS} GB/s per link"}), flush=True)
 
