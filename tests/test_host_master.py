@@ -130,3 +130,28 @@ def test_check_first_stage_feasible():
     assert master.check_first_stage_feasible(sp1, np.array([3.0, 3.0, 3.0, 3.0]))
     assert not master.check_first_stage_feasible(sp1, np.zeros(4))        # sum x >= 12 violated
     assert not master.check_first_stage_feasible(sp1, np.array([-1.0, 5.0, 5.0, 5.0]))
+
+
+def test_degenerate_master_multipliers_are_central():
+    """Parity note for cut removal (algorithm.jl:57-72): with two identical cuts tight
+    at the master optimum the dual is not unique.  The host IPM returns the central split
+    (each row half of the multiplier one cut alone gets), where a simplex-type solver (the
+    reference's CPLEX / GLPK) returns a vertex (all on one row).  The sum is what is unique, and
+    it is what this asserts; which duplicate a vertex solver keeps is solver-dependent, so this
+    part of the trajectory is unpinned."""
+    from sqlp_amd import master
+    # min 1/2 x^2 - 1/2 x + eta  s.t.  eta >= 2 - x (twice), eta >= 0, 0 <= x <= 10:
+    # x* = 1.5, eta* = 0.5, only the cut is tight (multiplier 1)
+    H = np.array([1.0, 0.0])
+    g = np.array([-0.5, 1.0])
+    G = np.array([[-1.0, -1.0], [-1.0, -1.0], [0.0, -1.0], [-1.0, 0.0], [1.0, 0.0]])
+    h = np.array([-2.0, -2.0, 0.0, 0.0, 10.0])
+    one = master.qp_solve(H, g, None, None, np.delete(G, 1, axis=0), np.delete(h, 1))
+    two = master.qp_solve(H, g, None, None, G, h)
+    assert one.status == two.status == master.OPTIMAL
+    np.testing.assert_allclose(two.z, [1.5, 0.5], atol=1e-7)
+    np.testing.assert_allclose(one.z, [1.5, 0.5], atol=1e-7)
+    lam1, lam2 = one.lam[0], two.lam[:2]
+    assert lam1 == pytest.approx(1.0, rel=1e-6)
+    assert lam2.sum() == pytest.approx(lam1, rel=1e-6)
+    assert lam2[0] == pytest.approx(lam2[1], rel=1e-6)        # central: split evenly
