@@ -136,9 +136,6 @@ constexpr int EG = TWOSD_ETA_G;
 #ifndef TWOSD_REC_UNROLL
 #define TWOSD_REC_UNROLL 1
 #endif
-#ifndef TWOSD_HARRIS2_ORDER
-#define TWOSD_HARRIS2_ORDER 0
-#endif
 #ifndef TWOSD_HYPER_WPE
 #define TWOSD_HYPER_WPE(R) ((R) >= 9 ? 2 : 3)
 #endif
@@ -465,13 +462,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                     if (c >= C) break;
                     if (!(elm & (1ull << c))) continue;
                     const double a = sg * av[u];
-#if TWOSD_HARRIS2_ORDER
-                    // |alpha| test first: the division only for a column that would win on |alpha|
-                    // (same result: both conditions must hold, neither has side effects)
-                    if (fabs(a) > bA && d[c] / a <= thmax) { bA = fabs(a); bq = 64 * c + lane; bD = d[c]; bAs = a; }
-#else
                     if (d[c] / a <= thmax && fabs(a) > bA) { bA = fabs(a); bq = 64 * c + lane; bD = d[c]; bAs = a; }
-#endif
                 }
             }
             const ArgBest eq = warg_max(bA, bq, bD, bAs);
