@@ -255,7 +255,8 @@ static int solve_one(const lp_t *L, const int *head0, const double *B0inv, const
             int atlb = (j < n) || (L->sense[j - n] == 'L');
             if (atlb ? (a > TOL_PIV) : (a < -TOL_PIV)) {
                 double d = var_cost(L, j) - col_dot(L, j, W->pi);
-                if (d / a <= theta_max && fabs(a) > amax) { amax = fabs(a); q = j; dq = d; aq_s = a; }
+                /* d / a <= theta_max as a product (a != 0, sign known): the kernel's form */
+                if ((a > 0.0 ? d <= theta_max * a : d >= theta_max * a) && fabs(a) > amax) { amax = fabs(a); q = j; dq = d; aq_s = a; }
             }
         }
         if (q < 0) { status = ST_NUMERIC; break; }

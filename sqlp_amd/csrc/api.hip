@@ -239,7 +239,7 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_kslot); dfree(c->d_kix); dfree(c->d_kv); dfree(c->d_kcoef); c->k_valid = false;
     dfree(c->d_sel_end); dfree(c->d_kp); dfree(c->d_ke); dfree(c->d_kraw); dfree(c->d_xaux); c->xaux_cap = 0; c->sel_cap_total = 0;
     dfree(c->d_d0); dfree(c->d_eidx); dfree(c->d_evals); dfree(c->d_stamps);
-    dfree(c->d_wr_col); dfree(c->d_wr_val); dfree(c->d_wr_ocol); dfree(c->d_wr_oval); dfree(c->d_bcp); dfree(c->d_bci); dfree(c->d_bcv);
+    dfree(c->d_wr_col); dfree(c->d_wr_val); dfree(c->d_wr_ocol); dfree(c->d_wr_oval); dfree(c->d_wcp); dfree(c->d_wcc); dfree(c->d_wcv); dfree(c->d_bcp); dfree(c->d_bci); dfree(c->d_bcv);
     dfree(c->d_brptr); dfree(c->d_brcol); dfree(c->d_brval);
     c->earena_slots = 0; c->earena_cap = 0;
     for (auto &e : c->epis) { dfree(e.d_dv); dfree(e.d_w); }
@@ -375,6 +375,13 @@ extern "C" int twosd_set_template(twosd_ctx *c, int m2, int n1, int n2, const in
         if ((rc = upload(&c->d_wr_ocol, oc)) || (rc = upload(&c->d_wr_oval, ov))) return rc;
         c->wr_width = wr;
         if ((rc = upload(&c->d_wr_col, wc)) || (rc = upload(&c->d_wr_val, wv))) return rc;
+        std::vector<int> cp(m2 + 1, 0), cc;
+        std::vector<double> cv;
+        for (int i = 0; i < m2; ++i) {
+            for (auto &e : rows[i]) { cc.push_back(e.first); cv.push_back(e.second); }
+            cp[i + 1] = (int)cc.size();
+        }
+        if ((rc = upload(&c->d_wcp, cp)) || (rc = upload(&c->d_wcc, cc)) || (rc = upload(&c->d_wcv, cv))) return rc;
     }
     c->has_template = true;
     c->k = 0;
@@ -2179,6 +2186,7 @@ int twosd::run_lp_ex(twosd_ctx *c, const double *x, const double *d_dv, int N, c
         H.colptr = c->d_colptr; H.rowidx = c->d_rowidx; H.val = c->d_val; H.q = c->d_q; H.btype = c->d_btype;
         H.wr_width = c->wr_width; H.wr_col = c->d_wr_col; H.wr_val = c->d_wr_val;
         H.wr_ocol = c->d_wr_ocol; H.wr_oval = c->d_wr_oval;
+        H.wcp = c->d_wcp; H.wcc = c->d_wcc; H.wcv = c->d_wcv;
         H.bcp = c->d_bcp; H.bci = c->d_bci; H.bcv = c->d_bcv;
         H.brptr = c->d_brptr; H.brcol = c->d_brcol; H.brval = c->d_brval;
         H.kslot = c->d_kslot; H.kix = c->d_kix; H.kv = c->d_kv; H.kcoef = c->d_kcoef;

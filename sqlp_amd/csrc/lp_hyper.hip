@@ -65,6 +65,70 @@ __device__ __forceinline__ void h_wave_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// scatter-add into the wave's own LDS slice: ds_add_f64, no return value, so no read-modify-write
+// latency chain.  One wave owns the slice and its LDS instructions execute in program order, so
+// every address accumulates its terms in a fixed order (deterministic), each term rounded once
+// as a product and once in the sum -- the arithmetic of the C oracle's dot products.
+__device__ __forceinline__ void lds_add(double *p, double v) {
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+// inclusive scans over the 64 lanes: DPP row shifts within each 16-lane row (lanes shifted in
+// from outside the row read 0, bound_ctrl), then the carries of the rows before (v_readlane)
+template <int K>
+__device__ __forceinline__ int h_row_shr(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x110 + K, 0xF, 0xF, true);
+}
+__device__ __forceinline__ int h_scan_add(int v, int lane) {
+    v += h_row_shr<1>(v);
+    v += h_row_shr<2>(v);
+    v += h_row_shr<4>(v);
+    v += h_row_shr<8>(v);
+    const int r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31), r2 = __builtin_amdgcn_readlane(v, 47);
+    return v + (lane >= 16 ? r0 : 0) + (lane >= 32 ? r1 : 0) + (lane >= 48 ? r2 : 0);
+}
+__device__ __forceinline__ int h_scan_max(int v, int lane) {   // v >= 0
+    v = max(v, h_row_shr<1>(v));
+    v = max(v, h_row_shr<2>(v));
+    v = max(v, h_row_shr<4>(v));
+    v = max(v, h_row_shr<8>(v));
+    const int r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31), r2 = __builtin_amdgcn_readlane(v, 47);
+    const int c = lane >= 48 ? max(max(r0, r1), r2) : lane >= 32 ? max(r0, r1) : lane >= 16 ? r0 : 0;
+    return max(v, c);
+}
+// Segmented scatter-add: lane j holds a row (entries p0 .. p0 + len - 1 of cidx / cval) and its
+// multiplier v; target[cidx[p]] += v * cval[p] over every entry of every row.  The rows are laid
+// end to end and consumed 64 entries per wave step (lane l: entry c0 + l), so a row of a few
+// entries does not occupy a whole step.  A lane finds its row as the last row start at or
+// before its entry (starts marked in the LDS scratch smark[64], all zero on entry and on exit,
+// then a max-scan over lanes).  Rows go in lane order across steps; entries of different rows
+// that meet in one address within a step are added by one ds_add_f64 in a fixed hardware order.
+// Returns the number of entries.
+__device__ __forceinline__ int h_seg_scatter(int p0, int len, double v, const int *__restrict__ cidx,
+                                             const double *__restrict__ cval, double *target, int *smark, int lane) {
+    const int incl = h_scan_add(len, lane);
+    const int excl = incl - len;
+    const int T = __builtin_amdgcn_readlane(incl, 63);
+    const int dd = p0 - excl;   // entry e of the concatenation sits at cidx[dd_row + e]
+    int carry = 0;
+    for (int c0 = 0; c0 < T; c0 += 64) {
+        if (len > 0 && excl >= c0 && excl < c0 + 64) smark[excl - c0] = lane + 1;
+        h_wave_sync();
+        int mv = smark[lane];
+        smark[lane] = 0;
+        mv = h_scan_max(mv, lane);
+        mv = mv > carry ? mv : carry;
+        carry = __builtin_amdgcn_readlane(mv, 63);
+        const int j = mv > 0 ? mv - 1 : 0;
+        const int dj = __builtin_amdgcn_ds_bpermute(4 * j, dd);
+        const uint64_t vb = (uint64_t)__double_as_longlong(v);
+        const uint32_t vlo = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * j, (int)(uint32_t)vb);
+        const uint32_t vhi = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * j, (int)(uint32_t)(vb >> 32));
+        const double vj = __longlong_as_double((long long)(((uint64_t)vhi << 32) | vlo));
+        const int e = c0 + lane;
+        if (e < T) lds_add(&target[cidx[dj + e]], vj * cval[dj + e]);
+    }
+    return T;
+}
 __device__ __forceinline__ double h_infeas(double x, int bt) {
     if (bt == BT_Y || bt == BT_L) return x < -HTOL_P ? x : 0.0;
     if (bt == BT_G) return x > HTOL_P ? x : 0.0;
@@ -90,19 +154,19 @@ __device__ __forceinline__ int h_prefix_count(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
-// per-wave LDS slice: a union of {ut, rho} (MP doubles each) and alpha (64C doubles, the
-// pivot row over all columns during pricing), the scenario deltas (k doubles), etap (u16),
-// etaoff (int)
-// (alpha spans the ncol = n + m real columns), the scenario deltas (k doubles), the dual
-// Devex weights (MP floats), etap (u16), etaoff (int)
+// per-wave LDS slice: a union of {ut, rho} (MP doubles each) and alpha (the pivot row over the
+// ncol = n + m real columns during pricing), the scenario deltas (k doubles), the pricing list
+// values (64 doubles), the dual Devex weights (MP floats), the pricing list rows and row-start
+// marks (64 ints each), etap (u16), etaoff (int)
 static __host__ __device__ inline int hyper_union_doubles(int R, int ncol) {
     const int a = (ncol + 1) & ~1;
     return 128 * R > a ? 128 * R : a;
 }
+// + the pricing list: the nonzeros of rho, (row, value), 64 per batch, and its row-start marks
 static __host__ __device__ inline size_t hyper_slice_bytes(int R, int ncol, int kmax, int k) {
     const int kmaxp = (kmax + 3) & ~3;
-    return 8 * (size_t)hyper_union_doubles(R, ncol) + 8 * (size_t)((k + 1) & ~1) + 4 * (size_t)(64 * R) + 2 * kmaxp +
-           4 * (kmaxp + 4);
+    return 8 * (size_t)hyper_union_doubles(R, ncol) + 8 * (size_t)((k + 1) & ~1) + 8 * 64 + 4 * (size_t)(64 * R) + 4 * 64 +
+           4 * 64 + 2 * kmaxp + 4 * (kmaxp + 4);
 }
 size_t hyper_lds_bytes(int R, int ncol, int kmax, int k) { return (size_t)kWavesPerBlock * hyper_slice_bytes(R, ncol, kmax, k); }
 
@@ -117,13 +181,21 @@ size_t hyper_lds_bytes(int R, int ncol, int kmax, int k) { return (size_t)kWaves
 #define TWOSD_PRICE_G 4
 #endif
 constexpr int EG = TWOSD_ETA_G;
-// alpha~ slots read together in the Harris passes
-#ifndef TWOSD_HARRIS_B
-#define TWOSD_HARRIS_B 1
+// scatters into LDS (pricing, rho, FTRAN) as ds_add_f64 (1) or as read-fma-write chains (0)
+#ifndef TWOSD_LDS_ADD
+#define TWOSD_LDS_ADD 1
 #endif
-// HB = 1: alpha~ read TWOSD_HARRIS_PF slots ahead (software pipelined; 0 = off)
-#ifndef TWOSD_HARRIS_PF
-#define TWOSD_HARRIS_PF 1
+// pricing as a segmented scatter, 64 W entries per wave step (1), or one W row per step (0)
+#ifndef TWOSD_PRICE_SEG
+#define TWOSD_PRICE_SEG 1
+#endif
+// FTRAN: B0^{-1} a_q as one segmented scatter (1) or column group by column group (0)
+#ifndef TWOSD_FTRAN_SEG
+#define TWOSD_FTRAN_SEG 1
+#endif
+// rho = u' B0^{-1} as one segmented scatter (1) or row group by row group (0)
+#ifndef TWOSD_RHO_SEG
+#define TWOSD_RHO_SEG 1
 #endif
 // unroll of the per-scenario gathers (x_B warm start, vertex recovery): loads in flight
 #ifndef TWOSD_XB_UNROLL
@@ -152,8 +224,11 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
     double *rho = ut + MP;                                  // pivot row of B^{-1}
     double *alpha = ut;                                     // pricing: alpha~_j over the same space
     double *dvl = ut + hyper_union_doubles(R, ncol);        // this scenario's coef_e(x) dv_e
-    float *w = reinterpret_cast<float *>(dvl + ((P.k + 1) & ~1));   // dual Devex weights (row i at w[i])
-    unsigned short *etap = reinterpret_cast<unsigned short *>(w + MP);
+    double *lstv = dvl + ((P.k + 1) & ~1);                  // pricing list: rho values
+    float *w = reinterpret_cast<float *>(lstv + 64);        // dual Devex weights (row i at w[i])
+    int *lsti = reinterpret_cast<int *>(w + MP);            // pricing list: rows
+    int *smark = lsti + 64;                                 // pricing: row starts within a wave step
+    unsigned short *etap = reinterpret_cast<unsigned short *>(smark + 64);
     int *etaoff = reinterpret_cast<int *>(etap + kmaxp);
 
     const int m = P.m, n = P.n;
@@ -174,6 +249,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         }
     };
     for (int j = lane; j < hyper_union_doubles(R, ncol); j += 64) ut[j] = 0.0;
+    smark[lane] = 0;
     h_wave_sync();
     STAMP_DECL
 
@@ -246,7 +322,9 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
 
         for (;;) {
             // ---- 1. leaving row (dual Devex: max infeas^2 / w, lowest row on ties)
-            double best = 0.0, bdel = 0.0;
+            // within the lane the rows are compared as fractions (dl^2 * w_best > best_num * w:
+            // no division per row), one division for the lane's winner
+            double bnum = 0.0, bden = 1.0, bdel = 0.0;
             int br = 0x7fffffff;
 #pragma unroll
             for (int t = 0; t < R; ++t) {
@@ -257,11 +335,11 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 const bool inf = (hb[t] >= 0) & (((xB[t] < -HTOL_P) & (bt != BT_G)) | ((xB[t] > HTOL_P) & ((bt & 1) != 0)));
                 if (inf) {
                     const double dl = xB[t];
-                    const double sc = dl * dl / (double)w[64 * t + lane];
-                    if (sc > best) { best = sc; br = 64 * t + lane; bdel = dl; }
+                    const double num = dl * dl, den = (double)w[64 * t + lane];
+                    if (num * bden > bnum * den) { bnum = num; bden = den; br = 64 * t + lane; bdel = dl; }
                 }
             }
-            const ArgBest lr = warg_max(best, br, bdel, 0.0);
+            const ArgBest lr = warg_max(bnum / bden, br, bdel, 0.0);
             const int r = lr.idx;
             STAMP(1)
             if (lr.key == 0.0) break;
@@ -302,6 +380,31 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             // rho = u' B0^{-1} as a row scatter over the nonzeros of u, which sit at r and at
             // the eta pivot rows; each row is consumed once (then zeroed), in the fixed order
             // r, etap[K-1], ..., etap[0], so the accumulation order is deterministic.
+#if TWOSD_RHO_SEG
+            // as one segmented scatter over the rows of u in that order, 64 rows per batch; a row
+            // that appears again later (pivoted more than once) contributes at its first position
+            // only, as the zeroing does in the row-by-row form
+            for (int b0 = 0; b0 <= K; b0 += 64) {
+                const int jj = b0 + lane;
+                const int gp = jj <= K ? (jj == 0 ? r : (int)etap[K - jj]) : -1;
+                const int nbt = K + 1 - b0 < 64 ? K + 1 - b0 : 64;
+                bool dup = false;
+                for (int i = 0; i < nbt - 1; ++i) dup |= (i < lane) & (__builtin_amdgcn_readlane(gp, i) == gp);
+                double up = 0.0;
+                int p0 = 0, len = 0;
+                if (gp >= 0 && !dup) {
+                    up = ut[gp];
+                    if (up != 0.0) {
+                        p0 = brptr[gp];
+                        len = brptr[gp + 1] - p0;
+                    }
+                }
+                nops += h_seg_scatter(p0, len, up, P.brcol, P.brval, rho, smark, lane);
+                h_wave_sync();
+                if (gp >= 0) ut[gp] = 0.0;
+                h_wave_sync();
+            }
+#else
             for (int tg = K; tg >= 0; tg -= EG) {
                 int gi[EG], gn[EG], gp[EG], go[EG];
                 double gv[EG];
@@ -322,9 +425,14 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                     if (tt < 0) break;
                     const double up = ut[gp[g]];
                     if (up != 0.0) {
+#if TWOSD_LDS_ADD
+                        if (lane < gn[g]) lds_add(&rho[gi[g]], up * gv[g]);
+                        for (int e = 64 + lane; e < gn[g]; e += 64) lds_add(&rho[P.brcol[go[g] + e]], up * P.brval[go[g] + e]);
+#else
                         if (lane < gn[g]) rho[gi[g]] = fma(up, gv[g], rho[gi[g]]);
                         for (int e = 64 + lane; e < gn[g]; e += 64)
                             rho[P.brcol[go[g] + e]] = fma(up, P.brval[go[g] + e], rho[P.brcol[go[g] + e]]);
+#endif
                         nops += gn[g];
                         h_wave_sync();
                         if (lane == 0) ut[gp[g]] = 0.0;
@@ -332,13 +440,12 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                     h_wave_sync();
                 }
             }
+#endif
             STAMP(3)
 
-            // ---- 3. pricing: alpha~_j = rho' a_j for every column as a row-wise scatter over
-            // the nonzeros of rho (2-5 % of the rows).  Rows go in ascending order, one row per
-            // wave step (its columns are distinct lanes), so alpha_j accumulates over i
-            // ascending: the same FMAs in the same order as a column-wise gather.  alpha lives
-            // in LDS over the ut/rho space (both zero here once rho is in registers).
+            // ---- 3. pricing: alpha~_j = rho' a_j for every column as a scatter over the nonzeros
+            // of rho (~6 % of the rows on storm).  alpha lives in LDS over the ut/rho space (both
+            // zero here once rho is in registers).
             double rv[R];
 #pragma unroll
             for (int t = 0; t < R; ++t) rv[t] = rho[64 * t + lane];
@@ -346,90 +453,114 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
 #pragma unroll
             for (int t = 0; t < R; ++t) rho[64 * t + lane] = 0.0;
             h_wave_sync();
-            // W rows as row-ELL of width WR <= 64 (padding column -1): one load round trip serves
-            // a group of 8 rows.  A row longer than 64 keeps 63 entries here; slot 63 holds
-            // column -2 - o and value n_rest: its remaining entries sit in an overflow CSR at o.
-            const int WR = P.wr_width;
+#if TWOSD_PRICE_SEG
+            // Segmented: the nonzero rows of rho (ascending) are compacted into the LDS list, 64
+            // per batch, and the batch's W rows (CSR) scattered 64 entries per wave step
+            // (h_seg_scatter; a row of ~6 entries no longer occupies a whole step).
+            {
+                uint64_t mk[R];
+                int tot = 0;
 #pragma unroll
-            for (int t = 0; t < R; ++t) {
-                uint64_t msk = __ballot(rv[t] != 0.0);
-                while (msk) {
-                    constexpr int G = TWOSD_PRICE_G;
-                    int gi[G], gc[G];
-                    double gr[G], gw[G];
+                for (int t = 0; t < R; ++t) {
+                    mk[t] = __ballot(rv[t] != 0.0);
+                    tot += __popcll(mk[t]);
+                }
+                for (int b0 = 0; b0 < tot; b0 += 64) {
+                    int base = -b0;
 #pragma unroll
-                    for (int g = 0; g < G; ++g) {
-                        gi[g] = -1; gc[g] = -1; gr[g] = 0.0; gw[g] = 0.0;
-                        if (msk) {
-                            const int l = __builtin_ctzll(msk);
-                            msk &= msk - 1;
-                            gi[g] = 64 * t + l;
-                            gr[g] = readlane_dbl(rv[t], l);
-                            if (lane < WR) { gc[g] = P.wr_col[(size_t)gi[g] * WR + lane]; gw[g] = P.wr_val[(size_t)gi[g] * WR + lane]; }
+                    for (int t = 0; t < R; ++t) {
+                        const int pos = base + h_prefix_count(mk[t]);
+                        if (rv[t] != 0.0 && pos >= 0 && pos < 64) {
+                            lsti[pos] = 64 * t + lane;
+                            lstv[pos] = rv[t];
                         }
+                        base += __popcll(mk[t]);
                     }
+                    h_wave_sync();
+                    const int nb = tot - b0 < 64 ? tot - b0 : 64;
+                    int p0 = 0, len = 0;
+                    double gr = 0.0;
+                    if (lane < nb) {
+                        const int gi = lsti[lane];
+                        gr = lstv[lane];
+                        p0 = P.wcp[gi];
+                        len = P.wcp[gi + 1] - p0;
+                        alpha[n + gi] = gr;   // slack of row i: entry 1 in row i only
+                    }
+                    nops += h_seg_scatter(p0, len, gr, P.wcc, P.wcv, alpha, smark, lane) + nb;
+                    h_wave_sync();   // the list is rewritten by the next batch
+                }
+            }
+#else
+            // Row by row: one W row (row-ELL of width WR <= 64, padding column -1) per wave step,
+            // rows ascending, PRICE_G rows per load round trip.  A row longer than 64 keeps 63
+            // entries here; slot 63 holds column -2 - o and value n_rest: its remaining entries
+            // sit in an overflow CSR at o.
+            {
+                const int WR = P.wr_width;
+                constexpr int G = TWOSD_PRICE_G;
 #pragma unroll
-                    for (int g = 0; g < G; ++g) {
-                        if (gi[g] < 0) break;
-                        if (gc[g] >= 0) alpha[gc[g]] = fma(gr[g], gw[g], alpha[gc[g]]);
-                        if (__ballot(gc[g] < -1)) {   // long row (rare): the rest, columns ascending
-                            const int o = -2 - __builtin_amdgcn_readlane(gc[g], 63);
-                            const int nr = (int)readlane_dbl(gw[g], 63);
-                            h_wave_sync();
-                            for (int e = lane; e < nr; e += 64) {
-                                const int cc = P.wr_ocol[o + e];
-                                alpha[cc] = fma(gr[g], P.wr_oval[o + e], alpha[cc]);
+                for (int t = 0; t < R; ++t) {
+                    uint64_t msk = __ballot(rv[t] != 0.0);
+                    while (msk) {
+                        int gi[G], gc[G];
+                        double gr[G], gw[G];
+#pragma unroll
+                        for (int g = 0; g < G; ++g) {
+                            gi[g] = -1; gc[g] = -1; gr[g] = 0.0; gw[g] = 0.0;
+                            if (msk) {
+                                const int l = __builtin_ctzll(msk);
+                                msk &= msk - 1;
+                                gi[g] = 64 * t + l;
+                                gr[g] = readlane_dbl(rv[t], l);
+                                if (lane < WR) { gc[g] = P.wr_col[(size_t)gi[g] * WR + lane]; gw[g] = P.wr_val[(size_t)gi[g] * WR + lane]; }
                             }
                         }
-                        if (lane == 0) alpha[n + gi[g]] = gr[g];   // slack of row i: entry 1 in row i only
-                        nops += WR + 1;
-                        h_wave_sync();
+#pragma unroll
+                        for (int g = 0; g < G; ++g) {
+                            if (gi[g] < 0) break;
+                            if (gc[g] >= 0) lds_add(&alpha[gc[g]], gr[g] * gw[g]);
+                            if (__ballot(gc[g] < -1)) {   // long row (rare): the rest, columns ascending
+                                const int o = -2 - __builtin_amdgcn_readlane(gc[g], 63);
+                                const int nr = (int)readlane_dbl(gw[g], 63);
+                                for (int e = lane; e < nr; e += 64) lds_add(&alpha[P.wr_ocol[o + e]], gr[g] * P.wr_oval[o + e]);
+                            }
+                            if (lane == 0) alpha[n + gi[g]] = gr[g];   // slack of row i: entry 1 in row i only
+                            nops += WR + 1;
+                        }
                     }
                 }
             }
+#endif
+            h_wave_sync();
             STAMP(4)
 
-            // Harris ratio test over the nonbasic columns (d in registers, alpha~ from LDS).  The
-            // alpha~ of HB slots are read together (unconditionally: masked slots are ignored), so
-            // HB LDS reads are in flight per wait instead of one
-            constexpr int HB = TWOSD_HARRIS_B;
+            // Harris ratio test over the nonbasic columns (d in registers, alpha~ from LDS); the
+            // alpha~ of slot c + 1 is read while slot c is tested (software pipelined)
+            // pass 1: thmax = min over the eligible columns of (d_j +- tol) / |alpha_j|, compared as
+            // fractions within the lane (nu * den_best < nu_best * den), one division per lane
             const double sg = delta > 0 ? 1.0 : -1.0;
-            double thmax = INFINITY;
+            double bnu = INFINITY, bde = 1.0;
             uint64_t nzm = 0, elm = 0;
-            double apf = TWOSD_HARRIS_PF ? alpha[lane] : 0.0;   // slot c + 1 (+ 2) read while slot c is tested
-            double apf2 = (TWOSD_HARRIS_PF > 1 && C > 1) ? alpha[64 + lane] : 0.0;
+            double apf = alpha[lane];
 #pragma unroll
-            for (int c0 = 0; c0 < C; c0 += HB) {
-                double av[HB];
-                if constexpr (TWOSD_HARRIS_PF && HB == 1) {
-                    av[0] = apf;
-                    if (TWOSD_HARRIS_PF > 1) {
-                        apf = apf2;
-                        if (c0 + 2 < C) apf2 = alpha[64 * (c0 + 2) + lane];
-                    } else if (c0 + 1 < C) {
-                        apf = alpha[64 * (c0 + 1) + lane];
-                    }
-                } else {
-#pragma unroll
-                for (int u = 0; u < HB; ++u) av[u] = (HB == 1 || c0 + u < C) ? alpha[64 * (c0 + u) + lane] : 0.0;
-                }
-#pragma unroll
-                for (int u = 0; u < HB; ++u) {
-                    const int c = c0 + u;
-                    if (c >= C) break;
-                    const uint64_t bit = 1ull << c;
-                    if (bmask & bit) continue;
-                    const double a = sg * av[u];
-                    if (a != 0.0) nzm |= bit;   // fixed columns too: their d_j (slack: -pi_i) stay current
-                    if (fixedm & bit) continue;
-                    const bool atlb = !(ubm & bit);
-                    if (atlb ? a > HTOL_PIV : a < -HTOL_PIV) {
-                        elm |= bit;
-                        thmax = fmin(thmax, ((atlb ? d[c] + HTOL_D : d[c] - HTOL_D)) / a);
-                    }
+            for (int c = 0; c < C; ++c) {
+                const double av = apf;
+                if (c + 1 < C) apf = alpha[64 * (c + 1) + lane];
+                const uint64_t bit = 1ull << c;
+                if (bmask & bit) continue;
+                const double a = sg * av;
+                if (a != 0.0) nzm |= bit;   // fixed columns too: their d_j (slack: -pi_i) stay current
+                if (fixedm & bit) continue;
+                const bool atlb = !(ubm & bit);
+                if (atlb ? a > HTOL_PIV : a < -HTOL_PIV) {
+                    elm |= bit;
+                    const double nu = atlb ? d[c] + HTOL_D : HTOL_D - d[c];
+                    const double de = fabs(a);
+                    if (nu * bde < bnu * de) { bnu = nu; bde = de; }
                 }
             }
-            thmax = wmin(thmax);
+            const double thmax = wmin(bnu / bde);
             if (thmax == INFINITY) {
                 status = TWOSD_LP_INFEASIBLE;
                 h_wave_sync();
@@ -438,32 +569,15 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             }
             double bA = 0.0, bD = 0.0, bAs = 0.0;
             int bq = 0x7fffffff;
-            apf = TWOSD_HARRIS_PF ? alpha[lane] : 0.0;
-            apf2 = (TWOSD_HARRIS_PF > 1 && C > 1) ? alpha[64 + lane] : 0.0;
+            apf = alpha[lane];
 #pragma unroll
-            for (int c0 = 0; c0 < C; c0 += HB) {
-                if (HB > 1 && !((elm >> c0) & ((1ull << HB) - 1))) continue;
-                double av[HB];
-                if constexpr (TWOSD_HARRIS_PF && HB == 1) {
-                    av[0] = apf;
-                    if (TWOSD_HARRIS_PF > 1) {
-                        apf = apf2;
-                        if (c0 + 2 < C) apf2 = alpha[64 * (c0 + 2) + lane];
-                    } else if (c0 + 1 < C) {
-                        apf = alpha[64 * (c0 + 1) + lane];
-                    }
-                } else {
-#pragma unroll
-                for (int u = 0; u < HB; ++u) av[u] = (HB == 1 || c0 + u < C) ? alpha[64 * (c0 + u) + lane] : 0.0;
-                }
-#pragma unroll
-                for (int u = 0; u < HB; ++u) {
-                    const int c = c0 + u;
-                    if (c >= C) break;
-                    if (!(elm & (1ull << c))) continue;
-                    const double a = sg * av[u];
-                    if (d[c] / a <= thmax && fabs(a) > bA) { bA = fabs(a); bq = 64 * c + lane; bD = d[c]; bAs = a; }
-                }
+            for (int c = 0; c < C; ++c) {
+                const double av = apf;
+                if (c + 1 < C) apf = alpha[64 * (c + 1) + lane];
+                if (!(elm & (1ull << c))) continue;
+                const double a = sg * av;
+                // d_j / a <= thmax, as a product (a != 0, its sign known)
+                if ((a > 0.0 ? d[c] <= thmax * a : d[c] >= thmax * a) && fabs(a) > bA) { bA = fabs(a); bq = 64 * c + lane; bD = d[c]; bAs = a; }
             }
             const ArgBest eq = warg_max(bA, bq, bD, bAs);
             const int q = eq.idx;
@@ -476,30 +590,12 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             }
             const double thetaD = eq.p0 / eq.p1;
             // d_j -= thetaD * alpha~_j for every nonbasic column with alpha_j != 0
-            apf = TWOSD_HARRIS_PF ? alpha[lane] : 0.0;
-            apf2 = (TWOSD_HARRIS_PF > 1 && C > 1) ? alpha[64 + lane] : 0.0;
+            apf = alpha[lane];
 #pragma unroll
-            for (int c0 = 0; c0 < C; c0 += HB) {
-                if (HB > 1 && !((nzm >> c0) & ((1ull << HB) - 1))) continue;
-                double av[HB];
-                if constexpr (TWOSD_HARRIS_PF && HB == 1) {
-                    av[0] = apf;
-                    if (TWOSD_HARRIS_PF > 1) {
-                        apf = apf2;
-                        if (c0 + 2 < C) apf2 = alpha[64 * (c0 + 2) + lane];
-                    } else if (c0 + 1 < C) {
-                        apf = alpha[64 * (c0 + 1) + lane];
-                    }
-                } else {
-#pragma unroll
-                for (int u = 0; u < HB; ++u) av[u] = (HB == 1 || c0 + u < C) ? alpha[64 * (c0 + u) + lane] : 0.0;
-                }
-#pragma unroll
-                for (int u = 0; u < HB; ++u) {
-                    const int c = c0 + u;
-                    if (c >= C) break;
-                    if (nzm & (1ull << c)) d[c] = fma(-thetaD, sg * av[u], d[c]);
-                }
+            for (int c = 0; c < C; ++c) {
+                const double av = apf;
+                if (c + 1 < C) apf = alpha[64 * (c + 1) + lane];
+                if (nzm & (1ull << c)) d[c] = fma(-thetaD, sg * av, d[c]);
             }
             h_wave_sync();
             zero_alpha();   // back to all-zero ut / rho
@@ -510,7 +606,22 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             // B0^{-1} under the nonzeros of a_q, lanes over a column's entries (distinct rows)
             {
                 const int np0 = q >= n ? 0 : P.colptr[q], np1 = q >= n ? 1 : P.colptr[q + 1];
-#if TWOSD_FTRAN_G > 1
+#if TWOSD_FTRAN_SEG
+                // the B0^{-1} columns under the nonzeros of a_q as one segmented scatter (lane j:
+                // nonzero np0 + j), 64 nonzeros per batch
+                for (int pw0 = np0; pw0 < np1; pw0 += 64) {
+                    const int pw = pw0 + lane;
+                    int p0 = 0, len = 0;
+                    double fa = 0.0;
+                    if (pw < np1) {
+                        const int cc = q >= n ? q - n : P.rowidx[pw];
+                        fa = q >= n ? 1.0 : P.val[pw];
+                        p0 = bcp[cc];
+                        len = bcp[cc + 1] - p0;
+                    }
+                    nops += h_seg_scatter(p0, len, fa, P.bci, P.bcv, ut, smark, lane);
+                }
+#elif TWOSD_FTRAN_G > 1
                 // the B0^{-1} columns of FG nonzeros of a_q per memory round trip (pointers and
                 // first 64 entries loaded together), applied in pw order as below
                 constexpr int FG = TWOSD_FTRAN_G;
@@ -532,6 +643,11 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
 #pragma unroll
                     for (int g = 0; g < FG; ++g) {
                         if (pw0 + g >= np1) break;
+#if TWOSD_LDS_ADD
+                        if (lane < fn[g]) lds_add(&ut[fi[g]], fa[g] * fv[g]);
+                        for (int e = 64 + lane; e < fn[g]; e += 64) lds_add(&ut[P.bci[fo[g] + e]], fa[g] * P.bcv[fo[g] + e]);
+                        nops += fn[g];
+#else
                         if (lane < fn[g]) ut[fi[g]] = fma(fa[g], fv[g], ut[fi[g]]);
                         for (int e = 64 + lane; e < fn[g]; e += 64) {
                             const int i = P.bci[fo[g] + e];
@@ -539,6 +655,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                         }
                         nops += fn[g];
                         h_wave_sync();
+#endif
                     }
                 }
 #else
@@ -555,6 +672,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 }
 #endif
             }
+            h_wave_sync();
             for (int tg = 0; tg < K; tg += EG) {
                 int gi[EG], gn[EG], go[EG];
                 double gv[EG];
@@ -575,12 +693,26 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                     const int p = etap[tt];
                     const double vp = ut[p];
                     if (vp != 0.0) {
+#if TWOSD_LDS_ADD
+                        // the pivot row p is replaced, the others accumulate (distinct rows)
+                        if (lane < gn[g]) {
+                            if (gi[g] == p) ut[p] = gv[g] * vp;
+                            else lds_add(&ut[gi[g]], gv[g] * vp);
+                        }
+                        for (int e = 64 + lane; e < gn[g]; e += 64) {
+                            const int i = eidx[go[g] + e];
+                            const double ev = evals[go[g] + e];
+                            if (i == p) ut[p] = ev * vp;
+                            else lds_add(&ut[i], ev * vp);
+                        }
+#else
                         if (lane < gn[g]) ut[gi[g]] = (gi[g] == p) ? gv[g] * vp : fma(gv[g], vp, ut[gi[g]]);
                         for (int e = 64 + lane; e < gn[g]; e += 64) {
                             const int i = eidx[go[g] + e];
                             const double ev = evals[go[g] + e];
                             ut[i] = (i == p) ? ev * vp : fma(ev, vp, ut[i]);
                         }
+#endif
                         nops += gn[g];
                     }
                     h_wave_sync();

@@ -98,6 +98,8 @@ struct twosd_ctx {
     int *d_wr_col = nullptr, *d_bcp = nullptr, *d_bci = nullptr;
     double *d_wr_val = nullptr, *d_bcv = nullptr;
     int *d_wr_ocol = nullptr;
+    int *d_wcp = nullptr, *d_wcc = nullptr;   // W by rows (CSR) for the segmented pricing scatter
+    double *d_wcv = nullptr;
     double *d_wr_oval = nullptr;
     int *d_brptr = nullptr, *d_brcol = nullptr;
     double *d_brval = nullptr;

@@ -32,6 +32,7 @@ struct HyperParams {
     int wr_width;                                       // W by rows as row-ELL (columns ascending, width
     const int *wr_col; const double *wr_val;            //   min(max row length, 64), padding column -1);
     const int *wr_ocol; const double *wr_oval;          //   long rows continue in an overflow CSR
+    const int *wcp, *wcc; const double *wcv;            // W by rows as CSR (columns ascending)
     const int *bcp, *bci; const double *bcv;            // B^{-1} CSC (MP + 1 column pointers, rows ascending)
     const int *brptr, *brcol; const double *brval;      // B^{-1} CSR (MP rows)
     // sliced ELL (entry e of slot s for lane l at [(slot_off[s] + e) * 64 + l]; padding: idx 0, val 0):
