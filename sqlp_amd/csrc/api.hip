@@ -706,7 +706,8 @@ extern "C" int twosd_pool_build(twosd_ctx *c, int epi, const double *x, int firs
     const EpiDevice &E = c->epis[epi];
     if (first < 0 || count < 0 || first + count > E.count || max_pool < 1 || (c->n1 > 0 && !x))
         return fail(TWOSD_E_ARG, "pool_build: bad arguments");
-    if (pool_select_lds_bytes(c->k) > 160 * 1024) return fail(TWOSD_E_UNSUPPORTED, "pool_build: k = %d random elements too many for pool selection", c->k);
+    if (pool_select_lds_bytes(c->k) + 17 * 1024 > 160 * 1024)   // + the selection kernels' static LDS
+        return fail(TWOSD_E_UNSUPPORTED, "pool_build: k = %d random elements too many for pool selection", c->k);
     HIPCHK(hipSetDevice(c->device));
     const int m = c->L.m;
     const int nh = count / 2, nv = count - nh;
@@ -1646,6 +1647,24 @@ extern "C" int twosd_set_distributions(twosd_ctx *c, int k, const int *kind, con
         (rc = upload(&c->d_dist_prob, prob)) || (rc = upload(&c->d_dist_p0, p0)) || (rc = upload(&c->d_dist_p1, p1)) ||
         (rc = upload(&c->d_dist_tmpl, tmpl)))
         return rc;
+    // mean absolute deviation E|V_e - E V_e| per element: the spread of the scenarios (the scale
+    // of the selection key's count weight)
+    c->dist_mad.assign(std::max(k, 1), 0.0);
+    for (int e = 0; e < k; ++e) {
+        double mad = 0.0;
+        if (kd[e] == 0) {
+            double ps = 0.0, mu = 0.0;
+            for (int i = off[e]; i < off[e + 1]; ++i) { mu += prob[i] * val[i]; ps += prob[i]; }
+            mu = ps > 0.0 ? mu / ps : 0.0;
+            for (int i = off[e]; i < off[e + 1]; ++i) mad += prob[i] * fabs(val[i] - mu);
+            mad = ps > 0.0 ? mad / ps : 0.0;
+        } else if (kd[e] == 1) {   // Normal(mu, sigma): sigma sqrt(2 / pi)
+            mad = p1[e] * std::sqrt(2.0 / M_PI);
+        } else {                   // Uniform(a, b): |b - a| / 4
+            mad = 0.25 * fabs(p1[e] - p0[e]);
+        }
+        c->dist_mad[e] = std::isfinite(mad) ? mad : 0.0;
+    }
     c->has_dist = true;
     return TWOSD_OK;
 }
@@ -1874,6 +1893,9 @@ __device__ __forceinline__ double dev_infeas(double x, int bt) {
 // x_B,i) followed by its element entries (e, B_p^{-1}[i][row_e]) at the basis's static capacity
 // offset; rows without entries add their constant infeasibility to cinf[p] (fixed-order sum).
 constexpr int kSelStreamThreads = 256;
+// count weight of the selection key in units of the mean |coef_e| E|V_e - E V_e| (storm: 13.5;
+// 1M bench: 0 -> 111.5 ms per step, 0.37 - 0.74 -> 105.5 - 105.8, 1.5 -> 112, 3 -> 115; ssn: no effect)
+constexpr double kSelCountWeight = 0.5;
 constexpr int kSelStreamRows = 1024;   // MP <= 1024 (R <= 16)
 __global__ void __launch_bounds__(kSelStreamThreads) pool_selstream_kernel(
     int m, int MP, int k, const double *__restrict__ xbase, const int *__restrict__ hb0,
@@ -2047,6 +2069,15 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
         HIPCHK(hipGetLastError());
         if (sel) {
             if (MP > kSelStreamRows) return fail(TWOSD_E_UNSUPPORTED, "pool selection: m = %d rows > %d", m, kSelStreamRows);
+            // count weight of the selection key: kSelCountWeight x the mean over the random elements
+            // of |coef_e(x)| E|V_e - E V_e| (one infeasible row is worth about half a typical
+            // scenario perturbation), 0 without distributions.  The same on every rank.
+            double sc = 0.0;
+            if (c->has_dist && k > 0) {
+                for (int e = 0; e < k; ++e) sc += fabs(coef[e]) * c->dist_mad[e];
+                sc /= k;
+            }
+            c->sel_cw = (float)(kSelCountWeight * sc);
             if (const char *e = getenv("TWOSD_SEL_CW")) c->sel_cw = (float)atof(e);   // selection-key experiments
             static const bool sel_order = !getenv("TWOSD_SEL_ROWORDER") || atoi(getenv("TWOSD_SEL_ROWORDER")) != 0;   // A/B knob
             hipLaunchKernelGGL(pool_selstream_kernel, dim3(P), dim3(kSelStreamThreads), 0, c->stream, m, MP, k, c->d_xbase,

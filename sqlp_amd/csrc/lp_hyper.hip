@@ -44,6 +44,10 @@ namespace twosd {
 #define STAMP_FLUSH                                                                         \
     if (lane == 0 && P.stamps)                                                              \
         for (int i_ = 0; i_ < 10; ++i_) atomicAdd(&P.stamps[i_], st_acc[i_]);
+#elif defined(TWOSD_ISA_MARK)   // assembly inspection only: phase markers as asm comments
+#define STAMP_DECL
+#define STAMP(i) asm volatile("; TWOSD_PHASE_END " #i);
+#define STAMP_FLUSH
 #else
 #define STAMP_DECL
 #define STAMP(i)
@@ -969,97 +973,140 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
 // signs for E), so a row's infeasibility is x' when x' > tol
 __device__ __forceinline__ float h_viol_f(float x, float cw) { return x > 1e-9f ? x + cw : 0.0f; }
 
-constexpr int kSelWaves = 16;   // 16 waves share one staged 64-scenario tile (latency hiding)
+constexpr int kSelWaves = 16;   // 16 waves share one staged scenario tile (latency hiding)
+#ifndef TWOSD_SEL_B
+#define TWOSD_SEL_B 16           // records per batch of the selection streams (loads in flight)
+#endif
+constexpr int kSelB = TWOSD_SEL_B;
+// Two scenarios per lane: s0 + lane (.x) and s0 + 64 + lane (.y), 128 per block.  The staged
+// deltas are (x, y) pairs, so one ds_read_b64 (2 LDS cycles per wave, as a ds_read_b32) and one
+// v_pk_fma_f32 serve both.  The arithmetic per scenario is that of one scenario per lane (same
+// fp32 fma and adds, same order), so the picks are identical to it (same pivots per x in the
+// bench A/B); measured on storm 1M: 11.2 -> 10.3 ms per step with 16-record batches.  The
+// kernels are SALU-bound on the wave-uniform record streams (SALU 2x VALU instructions).
+typedef float sel_f2 __attribute__((ext_vector_type(2)));
+constexpr int kSelTile = 128;
+__device__ __forceinline__ sel_f2 h_viol_f2(sel_f2 x, float cw) {
+    sel_f2 r;
+    r.x = h_viol_f(x.x, cw);
+    r.y = h_viol_f(x.y, cw);
+    return r;
+}
+// stage the k deltas of tile scenarios 0..127 (scenario sl at dv row srow(sl); nv valid) as
+// pairs: element e of lane l = (scenario l, scenario 64 + l)
+template <typename RowOf>
+__device__ __forceinline__ void h_stage_pairs(float *dvt, const double *__restrict__ dv, const double *__restrict__ kcoef,
+                                              int k, int nv, RowOf srow) {
+    for (int idx = threadIdx.x; idx < kSelTile * k; idx += 64 * kSelWaves) {
+        const int sl = idx / k, e = idx - sl * k;
+        dvt[2 * (e * 65 + (sl & 63)) + (sl >> 6)] = sl < nv ? (float)(kcoef[e] * dv[(size_t)srow(sl) * k + e]) : 0.0f;
+    }
+}
+// one basis' record stream for both scenarios of the lane (code < 0: row start), pruned once no
+// scenario of the wave can still win (alive2); returns the pair's keys (inf when pruned)
+template <typename Alive>
+__device__ __forceinline__ sel_f2 h_stream2(const int2 *__restrict__ rec, int j0, int j1, float cinf, float cw,
+                                            const sel_f2 *dvt2, int lane, Alive alive2) {
+    sel_f2 inf = {cinf, cinf}, x = {0.0f, 0.0f};
+    auto step = [&](int code, float v, sel_f2 dl) {
+        if (code < 0) {   // next row: close the previous one
+            inf += h_viol_f2(x, cw);
+            x = (sel_f2){v, v};
+        } else {
+            x = __builtin_elementwise_fma((sel_f2){v, v}, dl, x);
+        }
+    };
+    int j = (__ballot(alive2(inf)) == 0) ? j1 : j0;
+    for (; j + kSelB <= j1; j += kSelB) {   // batches of records: scalar loads and LDS reads in flight together
+        int2 rc[kSelB];
+        sel_f2 dl[kSelB];
+#pragma unroll
+        for (int u = 0; u < kSelB; ++u) rc[u] = rec[j + u];
+#pragma unroll
+        for (int u = 0; u < kSelB; ++u) dl[u] = dvt2[(rc[u].x < 0 ? 0 : rc[u].x) * 65 + lane];
+#pragma unroll
+        for (int u = 0; u < kSelB; ++u) step(rc[u].x, __int_as_float(rc[u].y), dl[u]);
+        // exact pruning: inf only grows, so once no scenario of the wave can still beat its best,
+        // this basis cannot win for any of them
+        if (__ballot(alive2(inf)) == 0) return (sel_f2){INFINITY, INFINITY};
+    }
+    for (; j < j1; ++j) {
+        const int2 r = rec[j];
+        step(r.x, __int_as_float(r.y), dvt2[(r.x < 0 ? 0 : r.x) * 65 + lane]);
+    }
+    inf += h_viol_f2(x, cw);
+    return inf;
+}
+
 __global__ void __launch_bounds__(64 * kSelWaves) pool_select_kernel(PoolSelParams S) {
-    extern __shared__ float dvt[];   // k x 65 (padded)
-    __shared__ float bsum[kSelWaves][64];
-    __shared__ int bidx[kSelWaves][64];
-    // best key found so far by any wave, per scenario (keys are >= 0, so the uint order of
-    // the fp32 bits is the float order): a wave stops a basis once it is strictly worse than
-    // another wave's best for every lane
-    __shared__ unsigned sbest[64];
+    extern __shared__ float dvt[];   // k x 65 pairs
+    const sel_f2 *dvt2 = reinterpret_cast<const sel_f2 *>(dvt);
+    __shared__ float bsum[kSelWaves][kSelTile];
+    __shared__ int bidx[kSelWaves][kSelTile];
+    // best key found so far by any wave, per scenario (keys are >= 0, so the uint order of the
+    // fp32 bits is the float order): a wave stops a basis once it is strictly worse than
+    // another wave's best for every scenario it holds
+    __shared__ unsigned sbest[kSelTile];
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar stream loads
-    const int s0 = blockIdx.x * 64;
-    const int k = S.k;
-    const int ns = min(64, S.N - s0);
-    for (int idx = threadIdx.x; idx < 64 * k; idx += 64 * kSelWaves) {
-        const int sl = idx / k, e = idx - sl * k;
-        dvt[e * 65 + sl] = sl < ns ? (float)(S.kcoef[e] * S.dv[(size_t)s0 * k + idx]) : 0.0f;
-    }
-    if (threadIdx.x < 64) sbest[threadIdx.x] = 0x7f800000u;   // +inf
+    const int s0 = blockIdx.x * kSelTile;
+    const int ns = min(kSelTile, S.N - s0);
+    h_stage_pairs(dvt, S.dv, S.kcoef, S.k, ns, [&](int sl) { return s0 + sl; });
+    if (threadIdx.x < kSelTile) sbest[threadIdx.x] = 0x7f800000u;   // +inf
     __syncthreads();
-    float best = INFINITY;
-    int bp = 0;
-    // a lane can still win with key `inf` only if inf < its own best (lower p wins ties within
+    sel_f2 best = {INFINITY, INFINITY};
+    int bpx = 0, bpy = 0;
+    // a scenario can still win with key `inf` only if inf < its own best (lower p wins ties within
     // the wave) and inf <= every other wave's best (ties with other waves are settled at the end)
-    auto alive = [&](float inf) {
-        return inf < best && inf <= __uint_as_float(__hip_atomic_load(&sbest[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    auto alive2 = [&](sel_f2 inf) {
+        const float ox = __uint_as_float(__hip_atomic_load(&sbest[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        const float oy = __uint_as_float(__hip_atomic_load(&sbest[64 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        return (inf.x < best.x && inf.x <= ox) || (inf.y < best.y && inf.y <= oy);
     };
     for (int p = wid; p < S.npool; p += kSelWaves) {
-        // one flat, wave-uniform stream per basis: a row-start record (code -1 - bound type,
-        // value xbase_i) followed by the row's entries (code e, value B^{-1}[i][row_e]);
-        // no load depends on the loop state, so the stream pipelines through the scalar cache
-        float inf = S.cinf[p], x = 0.0f;
-        const int j0 = S.sptr[p], j1 = S.send[p];
-        auto step = [&](int code, float v, float dl) {
-            if (code < 0) {   // next row: close the previous one
-                inf += h_viol_f(x, S.cw);
-                x = v;
-            } else {
-                x = fmaf(v, dl, x);
-            }
-        };
-        int j = (__ballot(alive(inf)) == 0) ? j1 : j0;   // constant rows alone already lose
-        for (; j + 8 <= j1; j += 8) {   // batches of 8 records: scalar loads and LDS reads in flight together
-            int2 rc[8];
-            float dl[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) rc[u] = S.rec[j + u];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) dl[u] = dvt[(rc[u].x < 0 ? 0 : rc[u].x) * 65 + lane];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) step(rc[u].x, __int_as_float(rc[u].y), dl[u]);
-            // exact pruning: inf only grows (sum of nonnegative terms), so once no lane can
-            // still beat its best, this basis cannot win for any of the 64 scenarios
-            if (__ballot(alive(inf)) == 0) { x = 0.0f; inf = INFINITY; j = j1; break; }
+        const sel_f2 inf = h_stream2(S.rec, S.sptr[p], S.send[p], S.cinf[p], S.cw, dvt2, lane, alive2);
+        if (inf.x < best.x) {
+            best.x = inf.x;
+            bpx = p;
+            atomicMin(&sbest[lane], __float_as_uint(inf.x));
         }
-        for (; j < j1; ++j) {
-            const int2 r = S.rec[j];
-            step(r.x, __int_as_float(r.y), dvt[(r.x < 0 ? 0 : r.x) * 65 + lane]);
-        }
-        inf += h_viol_f(x, S.cw);
-        if (inf < best) {
-            best = inf;
-            bp = p;
-            atomicMin(&sbest[lane], __float_as_uint(inf));
+        if (inf.y < best.y) {
+            best.y = inf.y;
+            bpy = p;
+            atomicMin(&sbest[64 + lane], __float_as_uint(inf.y));
         }
     }
-    bsum[wid][lane] = best;
-    bidx[wid][lane] = bp;
+    bsum[wid][lane] = best.x; bidx[wid][lane] = bpx;
+    bsum[wid][64 + lane] = best.y; bidx[wid][64 + lane] = bpy;
     __syncthreads();
-    if (wid == 0 && lane < ns) {
-        for (int w = 1; w < kSelWaves; ++w) {
-            const float v = bsum[w][lane];
-            const int pw = bidx[w][lane];
-            if (v < best || (v == best && pw < bp)) { best = v; bp = pw; }
+    if (wid < 2) {   // wave 0: scenarios 0..63, wave 1: 64..127
+        const int sl = 64 * wid + lane;
+        if (sl < ns) {
+            float b = bsum[0][sl];
+            int bp = bidx[0][sl];
+            for (int w = 1; w < kSelWaves; ++w) {
+                const float v = bsum[w][sl];
+                const int pw = bidx[w][sl];
+                if (v < b || (v == b && pw < bp)) { b = v; bp = pw; }
+            }
+            S.pick[s0 + sl] = bp;
+            if (S.key) S.key[s0 + sl] = b;
         }
-        S.pick[s0 + lane] = bp;
-        if (S.key) S.key[s0 + lane] = best;
     }
 }
 
-// ---- level 2: 64 consecutive entries of `order` (scenarios sorted by their level-1 pick, so a
+// ---- level 2: 128 consecutive entries of `order` (scenarios sorted by their level-1 pick, so a
 // tile holds one or two pick groups) per block; the block's 16 waves share the staged deltas
 // and split each group's candidate list (candidate ci on wave ci % 16).  Each candidate streams
 // its records wave-uniformly, as in level 1.  Result per scenario: least (key, ci) with the
 // level-1 pick as ci = -1, i.e. a candidate replaces the pick only with a strictly smaller key,
 // and among equal keys the earlier candidate wins (deterministic).
 __global__ void __launch_bounds__(64 * kSelWaves) pool_refine_kernel(PoolRefineParams S) {
-    extern __shared__ float dvt[];   // k x 65
-    __shared__ float rkey[kSelWaves][64];
-    __shared__ int rci[kSelWaves][64];
-    __shared__ unsigned sbest[64];   // best key so far over all waves, per scenario (as in level 1)
+    extern __shared__ float dvt[];   // k x 65 pairs
+    const sel_f2 *dvt2 = reinterpret_cast<const sel_f2 *>(dvt);
+    __shared__ float rkey[kSelWaves][kSelTile];
+    __shared__ int rci[kSelWaves][kSelTile];
+    __shared__ unsigned sbest[kSelTile];   // best key so far over all waves, per scenario (as in level 1)
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // XCD-aware tile remap: consecutive tiles (the same level-1 pick group, the same candidate
@@ -1067,95 +1114,82 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_refine_kernel(PoolRefineP
     // placement (speed only; any bijection is correct)
     const int nb = gridDim.x, b = blockIdx.x, xq = nb >> 3, xr = nb & 7, xc = b & 7;
     const int tile = xc * xq + min(xc, xr) + (b >> 3);
-    const int t0 = tile * 64;
-    const int k = S.k;
-    const int nv = min(64, S.N - t0);
-    for (int idx = threadIdx.x; idx < 64 * k; idx += 64 * kSelWaves) {
-        const int r = idx / k, e = idx - r * k;
-        dvt[e * 65 + r] = r < nv ? (float)(S.kcoef[e] * S.dv[(size_t)S.order[t0 + r] * k + e]) : 0.0f;
+    const int t0 = tile * kSelTile;
+    const int nv = min(kSelTile, S.N - t0);
+    h_stage_pairs(dvt, S.dv, S.kcoef, S.k, nv, [&](int sl) { return S.order[t0 + sl]; });
+    const bool vx = lane < nv, vy = 64 + lane < nv;
+    const int sx = vx ? S.order[t0 + lane] : 0, sy = vy ? S.order[t0 + 64 + lane] : 0;
+    const int px = vx ? S.pick[sx] : -1, py = vy ? S.pick[sy] : -1;
+    sel_f2 best = {vx ? S.key[sx] : 0.0f, vy ? S.key[sy] : 0.0f};
+    int bcx = -1, bcy = -1;
+    if (wid == 0) {
+        sbest[lane] = __float_as_uint(best.x);
+        sbest[64 + lane] = __float_as_uint(best.y);
     }
     __syncthreads();
-    const bool valid = lane < nv;
-    const int s = valid ? S.order[t0 + lane] : 0;
-    const int p1 = valid ? S.pick[s] : -1;
-    const float key1 = valid ? S.key[s] : 0.0f;
-    float best = key1;
-    int bci = -1;
-    if (wid == 0) sbest[lane] = __float_as_uint(key1);
-    __syncthreads();
-    // a candidate can still win for a lane only below the lane's own best (strict: the level-1
+    // a candidate can still win for a scenario only below its own best (strict: the level-1
     // pick and earlier candidates of this wave win ties) and not above any other wave's best
     // (ties with other waves are settled by candidate index at the end)
-    auto alive = [&](bool mine, float inf) {
-        return mine && inf < best &&
-               inf <= __uint_as_float(__hip_atomic_load(&sbest[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    bool mx = false, my = false;
+    auto alive2 = [&](sel_f2 inf) {
+        const float ox = __uint_as_float(__hip_atomic_load(&sbest[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        const float oy = __uint_as_float(__hip_atomic_load(&sbest[64 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        return (mx && inf.x < best.x && inf.x <= ox) || (my && inf.y < best.y && inf.y <= oy);
     };
-    uint64_t todo = __ballot(valid);
-    while (todo) {
-        const int g = __builtin_amdgcn_readlane(p1, __builtin_ctzll(todo));
-        const bool mine = valid && p1 == g;
-        todo &= ~__ballot(mine);
+    uint64_t todx = __ballot(vx), tody = __ballot(vy);
+    while (todx | tody) {
+        const int g = todx ? __builtin_amdgcn_readlane(px, __builtin_ctzll(todx))
+                           : __builtin_amdgcn_readlane(py, __builtin_ctzll(tody));
+        mx = vx && px == g;
+        my = vy && py == g;
+        todx &= ~__ballot(mx);
+        tody &= ~__ballot(my);
         for (int ci = wid; ci < S.ncand; ci += kSelWaves) {
             const int cb = S.cand[(size_t)g * S.ncand + ci];
             if (cb < 0) break;
-            float inf = S.cinf[cb], x = 0.0f;
-            auto step = [&](int code, float v, float dl) {
-                if (code < 0) {   // next row: close the previous one
-                    inf += h_viol_f(x, S.cw);
-                    x = v;
-                } else {
-                    x = fmaf(v, dl, x);
-                }
-            };
-            const int j0 = S.sptr[cb], j1 = S.send[cb];
-            int j = (__ballot(alive(mine, inf)) == 0) ? j1 : j0;
-            for (; j + 8 <= j1; j += 8) {
-                int2 rc[8];
-                float dl[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) rc[u] = S.rec[j + u];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) dl[u] = dvt[(rc[u].x < 0 ? 0 : rc[u].x) * 65 + lane];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) step(rc[u].x, __int_as_float(rc[u].y), dl[u]);
-                if (__ballot(alive(mine, inf)) == 0) { x = 0.0f; inf = INFINITY; j = j1; break; }
+            const sel_f2 inf = h_stream2(S.rec, S.sptr[cb], S.send[cb], S.cinf[cb], S.cw, dvt2, lane, alive2);
+            if (mx && inf.x < best.x) {
+                best.x = inf.x;
+                bcx = ci;
+                atomicMin(&sbest[lane], __float_as_uint(inf.x));
             }
-            for (; j < j1; ++j) {
-                const int2 r = S.rec[j];
-                step(r.x, __int_as_float(r.y), dvt[(r.x < 0 ? 0 : r.x) * 65 + lane]);
-            }
-            inf += h_viol_f(x, S.cw);
-            if (mine && inf < best) {
-                best = inf;
-                bci = ci;
-                atomicMin(&sbest[lane], __float_as_uint(inf));
+            if (my && inf.y < best.y) {
+                best.y = inf.y;
+                bcy = ci;
+                atomicMin(&sbest[64 + lane], __float_as_uint(inf.y));
             }
         }
     }
-    rkey[wid][lane] = best;
-    rci[wid][lane] = bci;
+    rkey[wid][lane] = best.x; rci[wid][lane] = bcx;
+    rkey[wid][64 + lane] = best.y; rci[wid][64 + lane] = bcy;
     __syncthreads();
-    if (wid == 0 && valid) {
-        for (int w = 1; w < kSelWaves; ++w) {
-            const float v = rkey[w][lane];
-            const int cw = rci[w][lane];
-            if (v < best || (v == best && cw >= 0 && (bci < 0 ? false : cw < bci))) { best = v; bci = cw; }
+    if (wid < 2) {
+        const int sl = 64 * wid + lane;
+        if (sl < nv) {
+            float bk = rkey[0][sl];
+            int bc = rci[0][sl];
+            for (int w = 1; w < kSelWaves; ++w) {
+                const float v = rkey[w][sl];
+                const int cw = rci[w][sl];
+                if (v < bk || (v == bk && cw >= 0 && (bc < 0 ? false : cw < bc))) { bk = v; bc = cw; }
+            }
+            const int s = S.order[t0 + sl];
+            if (bc >= 0) S.pick[s] = S.cand[(size_t)S.pick[s] * S.ncand + bc];
         }
-        if (bci >= 0) S.pick[s] = S.cand[(size_t)p1 * S.ncand + bci];
     }
 }
 
 hipError_t launch_pool_refine(const PoolRefineParams &p, hipStream_t s) {
     if (p.N <= 0 || p.ncand <= 0) return hipSuccess;
-    hipLaunchKernelGGL(pool_refine_kernel, dim3((p.N + 63) / 64), dim3(64 * kSelWaves), pool_select_lds_bytes(p.k), s, p);
+    hipLaunchKernelGGL(pool_refine_kernel, dim3((p.N + kSelTile - 1) / kSelTile), dim3(64 * kSelWaves), pool_select_lds_bytes(p.k), s, p);
     return hipGetLastError();
 }
 
-size_t pool_select_lds_bytes(int k) { return (size_t)4 * 65 * (size_t)std::max(k, 1); }
+size_t pool_select_lds_bytes(int k) { return (size_t)4 * 65 * (kSelTile / 64) * (size_t)std::max(k, 1); }
 
 hipError_t launch_pool_select(const PoolSelParams &p, hipStream_t s) {
     if (p.N <= 0) return hipSuccess;
-    const int nb = (p.N + 63) / 64;
+    const int nb = (p.N + kSelTile - 1) / kSelTile;
     hipLaunchKernelGGL(pool_select_kernel, dim3(nb), dim3(64 * kSelWaves), pool_select_lds_bytes(p.k), s, p);
     return hipGetLastError();
 }

@@ -69,7 +69,8 @@ struct twosd_ctx {
     int64_t sel_cap_total = 0;           // records the static capacity layout holds
     size_t sel_code_cap = 0;             // records d_sel_code has room for
     int64_t sel_nnz = 0, sel_rows = 0;
-    float sel_cw = 0.0f;                 // pool selection key: sum |infeas| + sel_cw * #infeasible rows
+    float sel_cw = 0.0f;                 // pool selection key: sum |infeas| + sel_cw * #infeasible rows (per x)
+    std::vector<double> dist_mad;        // mean absolute deviation E|V_e - E V_e| of each random element
     std::vector<double> sel_lo, sel_hi;   // training box of the deltas (empty: no row pruning)
     int *d_bnnz = nullptr;        // npool: nnz of each pool B^{-1} (FMA accounting)
     int *d_head_out = nullptr, *d_pool_pick = nullptr;   // optional LP outputs (pool building)
