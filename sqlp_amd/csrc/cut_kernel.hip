@@ -177,7 +177,7 @@ __global__ void __launch_bounds__(256, 2) cut_argmax2_kernel(CutParams P) {
     __shared__ double bs[2][kVT2];
     extern __shared__ unsigned long long hl[];      // nv entries when P.hist_lds
     const int lane = threadIdx.x & 63;
-    const int wid = threadIdx.x >> 6;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar staging loop
     if (P.hist_lds)
         for (int v = threadIdx.x; v < P.nv; v += 256) hl[v] = 0ull;
     const int g = lane >> 4, j = lane & 15;
