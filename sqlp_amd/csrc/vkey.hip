@@ -35,17 +35,49 @@ __global__ void vkey_clear_kernel(unsigned long long *keys, int *first, int *cnt
     }
 }
 
-__global__ void vkey_insert_kernel(int N, const unsigned long long *__restrict__ vkey, const int *__restrict__ status,
-                                   unsigned long long *keys, int *first, int *cnt, unsigned mask) {
-    for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < N; s += gridDim.x * blockDim.x) {
+// Scenarios in blocks of kVkItems: a block first merges its scenarios' keys in an LDS table of
+// twice as many slots (never full: load <= 1/2; LDS atomics), then inserts each distinct key once
+// into the global table with the block's lowest scenario and count.  Many scenarios share a vertex
+// (storm 1M: ~3k distinct keys), so per-scenario global atomics would serialize on the hot slots.
+// min and sum are order independent: the result equals per-scenario insertion.
+constexpr int kVkItems = 2048;
+constexpr int kVkLds = 2 * kVkItems;
+__global__ void __launch_bounds__(256) vkey_insert_kernel(int N, const unsigned long long *__restrict__ vkey,
+                                                          const int *__restrict__ status, unsigned long long *keys,
+                                                          int *first, int *cnt, unsigned mask) {
+    __shared__ unsigned long long lk[kVkLds];
+    __shared__ int lf[kVkLds], lc[kVkLds];
+    for (int i = threadIdx.x; i < kVkLds; i += blockDim.x) {
+        lk[i] = 0ull;
+        lf[i] = 0x7fffffff;
+        lc[i] = 0;
+    }
+    __syncthreads();
+    const int s0 = blockIdx.x * kVkItems, s1 = min(N, s0 + kVkItems);
+    for (int s = s0 + threadIdx.x; s < s1; s += blockDim.x) {
         if (status[s] != TWOSD_LP_OPTIMAL) continue;
         const unsigned long long k = vk_norm(vkey[s]);
+        unsigned i = vk_slot(k, kVkLds - 1);
+        for (;;) {
+            const unsigned long long old = atomicCAS(&lk[i], 0ull, k);
+            if (old == 0ull || old == k) {
+                atomicMin(&lf[i], s);
+                atomicAdd(&lc[i], 1);
+                break;
+            }
+            i = (i + 1) & (kVkLds - 1);
+        }
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < kVkLds; j += blockDim.x) {
+        const unsigned long long k = lk[j];
+        if (!k) continue;
         unsigned i = vk_slot(k, mask);
         for (;;) {
             const unsigned long long old = atomicCAS(&keys[i], 0ull, k);
             if (old == 0ull || old == k) {
-                atomicMin(&first[i], s);
-                atomicAdd(&cnt[i], 1);
+                atomicMin(&first[i], lf[j]);
+                atomicAdd(&cnt[i], lc[j]);
                 break;
             }
             i = (i + 1) & mask;
@@ -143,8 +175,8 @@ int vkey_first_occurrences(twosd_ctx *c, int N, const unsigned long long *d_vkey
     const int nb = std::max(1, std::min(4096, (N + 255) / 256));
     hipLaunchKernelGGL(vkey_clear_kernel, dim3(std::min(4096u, (w->cap + 255) / 256)), dim3(256), 0, c->stream, w->keys, w->first,
                        w->cnt, w->cap);
-    hipLaunchKernelGGL(vkey_insert_kernel, dim3(nb), dim3(256), 0, c->stream, N, d_vkey, d_status, w->keys, w->first, w->cnt,
-                       mask);
+    hipLaunchKernelGGL(vkey_insert_kernel, dim3(std::max(1, (N + kVkItems - 1) / kVkItems)), dim3(256), 0, c->stream, N, d_vkey, d_status,
+                       w->keys, w->first, w->cnt, mask);
     hipLaunchKernelGGL(vkey_flag_kernel, dim3(nb), dim3(256), 0, c->stream, N, d_vkey, d_status, w->keys, w->first, mask,
                        w->flag);
     HIPCHK(hipGetLastError());
