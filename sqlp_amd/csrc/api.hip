@@ -1009,6 +1009,37 @@ static int train_kcap(const twosd_ctx *c) {
     return std::max(32, (int)std::ceil(3.0 * c->piv_mean_ref));
 }
 
+// The training solves of a refresh (basis keys, eta files, final heads) under the pivot cap.  The
+// auto cap follows the last batch's pivots at the previous x; when x moved far from the pool's x
+// (bench with warmup 4: the x_EV pool trained from the primary basis, next x SD candidate 4 --
+// 58.5 pivots a scenario against a cap of 35), most training scenarios hit the cap and the
+// refresh would find almost no optimal bases.  If fewer than half end optimal, the training is
+// solved again without a cap (one extra launch, only on such a jump).
+static int refresh_training(twosd_ctx *c, const double *x, const double *d_dv, int count) {
+    LpRun o;
+    o.want_bkey = true;
+    o.want_etas = true;
+    o.want_head = true;
+    // training scenarios beyond the pivot cap only drop out of the basis count (one launch
+    // lasts as long as its slowest scenario: with one scenario per wave the cap bounds it)
+    o.kcap = train_kcap(c);
+    int rc;
+    if ((rc = run_lp_ex(c, x, d_dv, count, o))) return rc;
+    int opt = count;
+    if (o.kcap > 0) {
+        std::vector<int> st(count);
+        HIPCHK(hipMemcpy(st.data(), c->d_status, sizeof(int) * count, hipMemcpyDeviceToHost));
+        opt = (int)std::count(st.begin(), st.end(), (int)TWOSD_LP_OPTIMAL);
+        if (2 * opt < count) {
+            if (getenv("TWOSD_DEBUG")) fprintf(stderr, "refresh training: %d of %d optimal under cap %d, solved again uncapped\n", opt, count, o.kcap);
+            o.kcap = 0;
+            if ((rc = run_lp_ex(c, x, d_dv, count, o))) return rc;
+        }
+    }
+    c->last_train_opt = opt;
+    return TWOSD_OK;
+}
+
 extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int first, int count, int max_pool,
                                   int *pool_size) {
     if (!c || !c->has_basis) return fail(TWOSD_E_STATE, "pool_refresh: no primary basis");
@@ -1023,14 +1054,17 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
     const double *d_dv = E.d_dv + (size_t)first * c->k;
     int rc;
     // 1. training solves at x from the current pool: basis keys, eta files and heads by scenario
-    LpRun o;
-    o.want_bkey = true;
-    o.want_etas = true;
-    o.want_head = true;
-    // training scenarios beyond the pivot cap only drop out of the basis count (one launch
-    // lasts as long as its slowest scenario: with one scenario per wave the cap bounds it)
-    o.kcap = train_kcap(c);
-    if ((rc = run_lp_ex(c, x, d_dv, count, o))) return rc;
+    if ((rc = refresh_training(c, x, d_dv, count))) return rc;
+    if (getenv("TWOSD_DEBUG")) {
+        std::vector<int> st(count), itv(count);
+        HIPCHK(hipMemcpy(st.data(), c->d_status, sizeof(int) * count, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(itv.data(), c->d_iters, sizeof(int) * count, hipMemcpyDeviceToHost));
+        int h[8] = {0};
+        long long itsum = 0;
+        for (int s2 = 0; s2 < count; ++s2) { h[std::min(std::max(st[s2], 0), 7)]++; itsum += itv[s2]; }
+        fprintf(stderr, "pool_refresh training: kcap %d (ref %.2f), pool %zu, statuses 0:%d 1:%d 2:%d 3:%d 4:%d 5+:%d, mean iters %.2f\n",
+                train_kcap(c), c->piv_mean_ref, c->pool.size(), h[0], h[1], h[2], h[3], h[4], h[5] + h[6] + h[7], (double)itsum / count);
+    }
     const auto t1 = std::chrono::steady_clock::now();
     // 2. distinct optimal bases, most frequent first (ties: first occurrence), primary excluded
     const int *d_list = nullptr, *d_counts = nullptr;
@@ -1115,9 +1149,9 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
         c->pool.swap(keep);
         // the old pool's host data is released on a helper thread (thousands of vectors)
         std::thread([old = std::move(keep)]() mutable { old.clear(); }).detach();
-    } else if (R == 0) {
-        c->pool.resize(1);
     }
+    // R == 0 (no training scenario optimal): the current pool stays (any pool basis is a valid
+    // start; dropping to the primary basis alone would cost ~90 pivots a scenario)
     const auto tb = std::chrono::steady_clock::now();
     // training box of the deltas (selection row pruning), as twosd_pool_build; cached per
     // training range
@@ -1134,9 +1168,10 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
             }
     }
     const auto tu = std::chrono::steady_clock::now();
-    if (!device_built && (rc = upload_pool(c))) return rc;
+    const bool host_built = R > 0 && !device_built;   // R == 0: the pool is unchanged
+    if (host_built && (rc = upload_pool(c))) return rc;
     const auto tua = std::chrono::steady_clock::now();
-    if (!device_built && (rc = prepare_elements(c))) return rc;
+    if (host_built && (rc = prepare_elements(c))) return rc;
     const auto t3 = std::chrono::steady_clock::now();
     if (getenv("TWOSD_DEBUG")) {
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -1223,12 +1258,7 @@ extern "C" int twosd_refresh_train(twosd_ctx *c, int epi, const double *x, int f
     const auto t0 = std::chrono::steady_clock::now();
     const double *d_dv = E.d_dv + (size_t)first * c->k;
     int rc;
-    LpRun o;   // as twosd_pool_refresh step 1
-    o.want_bkey = true;
-    o.want_etas = true;
-    o.want_head = true;
-    o.kcap = train_kcap(c);
-    if ((rc = run_lp_ex(c, x, d_dv, count, o))) return rc;
+    if ((rc = refresh_training(c, x, d_dv, count))) return rc;   // as twosd_pool_refresh step 1
     const auto t1 = std::chrono::steady_clock::now();
     const int *d_list = nullptr, *d_counts = nullptr;
     int U = 0;

@@ -39,6 +39,7 @@ struct twosd_ctx {
     int kmax_override = 0;
     int train_kcap = 0;           // pivot cap of the refresh training solves (> 0; 0: auto; < 0: none)
     double piv_mean_ref = 0.0;    // mean pivots of the last large batch solve (the auto cap's scale)
+    int last_train_opt = 0;       // optimal training scenarios of the last refresh
     double t_us[5] = {0, 0, 0, 0, 0};   // LP kernel, dedup, cut partial, cut finalize, pool select
     // template
     bool has_template = false, has_basis = false;

@@ -204,3 +204,29 @@ def test_refresh_failure_leaves_context_refusing(monkeypatch):
     assert ctx.pool_refresh(tr, x, 0, 2048, 512) > 1        # and refreshes again
     obj, _, _, st = ctx.solve_values(x, vals)
     np.testing.assert_allclose(obj, ref, rtol=1e-9, atol=1e-9)
+
+
+def test_refresh_training_cap_too_low_is_solved_again():
+    """A training cap far below the pivots the jump to a new x needs (bench with warmup 4: the
+    x_EV pool, next x an SD candidate, cap 35 against 58.5 pivots a scenario) used to leave the
+    refresh with no optimal training scenario and the pool at the primary basis alone.  With
+    fewer than half of the training solves optimal, the refresh solves them again uncapped."""
+    from sqlp_amd import smps, twosd
+    inst = I.load("storm")
+    x_ev = I.x_ev("storm")
+    x2 = _sd_x()
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    ctx.compute_basis(x_ev, smps.mean_values(inst["sto"]))
+    tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(tr, I.sample("storm", 4096, seed=31))
+    assert ctx.pool_refresh(tr, x_ev, 0, 4096, 512) > 1
+    ev = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    vals = I.sample("storm", 2000, seed=32)
+    twosd.add_scenarios(ev, vals)
+    ctx.set_refresh_kcap(3)                     # almost no training scenario reaches optimality
+    P = ctx.pool_refresh(tr, x2, 0, 4096, 512)
+    assert P > 256                              # rebuilt from the uncapped training solves
+    o, _, _, st = twosd.solve_batch(ev, x2, 0, len(vals), want_pi=False)
+    assert (st == 0).all()
+    assert ctx.lp_stats()[0] / len(vals) < 20   # a pool at x2, not the primary basis alone
+    ctx.set_refresh_kcap(0)
