@@ -233,7 +233,7 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_ops);
     dfree(c->d_dvtmp);
     dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); c->sel_code_cap = 0; dfree(c->d_head_out); dfree(c->d_pool_pick); dfree(c->d_order); dfree(c->d_sort_tmp);
-    dfree(c->d_cand); dfree(c->d_sel_key); c->key_cap = 0; c->pool_l1 = c->pool_ncand = 0; c->order_cap = 0; c->sort_tmp_bytes = 0; c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
+    dfree(c->d_cand); dfree(c->d_sel_key); dfree(c->d_sel_pkey); dfree(c->d_sel_ppick); c->sel_pcap = 0; c->key_cap = 0; c->pool_l1 = c->pool_ncand = 0; c->order_cap = 0; c->sort_tmp_bytes = 0; c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
     dfree(c->d_dist_kind); dfree(c->d_dist_off); dfree(c->d_dist_val); dfree(c->d_dist_prob); dfree(c->d_dist_p0);
     dfree(c->d_dist_p1); dfree(c->d_dist_tmpl); c->has_dist = false;
     dfree(c->d_kslot); dfree(c->d_kix); dfree(c->d_kv); dfree(c->d_kcoef); c->k_valid = false;
@@ -2158,6 +2158,13 @@ static int select_pool(twosd_ctx *c, const double *d_dv, int N, int *d_pick, int
         if ((rc = dalloc(&c->d_sel_key, (size_t)N))) return rc;
         c->key_cap = N;
     }
+    // partials of the chunked selections (small batches: several pool chunks per scenario tile)
+    const int g1 = pool_select_split(N, np1), g2 = two ? pool_refine_split(N, c->pool_ncand) : 1;
+    const size_t pneed = (size_t)std::max(g1, g2) * N;
+    if (std::max(g1, g2) > 1 && pneed > c->sel_pcap) {
+        if ((rc = dalloc(&c->d_sel_pkey, pneed)) || (rc = dalloc(&c->d_sel_ppick, pneed))) return rc;
+        c->sel_pcap = pneed;
+    }
     PoolSelParams S{};
     S.N = N; S.k = c->k; S.npool = np1; S.dv = d_dv;
     S.kcoef = c->d_kcoef;
@@ -2165,6 +2172,8 @@ static int select_pool(twosd_ctx *c, const double *d_dv, int N, int *d_pick, int
     S.pick = d_pick;
     S.cw = c->sel_cw;
     S.key = two ? c->d_sel_key : nullptr;
+    S.pkey = g1 > 1 ? c->d_sel_pkey : nullptr;
+    S.ppick = g1 > 1 ? c->d_sel_ppick : nullptr;
     HIPCHK(launch_pool_select(S, c->stream));
     if (two) {
         HIPCHK(sort_by_pool(d_pick, c->d_order, N, np1, c->d_sort_tmp, &tb, c->stream));
@@ -2172,6 +2181,8 @@ static int select_pool(twosd_ctx *c, const double *d_dv, int N, int *d_pick, int
         Q.N = N; Q.k = c->k; Q.ncand = c->pool_ncand; Q.dv = d_dv; Q.kcoef = c->d_kcoef;
         Q.cinf = c->d_sel_cinf; Q.sptr = c->d_sel_ptr; Q.send = c->d_sel_end; Q.rec = S.rec;
         Q.order = c->d_order; Q.cand = c->d_cand; Q.pick = d_pick; Q.key = c->d_sel_key; Q.cw = c->sel_cw;
+        Q.pkey = g2 > 1 ? c->d_sel_pkey : nullptr;
+        Q.pci = g2 > 1 ? c->d_sel_ppick : nullptr;
         HIPCHK(launch_pool_refine(Q, c->stream));
     }
     HIPCHK(sort_by_pool(d_pick, c->d_order, N, P, c->d_sort_tmp, &tb, c->stream));

@@ -1063,7 +1063,11 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_select_kernel(PoolSelPara
         const float oy = __uint_as_float(__hip_atomic_load(&sbest[64 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
         return (inf.x < best.x && inf.x <= ox) || (inf.y < best.y && inf.y <= oy);
     };
-    for (int p = wid; p < S.npool; p += kSelWaves) {
+    // blockIdx.y: a contiguous chunk of the pool (several chunks per tile when the batch alone
+    // would not fill the GPU; pool_select_merge_kernel merges them)
+    const int p_lo = (int)((long long)S.npool * blockIdx.y / gridDim.y), p_hi = (int)((long long)S.npool * (blockIdx.y + 1) / gridDim.y);
+    bpx = bpy = p_lo;
+    for (int p = p_lo + wid; p < p_hi; p += kSelWaves) {
         const sel_f2 inf = h_stream2(S.rec, S.sptr[p], S.send[p], S.cinf[p], S.cw, dvt2, lane, alive2);
         if (inf.x < best.x) {
             best.x = inf.x;
@@ -1089,8 +1093,13 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_select_kernel(PoolSelPara
                 const int pw = bidx[w][sl];
                 if (v < b || (v == b && pw < bp)) { b = v; bp = pw; }
             }
-            S.pick[s0 + sl] = bp;
-            if (S.key) S.key[s0 + sl] = b;
+            if (gridDim.y == 1) {
+                S.pick[s0 + sl] = bp;
+                if (S.key) S.key[s0 + sl] = b;
+            } else {
+                S.ppick[(size_t)blockIdx.y * S.N + s0 + sl] = bp;
+                S.pkey[(size_t)blockIdx.y * S.N + s0 + sl] = b;
+            }
         }
     }
 }
@@ -1136,6 +1145,8 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_refine_kernel(PoolRefineP
         const float oy = __uint_as_float(__hip_atomic_load(&sbest[64 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
         return (mx && inf.x < best.x && inf.x <= ox) || (my && inf.y < best.y && inf.y <= oy);
     };
+    // blockIdx.y: a contiguous chunk of the candidate lists (pool_refine_merge_kernel merges)
+    const int c_lo = (int)((long long)S.ncand * blockIdx.y / gridDim.y), c_hi = (int)((long long)S.ncand * (blockIdx.y + 1) / gridDim.y);
     uint64_t todx = __ballot(vx), tody = __ballot(vy);
     while (todx | tody) {
         const int g = todx ? __builtin_amdgcn_readlane(px, __builtin_ctzll(todx))
@@ -1144,7 +1155,7 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_refine_kernel(PoolRefineP
         my = vy && py == g;
         todx &= ~__ballot(mx);
         tody &= ~__ballot(my);
-        for (int ci = wid; ci < S.ncand; ci += kSelWaves) {
+        for (int ci = c_lo + wid; ci < c_hi; ci += kSelWaves) {
             const int cb = S.cand[(size_t)g * S.ncand + ci];
             if (cb < 0) break;
             const sel_f2 inf = h_stream2(S.rec, S.sptr[cb], S.send[cb], S.cinf[cb], S.cw, dvt2, lane, alive2);
@@ -1174,14 +1185,63 @@ __global__ void __launch_bounds__(64 * kSelWaves) pool_refine_kernel(PoolRefineP
                 if (v < bk || (v == bk && cw >= 0 && (bc < 0 ? false : cw < bc))) { bk = v; bc = cw; }
             }
             const int s = S.order[t0 + sl];
-            if (bc >= 0) S.pick[s] = S.cand[(size_t)S.pick[s] * S.ncand + bc];
+            if (gridDim.y > 1) {
+                S.pkey[(size_t)blockIdx.y * S.N + s] = bk;
+                S.pci[(size_t)blockIdx.y * S.N + s] = bc;
+            } else if (bc >= 0) {
+                S.pick[s] = S.cand[(size_t)S.pick[s] * S.ncand + bc];
+            }
         }
     }
 }
 
+// merges of the chunked selections, per scenario in chunk order: the rules of the in-block merges
+// (level 1: least (key, basis); level 2: least key, the level-1 pick (-1) keeps ties, then the
+// earlier candidate), so the picks equal those of one chunk
+__global__ void pool_select_merge_kernel(int N, int G, const float *__restrict__ pkey, const int *__restrict__ ppick, int *pick,
+                                         float *key) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= N) return;
+    float b = pkey[s];
+    int bp = ppick[s];
+    for (int y = 1; y < G; ++y) {
+        const float v = pkey[(size_t)y * N + s];
+        const int p = ppick[(size_t)y * N + s];
+        if (v < b || (v == b && p < bp)) { b = v; bp = p; }
+    }
+    pick[s] = bp;
+    if (key) key[s] = b;
+}
+__global__ void pool_refine_merge_kernel(int N, int G, int ncand, const float *__restrict__ pkey, const int *__restrict__ pci,
+                                         const int *__restrict__ cand, int *pick) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= N) return;
+    float bk = pkey[s];
+    int bc = pci[s];
+    for (int y = 1; y < G; ++y) {
+        const float v = pkey[(size_t)y * N + s];
+        const int c = pci[(size_t)y * N + s];
+        if (v < bk || (v == bk && c >= 0 && (bc < 0 ? false : c < bc))) { bk = v; bc = c; }
+    }
+    if (bc >= 0) pick[s] = cand[(size_t)pick[s] * ncand + bc];
+}
+
+// chunks per tile: enough blocks to fill the GPU (~1024) when the batch alone does not, at least
+// kSelWaves bases / candidates per chunk
+static int sel_split(int N, int items) {
+    const int nb = (N + kSelTile - 1) / kSelTile;
+    int g = (1024 + nb - 1) / nb;
+    g = std::min(g, std::max(1, items / kSelWaves));
+    return std::max(1, std::min(g, 16));
+}
+int pool_select_split(int N, int npool) { return sel_split(N, npool); }
+int pool_refine_split(int N, int ncand) { return sel_split(N, ncand); }
+
 hipError_t launch_pool_refine(const PoolRefineParams &p, hipStream_t s) {
     if (p.N <= 0 || p.ncand <= 0) return hipSuccess;
-    hipLaunchKernelGGL(pool_refine_kernel, dim3((p.N + kSelTile - 1) / kSelTile), dim3(64 * kSelWaves), pool_select_lds_bytes(p.k), s, p);
+    const int G = p.pkey ? pool_refine_split(p.N, p.ncand) : 1;
+    hipLaunchKernelGGL(pool_refine_kernel, dim3((p.N + kSelTile - 1) / kSelTile, G), dim3(64 * kSelWaves), pool_select_lds_bytes(p.k), s, p);
+    if (G > 1) hipLaunchKernelGGL(pool_refine_merge_kernel, dim3((p.N + 255) / 256), dim3(256), 0, s, p.N, G, p.ncand, p.pkey, p.pci, p.cand, p.pick);
     return hipGetLastError();
 }
 
@@ -1190,7 +1250,9 @@ size_t pool_select_lds_bytes(int k) { return (size_t)4 * 65 * (kSelTile / 64) * 
 hipError_t launch_pool_select(const PoolSelParams &p, hipStream_t s) {
     if (p.N <= 0) return hipSuccess;
     const int nb = (p.N + kSelTile - 1) / kSelTile;
-    hipLaunchKernelGGL(pool_select_kernel, dim3(nb), dim3(64 * kSelWaves), pool_select_lds_bytes(p.k), s, p);
+    const int G = p.pkey ? pool_select_split(p.N, p.npool) : 1;
+    hipLaunchKernelGGL(pool_select_kernel, dim3(nb, G), dim3(64 * kSelWaves), pool_select_lds_bytes(p.k), s, p);
+    if (G > 1) hipLaunchKernelGGL(pool_select_merge_kernel, dim3((p.N + 255) / 256), dim3(256), 0, s, p.N, G, p.pkey, p.ppick, p.pick, p.key);
     return hipGetLastError();
 }
 

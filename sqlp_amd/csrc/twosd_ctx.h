@@ -81,6 +81,9 @@ struct twosd_ctx {
     int pool_l1 = 0, pool_ncand = 0;
     int *d_cand = nullptr;
     float *d_sel_key = nullptr;
+    float *d_sel_pkey = nullptr;          // chunked selection partials (split x N)
+    int *d_sel_ppick = nullptr;
+    size_t sel_pcap = 0;
     size_t key_cap = 0;
     int *d_order = nullptr;       // LP visiting order grouped by pool basis
     char *d_sort_tmp = nullptr;

@@ -136,6 +136,7 @@ struct PoolSelParams {
     int *pick;                                          // N out
     float cw;                                           // key = sum |infeas| + cw * #infeasible rows
     float *key;                                         // N out (nullable): key of the pick
+    float *pkey; int *ppick;                            // split x N partials (nullable: no split)
 };
 // second level of the two-level pool selection: scenarios in `order` (grouped by their
 // level-1 pick) try the candidate bases of their level-1 pick (cand: nl1 x ncand, -1 pad)
@@ -149,9 +150,13 @@ struct PoolRefineParams {
     int *pick;                                          // N in (level 1) / out
     const float *key;                                   // N: level-1 key
     float cw;
+    float *pkey; int *pci;                              // split x N partials (nullable: no split)
 };
 hipError_t launch_pool_refine(const PoolRefineParams &p, hipStream_t s);
 size_t pool_select_lds_bytes(int k);
+// chunks of the pool / candidate lists per scenario tile for a batch of N (<= 16)
+int pool_select_split(int N, int npool);
+int pool_refine_split(int N, int ncand);
 // stable sort of scenarios [0, N) by pool pick -> order (pool_sort.hip); tmp == nullptr: size query
 hipError_t sort_by_pool(const int *pick, int *order, int N, int npool, void *tmp, size_t *tmp_bytes, hipStream_t s);
 hipError_t launch_pool_select(const PoolSelParams &p, hipStream_t s);
