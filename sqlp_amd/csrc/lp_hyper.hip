@@ -1229,6 +1229,7 @@ __global__ void pool_refine_merge_kernel(int N, int G, int ncand, const float *_
 // chunks per tile: enough blocks to fill the GPU (~1024) when the batch alone does not, at least
 // kSelWaves bases / candidates per chunk
 static int sel_split(int N, int items) {
+    if (getenv("TWOSD_SEL_NOSPLIT")) return 1;   // test hook: one chunk (the picks must not change)
     const int nb = (N + kSelTile - 1) / kSelTile;
     int g = (1024 + nb - 1) / nb;
     g = std::min(g, std::max(1, items / kSelWaves));

@@ -231,3 +231,33 @@ def test_pool_selection_picks_least_infeasible():
     assert (got <= best + slack).all(), np.max(got - best - slack)
     assert np.mean(got == best) > 0.9
     assert len(np.unique(picks)) > 1
+
+
+def test_pool_selection_split_equals_one_chunk(monkeypatch):
+    """Small batches split the pool (level 1) and the candidate lists (level 2) over several
+    blocks per scenario tile and merge per scenario with the in-block rules (least key, then the
+    lowest basis / the level-1 pick / the earlier candidate): the picks equal those of one chunk
+    per tile (TWOSD_SEL_NOSPLIT), with the count-weighted key of device-drawn scenarios."""
+    from sqlp_amd import smps, twosd
+    inst = I.load("storm")
+    x = I.x_ev("storm")
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    ctx.compute_basis(x, smps.mean_values(inst["sto"]))
+    ctx.set_distributions(inst["sto"])
+    tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_sampled_scenarios(tr, 8192, 41)
+    assert ctx.pool_refresh(tr, x, 0, 8192, 1024) > 128
+    ctx.pool_build_candidates(tr, x, 0, 8192, 128, 160)
+    ev = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    N = 4096
+    twosd.add_sampled_scenarios(ev, N, 42)
+    o1, _, _, st1 = twosd.solve_batch(ev, x, 0, N, want_pi=False)
+    p1 = ctx.last_pool_picks(N)
+    ctx.invalidate_x()
+    monkeypatch.setenv("TWOSD_SEL_NOSPLIT", "1")
+    o2, _, _, st2 = twosd.solve_batch(ev, x, 0, N, want_pi=False)
+    p2 = ctx.last_pool_picks(N)
+    assert (st1 == 0).all() and (st2 == 0).all()
+    np.testing.assert_array_equal(p1, p2)
+    np.testing.assert_array_equal(o1, o2)
+    assert len(np.unique(p1)) > 128                   # level-2 candidates were picked too
