@@ -341,9 +341,24 @@ __global__ __launch_bounds__(kPgThreads) void pg_fill_kernel(PgArgs A, PgFill F)
     const int *irow = A.inter_row + A.inter_off[a];
     const double *ival = A.inter_val + A.inter_off[a];
     if (wv == 0) {
-        // B^{-1} rows (CSR, columns ascending): walk the columns in order, per-row cursors
+        // B^{-1} rows (CSR, columns ascending): walk the columns in order, per-row cursors (a
+        // column's rows are distinct, so its entries go in any lane order).  The first 64 entries
+        // of column c + 1 are loaded while column c is written: one memory round trip per column
+        // hides behind the previous one (column sizes from the LDS scan, cs)
+        int ni = 0;
+        double nv = 0.0;
+        if (m > 0 && lane < cs[1] - cs[0]) { ni = irow[ic[0] + lane]; nv = ival[ic[0] + lane]; }
         for (int c = 0; c < m; ++c) {
-            for (int q = ic[c] + lane; q < ic[c] + keptc[c]; q += 64) {   // distinct rows
+            const int kc = cs[c + 1] - cs[c];
+            const int i0 = ni;
+            const double v0 = nv;
+            if (c + 1 < m && lane < cs[c + 2] - cs[c + 1]) { ni = irow[ic[c + 1] + lane]; nv = ival[ic[c + 1] + lane]; }
+            if (lane < kc) {
+                const int at = nb + rs[i0] + cur[i0]++;
+                F.brcol[at] = c;
+                F.brval[at] = v0;
+            }
+            for (int q = ic[c] + 64 + lane; q < ic[c] + kc; q += 64) {   // columns of > 64 rows
                 const int i = irow[q];
                 const int at = nb + rs[i] + cur[i]++;
                 F.brcol[at] = c;
@@ -352,19 +367,29 @@ __global__ __launch_bounds__(kPgThreads) void pg_fill_kernel(PgArgs A, PgFill F)
             __builtin_amdgcn_wave_barrier();
         }
     } else if (wv == 1) {
-        // element rows (CSR, e ascending) and their sliced ELL: walk the elements in order
+        // element rows (CSR, e ascending) and their sliced ELL: walk the elements in order, the
+        // next element's column loaded ahead as above
+        auto put = [&](int e, int i, double v) {
+            const int j = ecur[i]++;
+            F.ke[eb + es[i] + j] = e;
+            F.kraw[eb + es[i] + j] = v;
+            const size_t at = ((size_t)ws[i >> 6] + j) * 64 + (i & 63);
+            F.kix[at] = e;
+            F.kv[at] = v;
+        };
+        int ni = 0, nc = k > 0 ? A.pos_row[0] : 0;
+        double nv = 0.0;
+        if (k > 0 && lane < cs[nc + 1] - cs[nc]) { ni = irow[ic[nc] + lane]; nv = ival[ic[nc] + lane]; }
         for (int e = 0; e < k; ++e) {
-            const int c = A.pos_row[e];
-            for (int q = ic[c] + lane; q < ic[c] + keptc[c]; q += 64) {
-                const int i = irow[q];
-                const double v = ival[q];
-                const int j = ecur[i]++;
-                F.ke[eb + es[i] + j] = e;
-                F.kraw[eb + es[i] + j] = v;
-                const size_t at = ((size_t)ws[i >> 6] + j) * 64 + (i & 63);
-                F.kix[at] = e;
-                F.kv[at] = v;
+            const int c = nc, i0 = ni;
+            const double v0 = nv;
+            const int kc = cs[c + 1] - cs[c];
+            if (e + 1 < k) {
+                nc = A.pos_row[e + 1];
+                if (lane < cs[nc + 1] - cs[nc]) { ni = irow[ic[nc] + lane]; nv = ival[ic[nc] + lane]; }
             }
+            if (lane < kc) put(e, i0, v0);
+            for (int q = ic[c] + 64 + lane; q < ic[c] + kc; q += 64) put(e, irow[q], ival[q]);
             __builtin_amdgcn_wave_barrier();
         }
     } else {
