@@ -90,7 +90,9 @@ def main():
     ap.add_argument("--instance", default="storm")
     ap.add_argument("--scenarios", type=int, default=1_000_000)
     ap.add_argument("--vertices", type=int, default=4096)
-    ap.add_argument("--tie-rel", type=float, default=1e-12)
+    ap.add_argument("--tie-rel", type=float, default=0.0,
+                    help="argmax tie rule: 0 = the reference's strict '>' (subprob.jl:156, first maximum); > 0 the "
+                         "build's near-tie rule (DESIGN.md §3)")
     ap.add_argument("--seed", type=int, default=20250219)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
@@ -99,6 +101,9 @@ def main():
                     help="first-stage points the timed steps cycle over: 0 = the EV solution (pool training "
                          "point), i > 0 = the candidate of SD iteration i (storm master + GPU hot path)")
     ap.add_argument("--spot", type=int, default=4096, help="parity spot-check scenarios per x point (0: off)")
+    ap.add_argument("--trajectory", type=int, default=20,
+                    help="K > 0: after the timed cycle, time K more steps at K DISTINCT consecutive SD candidates "
+                         "(iterations last+1 .. last+K of the same SD run, no revisits), reported beside the cycle")
     ap.add_argument("--refresh", type=int, default=1,
                     help="1: a step at an x other than the pool's rebuilds the pool there (twosd_pool_refresh + "
                          "candidate lists, inside the timed step); 0: keep the x_EV pool for every x")
@@ -158,11 +163,13 @@ def main():
     # first-stage points of the timed steps: x_EV and SD candidates (identical on every rank)
     t_traj = time.perf_counter()
     x_iters = sorted({int(v) for v in args.x_points.split(",")})
-    xs = sd_points(cor, tim, sp2, sto, positions, x, x_iters, args.seed + 7, device)
+    traj_iters = list(range(max(x_iters) + 1, max(x_iters) + 1 + max(0, args.trajectory)))
+    xs = sd_points(cor, tim, sp2, sto, positions, x, x_iters + traj_iters, args.seed + 7, device)
     if world > 1:
         t = torch.tensor(np.stack(xs), dtype=torch.float64, device=device)
         torch.distributed.broadcast(t, 0)
         xs = [row for row in t.cpu().numpy()]
+    xs, xs_traj = xs[:len(x_iters)], xs[len(x_iters):]
     t_traj = time.perf_counter() - t_traj
     ctx = twosd.SDContext(sp2, sto, device=device.index)
     ctx.compute_basis(x, smps.mean_values(sto, positions))
@@ -291,11 +298,12 @@ def main():
         pool_at["last_ms"] = dict(zip(("train", "keys", "build", "host_upload", "total", "candidates"), ms))
         return time.perf_counter() - t0
 
+    step_obj = {"value": None}   # incumbent objective of the last step
     heads_at = {}    # first pool bases at each x point (the pooled CPU baseline starts from the same bases)
 
-    def step(xx, rec=None):
+    def step(xx, rec=None, per_x_stats=True):
         t_ref = refresh(xx)
-        if rec:
+        if rec and per_x_stats:
             per_x[cur["xi"]]["refresh"] += t_ref
             if t_ref > 0:
                 per_x[cur["xi"]]["refresh_parts"] = {k_: round(v, 2) for k_, v in pool_at["last_ms"].items()}
@@ -306,6 +314,7 @@ def main():
         if t_ref == 0.0:
             ctx.invalidate_x()
         alpha = 0.0
+        objective = 0.0
         for epi_e, tw in zip(epis, total_weights):
             if args.no_dedup:
                 twosd.solve_batch(epi_e, xx, 0, n_local, want_pi=False)
@@ -319,12 +328,18 @@ def main():
                     V.truncate(nv)
                     sdist.push_sharded(V, new)
                 V.truncate(nv)
+            # incumbent objective at xx: sum_s w_s obj_s / sum_s w_s of the epigraph's scenarios (device
+            # reduction of the solve; across ranks all-reduced together with the cut partials)
+            obj_sums = ctx.last_objective()
             if world == 1:
                 alpha += twosd.build_sasa_cut(epi_e, xx, V, args.tie_rel).alpha / E
             else:
-                alpha += sdist.build_cut_sharded(ctx, epi_e, xx, tw, args.tie_rel, device)[0] / E
+                a_, _, obj_sums = sdist.build_cut_sharded(ctx, epi_e, xx, tw, args.tie_rel, device, extra=obj_sums)
+                alpha += a_ / E
+            objective += obj_sums[0] / obj_sums[1] / E
             if rec:
                 rec()      # per-epigraph kernel timings (HIP events of the last calls)
+        step_obj["value"] = objective
         return alpha
 
     def barrier():
@@ -362,6 +377,7 @@ def main():
         alpha = step(xs[i % X], record)
         px = per_x[i % X]
         px["wall"] += time.perf_counter() - ts; px["steps"] += 1; px["alpha"] = alpha
+        px["objective"] = step_obj["value"]
         step_log.append([i % X, round(1e3 * (time.perf_counter() - ts), 2), round(1e3 * (px["refresh"] - r0), 2),
                          round(cur["lp"] / 1e3, 2), round(cur["piv"] / max(n_local * E, 1), 3)])
     barrier()
@@ -375,6 +391,38 @@ def main():
     K = args.steps
     ms_step = 1e3 * elapsed / K
     value = N * K / elapsed
+
+    # trajectory: K distinct consecutive SD candidates (no revisits), each step refreshing at its
+    # new x like a real SD run; timed like the cycle (barrier + synchronize, max over ranks)
+    traj = None
+    if xs_traj:
+        tr_log = []
+        tr_piv = 0
+        barrier()
+        t0 = time.perf_counter()
+        for it, xx in zip(traj_iters, xs_traj):
+            cur["piv"] = 0; cur["lp"] = 0.0
+            ts = time.perf_counter()
+            step(xx, lambda: cur.update(piv=cur["piv"] + ctx.lp_stats()[0], lp=cur["lp"] + ctx.timings_us()[0]),
+                 per_x_stats=False)
+            tr_piv += cur["piv"]
+            tr_log.append([it, round(1e3 * (time.perf_counter() - ts), 2), round(cur["lp"] / 1e3, 2),
+                           round(cur["piv"] / max(n_local * E, 1), 3), step_obj["value"]])
+        barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=device)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            el = float(t.item())
+        Kt = len(xs_traj)
+        traj = {"value": N * Kt / el, "unit": "subproblems/s", "steps": Kt, "ms_per_step": 1e3 * el / Kt,
+                "sd_iterations": [traj_iters[0], traj_iters[-1]],
+                "rel_step_mean": float(np.mean([np.linalg.norm(b - a) / np.linalg.norm(a)
+                                                for a, b in zip([xs[-1]] + xs_traj[:-1], xs_traj)])),
+                "lp_pivots_mean": tr_piv / (Kt * max(n_local * E, 1)),
+                "steps_log": {"columns": ["sd_iteration", "ms", "lp_kernel_ms", "lp_pivots_mean", "incumbent_objective"],
+                              "rows": tr_log},
+                "note": "distinct consecutive SD candidates after the cycle's last point, pool refreshed at every x"}
 
     k = len(positions)
     passes = K * E                 # LP launches / cut passes in the timed region
@@ -396,7 +444,8 @@ def main():
                  "pool_refresh_parts_ms": px.get("refresh_parts"),
                  "lp_kernel_ms": px["lp"] / 1e3 / max(px["steps"], 1),
                  "lp_pivots_mean": px["piv"] / max(px["n"], 1),
-                 "alpha": px["alpha"]}
+                 "alpha": px["alpha"],
+                 "incumbent_objective": px.get("objective")}
                 for it, xx, px in zip(x_iters, xs, per_x)]
 
     out = {
@@ -435,6 +484,9 @@ def main():
         "lp_pivots_mean": piv_sum / (passes * n_local), "lp_pivots_max": piv_max,
         "x_points": x_points,
         "steps_log": {"columns": ["x_index", "ms", "refresh_ms", "lp_kernel_ms", "lp_pivots_mean"], "rows": step_log},
+        "tie_rule": ("strict '>' (the reference's argmax_procedure, subprob.jl:156)" if args.tie_rel == 0 else
+                     f"near-tie: lowest vertex index within {args.tie_rel:g} (1 + |max|) of the maximum"),
+        "trajectory": traj,
         "roofline": {"kernel": "lp_hyper_kernel", "bound": "mfma",
                      "note": "fp64 peak (vector == matrix on gfx950); achieved = counted fp64 FLOPs of the executed pivot path / LP kernel time",
                      "achieved": lp_tflops, "peak": PEAK_FP64_TFS, "unit": "TFLOP/s",
@@ -548,9 +600,21 @@ def spot_check(sp2, ctx, epi, V, xs, x_iters, positions, args):
         ok = (st == 0) & (o_st == 0)
         lp_err = float(np.max(np.abs(obj[ok] - o_obj[ok]) / (1.0 + np.abs(o_obj[ok])))) if ok.any() else None
         cut = twosd.build_sasa_cut(sub, xx, V, args.tie_rel)
-        a, b, _, _ = cpu.build_cut(sp2.r, T, xx, Vm, rows, DR, np.ones(n), tie_rel=args.tie_rel, nthreads=threads)
+        a, b, omv, _ = cpu.build_cut(sp2.r, T, xx, Vm, rows, DR, np.ones(n), tie_rel=args.tie_rel, nthreads=threads)
+        # near ties: scenarios whose two best vertex scores agree to 1e-9 relative (there the strict
+        # '>' of the reference picks by the last bits of the summation order, so alpha and beta may
+        # differ while the cut value alpha + beta'x = sum_s p_s max_val_s does not)
+        scores = (Vm @ (sp2.r - T @ xx))[None, :] + DR @ Vm[:, rows].T
+        top2 = np.sort(scores, axis=1)[:, -2:] if Vm.shape[0] > 1 else np.hstack([scores, scores - 1.0])
+        ties = int(((top2[:, 1] - top2[:, 0]) <= 1e-9 * (1.0 + np.abs(top2[:, 1]))).sum())
+        cv_gpu = cut.alpha + float(cut.beta @ xx)
+        cv_cpu = float(np.mean(omv))
         res.append({"x_iteration": it, "scenarios": n, "lp_not_optimal": int((~ok).sum()),
                     "lp_obj_max_rel_err": lp_err,
+                    "incumbent_objective_rel_err": abs(float(np.mean(obj[ok])) - float(np.mean(o_obj[ok]))) /
+                    (1.0 + abs(float(np.mean(o_obj[ok])))) if ok.any() else None,
+                    "cut_value_rel_err": abs(cv_gpu - cv_cpu) / (1.0 + abs(cv_cpu)),
+                    "near_tie_scenarios": ties,
                     "alpha_rel_err": abs(cut.alpha - a) / (1.0 + abs(a)),
                     "beta_max_rel_err": float(np.max(np.abs(cut.beta - b)) / (1.0 + np.max(np.abs(b))))})
     return res

@@ -133,10 +133,21 @@ int twosd_last_refresh_ms(twosd_ctx *ctx, double *ms5);
  *   4. twosd_refresh_assemble: from the G gathered packs (DEVICE, `stride` bytes apart, rank
  *      order), the pool = primary + the sources order[0, R) (source ids: 1 + the rank-major
  *      position of a base among all packs), with the union box_lo/box_hi[k] of the slices.
+ *      R = 0 (no optimal training scenario on any rank) keeps the current pool, as
+ *      twosd_pool_refresh does.
  * Selection becomes flat; twosd_pool_candidate_picks / twosd_pool_set_candidates split the
  * two-level candidate lists the same way (picks of each rank's slice, lists from all picks). */
 int twosd_refresh_train(twosd_ctx *ctx, int epi, const double *x, int first, int count, int *n_bases, double *box_lo,
                         double *box_hi);
+/* The training solve of step 1 under a cap the ranks agree on: kcap > 0 pivots (<= 0: none), one
+ * launch, no retry; *n_optimal = training scenarios of the slice that ended optimal.  The caller
+ * derives kcap from every rank's twosd_refresh_cap_stats (pivot sum and size of the last batch of
+ * >= 4096 scenarios: 3 x the global mean, at least 32) and, when fewer than half of ALL ranks'
+ * training scenarios ended optimal, calls it again with kcap = 0 on every rank -- the rule
+ * twosd_pool_refresh applies to one rank, decided once for all of them. */
+int twosd_refresh_train_ex(twosd_ctx *ctx, int epi, const double *x, int first, int count, int kcap, int *n_bases,
+                           int *n_optimal, double *box_lo, double *box_hi);
+int twosd_refresh_cap_stats(twosd_ctx *ctx, int64_t *pivots_sum, int64_t *scenarios);
 int twosd_refresh_train_bases(twosd_ctx *ctx, uint64_t *keys, int *counts, int *reps);
 int twosd_refresh_build_local(twosd_ctx *ctx, int n_own, const int *reps, int64_t *pack_bytes);
 int twosd_refresh_pack(twosd_ctx *ctx, void *d_dst);
@@ -262,11 +273,19 @@ int twosd_last_timings(twosd_ctx *ctx, double *us5);
 /* Statistics of the last LP batch: sum of simplex pivots, max pivots. */
 int twosd_last_lp_stats(twosd_ctx *ctx, int64_t *pivots_sum, int *pivots_max);
 
+/* Incumbent objective of the last twosd_solve_batch / twosd_solve_push / twosd_solve_values
+ * batch: *weighted_sum = sum_s w_s obj_s and *weight_sum = sum_s w_s over its scenarios (the
+ * epigraph's add_scenario! weights; 1.0 for solve_values), reduced in a fixed order (the same
+ * bits on every run).  weighted_sum / weight_sum is the sample-average recourse at x that
+ * evaluate (smps_routines.jl:67-82) and the incumbent estimate of sd_iteration! form; across
+ * ranks the caller adds the ranks' sums (north star: the all-reduce of the incumbent objective). */
+int twosd_last_objective(twosd_ctx *ctx, double *weighted_sum, double *weight_sum);
+
 /* Diagnostic: pivots and status of every scenario of the last LP launch (by scenario index;
  * after a pool refresh: its training solves). */
 int twosd_last_lp_iters(twosd_ctx *ctx, int N, int *iters, int *status);
 
-/* Pivot cap of the training solves of a pool refresh: > 0 explicit, 0 auto (default: 4 x the
+/* Pivot cap of the training solves of a pool refresh: > 0 explicit, 0 auto (default: 3 x the
  * mean pivots of the last batch of >= 4096 scenarios, at least 32; none before such a batch),
  * < 0 none (the kernel's kmax).  A training scenario that needs more pivots drops out of the
  * basis count instead of holding the launch: one wavefront per scenario, so a launch lasts as

@@ -71,6 +71,9 @@ SIGNATURES = [
     ("twosd_last_lp_iters", I, [P, I, P, P]),
     ("twosd_set_refresh_kcap", I, [P, I]),
     ("twosd_refresh_train", I, [P, I, P, I, I, P, P, P]),
+    ("twosd_refresh_train_ex", I, [P, I, P, I, I, I, P, P, P, P]),
+    ("twosd_refresh_cap_stats", I, [P, P, P]),
+    ("twosd_last_objective", I, [P, P, P]),
     ("twosd_refresh_train_bases", I, [P, P, P, P]),
     ("twosd_refresh_build_local", I, [P, I, P, P]),
     ("twosd_refresh_pack", I, [P, P]),

@@ -259,7 +259,7 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_rt_pack); dfree(c->d_gs_heads); dfree(c->d_gs_cnt); dfree(c->d_gs_tot); dfree(c->d_gs_valid);
     dfree(c->d_gs_irow); dfree(c->d_gs_ioff); dfree(c->d_gs_ival);
     if (c->d_gs_seg) { hipFree(c->d_gs_seg); c->d_gs_seg = nullptr; c->gs_seg_cap = 0; }
-    c->rt_epi = -1; c->rt_nown = -1;
+    c->rt_epi = -1; c->rt_nown = -1; c->rt_trained = false;
     if (c->pool_hb) { hipHostFree(c->pool_hb); c->pool_hb = nullptr; c->pool_hb_cap = 0; }
     c->has_template = c->has_basis = false;
 }
@@ -681,6 +681,7 @@ extern "C" int twosd_pool_size(twosd_ctx *c, int *size) {
 }
 
 extern "C" int twosd_pool_get(twosd_ctx *c, int p, int *head) {
+    if (c && !c->has_basis) return fail(TWOSD_E_STATE, "pool_get: no basis");
     if (!c || !head || p < 0 || p >= (int)c->pool.size()) return fail(TWOSD_E_ARG, "pool_get: basis %d of %zu", p, c ? c->pool.size() : 0);
     const std::vector<int> &h = head_of(c, p);
     std::copy(h.begin(), h.end(), head);
@@ -914,6 +915,9 @@ static int pg_assemble(twosd_ctx *c, PgArgs &A, const int *h_tot, const int *h_v
     // arrays that no longer hold it.  The context then drops its basis, so every later solve
     // fails cleanly (TWOSD_E_STATE) until twosd_compute_basis / twosd_set_basis installs one.
     auto broken = [c](int code) {
+        // the device-built bases read their heads lazily from pool_hb, which the failing path may
+        // have reallocated or overwritten: keep only the primary (a host basis)
+        if (c->pool.size() > 1) c->pool.resize(1);
         c->has_basis = false;
         c->prep_valid = false;
         c->k_valid = false;
@@ -1015,14 +1019,14 @@ static int train_kcap(const twosd_ctx *c) {
 // 58.5 pivots a scenario against a cap of 35), most training scenarios hit the cap and the
 // refresh would find almost no optimal bases.  If fewer than half end optimal, the training is
 // solved again without a cap (one extra launch, only on such a jump).
-static int refresh_training(twosd_ctx *c, const double *x, const double *d_dv, int count) {
+static int refresh_training(twosd_ctx *c, const double *x, const double *d_dv, int count, int kcap, bool retry, int *n_opt) {
     LpRun o;
     o.want_bkey = true;
     o.want_etas = true;
     o.want_head = true;
     // training scenarios beyond the pivot cap only drop out of the basis count (one launch
     // lasts as long as its slowest scenario: with one scenario per wave the cap bounds it)
-    o.kcap = train_kcap(c);
+    o.kcap = kcap;
     int rc;
     if ((rc = run_lp_ex(c, x, d_dv, count, o))) return rc;
     int opt = count;
@@ -1030,13 +1034,14 @@ static int refresh_training(twosd_ctx *c, const double *x, const double *d_dv, i
         std::vector<int> st(count);
         HIPCHK(hipMemcpy(st.data(), c->d_status, sizeof(int) * count, hipMemcpyDeviceToHost));
         opt = (int)std::count(st.begin(), st.end(), (int)TWOSD_LP_OPTIMAL);
-        if (2 * opt < count) {
+        if (retry && 2 * opt < count) {
             if (getenv("TWOSD_DEBUG")) fprintf(stderr, "refresh training: %d of %d optimal under cap %d, solved again uncapped\n", opt, count, o.kcap);
             o.kcap = 0;
             if ((rc = run_lp_ex(c, x, d_dv, count, o))) return rc;
         }
     }
     c->last_train_opt = opt;
+    if (n_opt) *n_opt = opt;
     return TWOSD_OK;
 }
 
@@ -1054,7 +1059,7 @@ extern "C" int twosd_pool_refresh(twosd_ctx *c, int epi, const double *x, int fi
     const double *d_dv = E.d_dv + (size_t)first * c->k;
     int rc;
     // 1. training solves at x from the current pool: basis keys, eta files and heads by scenario
-    if ((rc = refresh_training(c, x, d_dv, count))) return rc;
+    if ((rc = refresh_training(c, x, d_dv, count, train_kcap(c), true, nullptr))) return rc;
     if (getenv("TWOSD_DEBUG")) {
         std::vector<int> st(count), itv(count);
         HIPCHK(hipMemcpy(st.data(), c->d_status, sizeof(int) * count, hipMemcpyDeviceToHost));
@@ -1246,8 +1251,10 @@ static int rt_copy(twosd_ctx *c, const std::vector<CopySeg> &segs) {
     return TWOSD_OK;
 }
 
-extern "C" int twosd_refresh_train(twosd_ctx *c, int epi, const double *x, int first, int count, int *n_bases,
-                                   double *box_lo, double *box_hi) {
+// kcap: the training pivot cap (> 0; <= 0 none); retry: solve again uncapped when fewer than
+// half end optimal (the single-rank rule, decided by this rank alone)
+static int refresh_train_impl(twosd_ctx *c, int epi, const double *x, int first, int count, int kcap, bool retry,
+                              int *n_bases, int *n_opt, double *box_lo, double *box_hi) {
     if (!c || !c->has_basis) return fail(TWOSD_E_STATE, "refresh_train: no primary basis");
     if (epi < 0 || epi >= (int)c->epis.size()) return fail(TWOSD_E_ARG, "refresh_train: epigraph %d does not exist", epi);
     const EpiDevice &E = c->epis[epi];
@@ -1258,7 +1265,8 @@ extern "C" int twosd_refresh_train(twosd_ctx *c, int epi, const double *x, int f
     const auto t0 = std::chrono::steady_clock::now();
     const double *d_dv = E.d_dv + (size_t)first * c->k;
     int rc;
-    if ((rc = refresh_training(c, x, d_dv, count))) return rc;   // as twosd_pool_refresh step 1
+    c->rt_trained = false;
+    if ((rc = refresh_training(c, x, d_dv, count, kcap, retry, n_opt))) return rc;   // as twosd_pool_refresh step 1
     const auto t1 = std::chrono::steady_clock::now();
     const int *d_list = nullptr, *d_counts = nullptr;
     int U = 0;
@@ -1284,19 +1292,31 @@ extern "C" int twosd_refresh_train(twosd_ctx *c, int epi, const double *x, int f
                 c->rt_lo[e] = std::min(c->rt_lo[e], dv[(size_t)s2 * c->k + e]);
                 c->rt_hi[e] = std::max(c->rt_hi[e], dv[(size_t)s2 * c->k + e]);
             }
-        c->rt_epi = epi; c->rt_first = first; c->rt_count = count; c->rt_n = E.count;
     }
+    c->rt_epi = epi; c->rt_first = first; c->rt_count = count; c->rt_n = E.count;
     if (box_lo) std::copy(c->rt_lo.begin(), c->rt_lo.end(), box_lo);
     if (box_hi) std::copy(c->rt_hi.begin(), c->rt_hi.end(), box_hi);
     c->rt_nown = -1;
+    c->rt_trained = true;
     c->last_refresh_ms[0] = std::chrono::duration<double, std::milli>(t1 - t0).count();
     c->last_refresh_ms[1] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
     *n_bases = U;
     return TWOSD_OK;
 }
 
+extern "C" int twosd_refresh_train(twosd_ctx *c, int epi, const double *x, int first, int count, int *n_bases,
+                                   double *box_lo, double *box_hi) {
+    if (!c) return fail(TWOSD_E_ARG, "refresh_train: NULL context");
+    return refresh_train_impl(c, epi, x, first, count, train_kcap(c), true, n_bases, nullptr, box_lo, box_hi);
+}
+
+extern "C" int twosd_refresh_train_ex(twosd_ctx *c, int epi, const double *x, int first, int count, int kcap, int *n_bases,
+                                      int *n_optimal, double *box_lo, double *box_hi) {
+    return refresh_train_impl(c, epi, x, first, count, kcap > 0 ? kcap : 0, false, n_bases, n_optimal, box_lo, box_hi);
+}
+
 extern "C" int twosd_refresh_train_bases(twosd_ctx *c, uint64_t *keys, int *counts, int *reps) {
-    if (!c || c->rt_epi < 0) return fail(TWOSD_E_STATE, "refresh_train_bases: no training solve (twosd_refresh_train)");
+    if (!c || !c->rt_trained) return fail(TWOSD_E_STATE, "refresh_train_bases: no training solve (twosd_refresh_train)");
     const size_t U = c->rt_keys.size();
     if (keys) std::copy(c->rt_keys.begin(), c->rt_keys.end(), keys);
     if (counts) std::copy(c->rt_counts.begin(), c->rt_counts.end(), counts);
@@ -1305,7 +1325,7 @@ extern "C" int twosd_refresh_train_bases(twosd_ctx *c, uint64_t *keys, int *coun
 }
 
 extern "C" int twosd_refresh_build_local(twosd_ctx *c, int n_own, const int *reps, int64_t *pack_bytes) {
-    if (!c || c->rt_epi < 0) return fail(TWOSD_E_STATE, "refresh_build_local: no training solve (twosd_refresh_train)");
+    if (!c || !c->rt_trained) return fail(TWOSD_E_STATE, "refresh_build_local: no training solve (twosd_refresh_train)");
     if (n_own < 0 || (n_own > 0 && !reps) || !pack_bytes) return fail(TWOSD_E_ARG, "refresh_build_local: bad arguments");
     for (int j = 0; j < n_own; ++j)
         if (reps[j] < 0 || reps[j] >= c->rt_count) return fail(TWOSD_E_ARG, "refresh_build_local: representative %d outside the slice", reps[j]);
@@ -1452,11 +1472,17 @@ extern "C" int twosd_refresh_assemble(twosd_ctx *c, int G, const void *d_packs, 
     A.tot = c->d_gs_tot; A.nztot = c->d_gs_tot + 4 * nsrc; A.valid = c->d_gs_valid;
     A.inter_off = c->d_gs_ioff; A.inter_row = c->d_gs_irow; A.inter_val = c->d_gs_ival;
     A.gheads = c->d_gs_heads;
-    std::vector<int> ord(R + 1);
-    ord[0] = 0;
-    std::copy(order, order + R, ord.begin() + 1);
-    if ((rc = pg_assemble(c, A, h_tot, h_valid, ord)) != 0)
-        return rc < 0 ? rc : fail(TWOSD_E_STATE, "refresh_assemble: the primary basis failed the device checks");
+    // R == 0 (no rank had an optimal training scenario, or max_pool <= 1): the current pool stays,
+    // as in twosd_pool_refresh (falling back to the primary basis alone costs ~90 pivots a scenario)
+    if (R > 0) {
+        std::vector<int> ord(R + 1);
+        ord[0] = 0;
+        std::copy(order, order + R, ord.begin() + 1);
+        if ((rc = pg_assemble(c, A, h_tot, h_valid, ord)) != 0)
+            return rc < 0 ? rc : fail(TWOSD_E_STATE, "refresh_assemble: the primary basis failed the device checks");
+    } else {
+        c->prep_valid = false;   // the selection box below changes
+    }
     // selection box: the union of the ranks' training boxes
     if (c->k > 0) {
         c->sel_lo.assign(box_lo, box_lo + c->k);
@@ -1464,6 +1490,7 @@ extern "C" int twosd_refresh_assemble(twosd_ctx *c, int G, const void *d_packs, 
         c->box_epi = -1;   // not the single-rank cache
     }
     c->rt_nown = -1;
+    c->rt_trained = false;
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     c->last_refresh_ms[3] = ms;
     c->last_refresh_ms[4] = c->last_refresh_ms[0] + c->last_refresh_ms[1] + c->last_refresh_ms[2] + ms;
@@ -1731,7 +1758,7 @@ extern "C" int twosd_add_sampled_scenarios(twosd_ctx *c, int epi, int N, uint64_
     return TWOSD_OK;
 }
 
-static int copy_lp_outputs(twosd_ctx *c, int N, double *obj, double *pi, double *y, int *status);
+static int copy_lp_outputs(twosd_ctx *c, int N, double *obj, double *pi, double *y, int *status, const double *d_w);
 
 // evaluate(sp1, sp2, sto, x; N) stage-2 part (smps_routines.jl:67-82) on device-drawn
 // scenarios: *s2 = sum over scenarios first..first+count-1 of the stream `seed`, in index
@@ -1760,7 +1787,7 @@ extern "C" int twosd_evaluate_sampled(twosd_ctx *c, const double *x, int64_t N_t
         HIPCHK(launch_sample(S, c->stream));
         if ((rc = run_lp(c, x, c->d_dvtmp, n, false, false))) return rc;
         obj.resize(n);
-        if ((rc = copy_lp_outputs(c, n, obj.data(), nullptr, nullptr, nullptr))) return rc;
+        if ((rc = copy_lp_outputs(c, n, obj.data(), nullptr, nullptr, nullptr, nullptr))) return rc;
         for (int i = 0; i < n; ++i) acc += invN * obj[i];
     }
     *s2 = acc;
@@ -2240,7 +2267,7 @@ int twosd::run_lp_ex(twosd_ctx *c, const double *x, const double *d_dv, int N, c
         const int kmax = c->kmax_override > 0 ? c->kmax_override : std::min(256, std::max(64, 2 * m + 32));
         const int ecap = std::max(4096, 32 * MP);
         const int CH = c->CH;
-        int bpc = hyper_max_blocks_per_cu(R, CH, n + m, kmax, c->k);
+        int bpc = hyper_max_blocks_per_cu(R, CH, kmax, c->k);
         if (const char *e = getenv("TWOSD_BPC")) bpc = std::min(bpc, std::max(1, atoi(e)));   // diagnostics: occupancy sweep
         if (bpc < 1) return fail(TWOSD_E_UNSUPPORTED, "LP kernel: LDS slice too large (m = %d, k = %d)", m, c->k);
         const int nblocks = std::max(1, std::min((NL + kWavesPerBlock - 1) / kWavesPerBlock, bpc * c->num_cus));
@@ -2334,7 +2361,7 @@ int twosd::run_lp_ex(twosd_ctx *c, const double *x, const double *d_dv, int N, c
             H.order = c->d_order;
         }
         HIPCHK(hipEventRecord(c->ev[2], c->stream));
-        HIPCHK(launch_hyper(R, CH, H, nblocks, hyper_lds_bytes(R, n + m, kmax, c->k), c->stream));
+        HIPCHK(launch_hyper(R, CH, H, nblocks, hyper_lds_bytes(R, CH, kmax, c->k), c->stream));
         HIPCHK(hipEventRecord(c->ev[1], c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         float ms = 0, ms_sel = 0;
@@ -2377,26 +2404,89 @@ __global__ void lp_stats_kernel(int N, const int *__restrict__ its, const long l
     }
 }
 
-static int copy_lp_outputs(twosd_ctx *c, int N, double *obj, double *pi, double *y, int *status) {
+// incumbent objective of a batch: sum_s w_s obj_s and sum_s w_s (w = 1 without weights), each
+// block over a fixed stride of scenarios, then a fixed tree in the block; the host adds the
+// kObjBlocks partials in block order, so the sums do not depend on scheduling
+constexpr int kObjBlocks = 256;
+__global__ void __launch_bounds__(256) lp_obj_kernel(int N, const double *__restrict__ obj, const double *__restrict__ w,
+                                                     double *__restrict__ part) {
+    __shared__ double sa[256], sb[256];
+    double a = 0.0, b = 0.0;
+    for (int s = blockIdx.x * 256 + threadIdx.x; s < N; s += kObjBlocks * 256) {
+        const double ws = w ? w[s] : 1.0;
+        a = fma(ws, obj[s], a);
+        b += ws;
+    }
+    sa[threadIdx.x] = a;
+    sb[threadIdx.x] = b;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            sa[threadIdx.x] += sa[threadIdx.x + o];
+            sb[threadIdx.x] += sb[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = sa[0];
+        part[2 * blockIdx.x + 1] = sb[0];
+    }
+}
+
+// d_w: the batch's scenario weights (nullable: 1.0), for the objective sum
+static int copy_lp_outputs(twosd_ctx *c, int N, double *obj, double *pi, double *y, int *status, const double *d_w) {
     if (!c->d_lpstats) {
         int rc = dalloc(&c->d_lpstats, 4);
+        if (rc) return rc;
+    }
+    if (!c->d_objpart) {
+        int rc = dalloc(&c->d_objpart, (size_t)2 * kObjBlocks);
         if (rc) return rc;
     }
     HIPCHK(hipMemsetAsync(c->d_lpstats, 0, 4 * sizeof(unsigned long long), c->stream));
     hipLaunchKernelGGL(lp_stats_kernel, dim3((unsigned)std::min(1024, (N + 255) / 256)), dim3(256), 0, c->stream, N,
                        c->d_iters, c->d_ops, c->d_status, c->d_lpstats);
     HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(lp_obj_kernel, dim3(kObjBlocks), dim3(256), 0, c->stream, N, c->d_obj, d_w, c->d_objpart);
+    HIPCHK(hipGetLastError());
     unsigned long long stv[4];
+    double part[2 * kObjBlocks];
     HIPCHK(hipMemcpyAsync(stv, c->d_lpstats, sizeof(stv), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(part, c->d_objpart, sizeof(part), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     if (obj) HIPCHK(hipMemcpy(obj, c->d_obj, sizeof(double) * N, hipMemcpyDeviceToHost));
     if (pi) HIPCHK(hipMemcpy(pi, c->d_pi, sizeof(double) * N * c->L.m, hipMemcpyDeviceToHost));
     if (y) HIPCHK(hipMemcpy(y, c->d_y, sizeof(double) * N * c->L.n, hipMemcpyDeviceToHost));
     if (status) HIPCHK(hipMemcpy(status, c->d_status, sizeof(int) * N, hipMemcpyDeviceToHost));
     c->last_pivots_sum = (int64_t)stv[0]; c->last_ops_sum = (int64_t)stv[1]; c->last_pivots_max = (int)stv[2];
-    if (N >= 4096) c->piv_mean_ref = (double)stv[0] / N;
+    if (N >= 4096) {
+        c->piv_mean_ref = (double)stv[0] / N;
+        c->piv_ref_sum = (int64_t)stv[0];
+        c->piv_ref_n = N;
+    }
+    double ow = 0.0, wt = 0.0;
+    for (int b = 0; b < kObjBlocks; ++b) {
+        ow += part[2 * b];
+        wt += part[2 * b + 1];
+    }
+    c->last_obj_wsum = ow;
+    c->last_obj_w = wt;
     const long long bad = (long long)stv[3];
     if (bad) return fail(TWOSD_E_LP, "%lld of %d scenario LPs not optimal (see status[])", bad, N);
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_last_objective(twosd_ctx *c, double *weighted_sum, double *weight_sum) {
+    if (!c) return fail(TWOSD_E_ARG, "last_objective: NULL");
+    if (weighted_sum) *weighted_sum = c->last_obj_wsum;
+    if (weight_sum) *weight_sum = c->last_obj_w;
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_refresh_cap_stats(twosd_ctx *c, int64_t *pivots_sum, int64_t *scenarios) {
+    if (!c) return fail(TWOSD_E_ARG, "refresh_cap_stats: NULL");
+    if (pivots_sum) *pivots_sum = c->piv_ref_sum;
+    if (scenarios) *scenarios = c->piv_ref_n;
     return TWOSD_OK;
 }
 
@@ -2412,7 +2502,7 @@ extern "C" int twosd_solve_batch(twosd_ctx *c, int epi, const double *x, int fir
     HIPCHK(hipSetDevice(c->device));
     int rc = run_lp(c, x, E.d_dv + (size_t)first * c->k, count, pi != nullptr, y != nullptr);
     if (rc) return rc;
-    return copy_lp_outputs(c, count, obj, pi, y, status);
+    return copy_lp_outputs(c, count, obj, pi, y, status, E.d_w + first);
 }
 
 extern "C" int twosd_solve_values(twosd_ctx *c, const double *x, int N, const double *values, double *obj, double *pi,
@@ -2430,7 +2520,7 @@ extern "C" int twosd_solve_values(twosd_ctx *c, const double *x, int N, const do
     if ((rc = dgrow(&c->d_dvtmp, &c->dvtmp_cap, (size_t)N * std::max(k, 1), 0, c->stream))) return rc;
     HIPCHK(hipMemcpy(c->d_dvtmp, dv.data(), sizeof(double) * dv.size(), hipMemcpyHostToDevice));
     if ((rc = run_lp(c, x, c->d_dvtmp, N, pi != nullptr, y != nullptr))) return rc;
-    return copy_lp_outputs(c, N, obj, pi, y, status);
+    return copy_lp_outputs(c, N, obj, pi, y, status, nullptr);
 }
 
 extern "C" int twosd_last_timings(twosd_ctx *c, double *us5) {
@@ -2503,8 +2593,9 @@ extern "C" int twosd_solve_push(twosd_ctx *c, int epi, const double *x, int firs
     int rc = run_lp_ex(c, x, d_dv, count, o);
     if (rc) return rc;
     const double t_lp = c->t_us[0], t_sel = c->t_us[4];
-    rc = copy_lp_outputs(c, count, obj, nullptr, nullptr, status);
+    rc = copy_lp_outputs(c, count, obj, nullptr, nullptr, status, E.d_w + first);
     if (rc) return rc;   // some LP not optimal: nothing pushed
+    const double obj_wsum = c->last_obj_wsum, obj_w = c->last_obj_w;
     const int64_t piv_sum = c->last_pivots_sum, ops_sum = c->last_ops_sum;
     const int piv_max = c->last_pivots_max;
     float ms = 0, ms_key = 0;
@@ -2552,6 +2643,7 @@ extern "C" int twosd_solve_push(twosd_ctx *c, int epi, const double *x, int firs
         c->t_us[4] = t_sel;
         c->last_pivots_sum = piv_sum; c->last_ops_sum = ops_sum; c->last_pivots_max = piv_max;
     }
+    c->last_obj_wsum = obj_wsum; c->last_obj_w = obj_w;   // of the batch, not of the representatives' re-solve
     c->t_us[1] = 1e3 * (ms + ms_key);
     if (new_size) *new_size = c->dvs.size;
     return TWOSD_OK;

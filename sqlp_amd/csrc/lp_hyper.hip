@@ -19,6 +19,7 @@
 // rounding.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <type_traits>
 #include "twosd_internal.h"
 #include "wave_ops.h"
 
@@ -133,12 +134,12 @@ __device__ __forceinline__ int h_seg_scatter(int p0, int len, double v, const in
     }
     return T;
 }
-__device__ __forceinline__ double h_infeas(double x, int bt) {
-    if (bt == BT_Y || bt == BT_L) return x < -HTOL_P ? x : 0.0;
-    if (bt == BT_G) return x > HTOL_P ? x : 0.0;
-    return fabs(x) > HTOL_P ? x : 0.0;
+// sign bit of an fp64 value as a 64-bit mask: flip(v, 1) = -v, exactly
+__device__ __forceinline__ double h_flip(double v, uint64_t signmask) {
+    return __longlong_as_double(__double_as_longlong(v) ^ (long long)signmask);
 }
 
+// register-array element p = 64 * slot + lane (p uniform)
 template <int R>
 __device__ __forceinline__ int h_get_row_i(const int (&a)[R], int p) {
     // one readlane per slot and a scalar select: a select chain over a[t] is folded by the
@@ -159,55 +160,30 @@ __device__ __forceinline__ int h_prefix_count(uint64_t m) {
 }
 
 // per-wave LDS slice: a union of {ut, rho} (MP doubles each) and alpha (the pivot row over the
-// ncol = n + m real columns during pricing), the scenario deltas (k doubles), the pricing list
+// 64C column slots during pricing; the columns past n + m are never scattered to, so every slot
+// can be read and zeroed unconditionally), the scenario deltas (k doubles), the pricing list
 // values (64 doubles), the dual Devex weights (MP floats), the pricing list rows and row-start
 // marks (64 ints each), etap (u16), etaoff (int)
-static __host__ __device__ inline int hyper_union_doubles(int R, int ncol) {
-    const int a = (ncol + 1) & ~1;
-    return 128 * R > a ? 128 * R : a;
+static __host__ __device__ inline int hyper_union_doubles(int R, int C) {
+    return 128 * R > 64 * C ? 128 * R : 64 * C;
 }
-// + the pricing list: the nonzeros of rho, (row, value), 64 per batch, and its row-start marks
-static __host__ __device__ inline size_t hyper_slice_bytes(int R, int ncol, int kmax, int k) {
+static __host__ __device__ inline size_t hyper_slice_bytes(int R, int C, int kmax, int k) {
     const int kmaxp = (kmax + 3) & ~3;
-    return 8 * (size_t)hyper_union_doubles(R, ncol) + 8 * (size_t)((k + 1) & ~1) + 8 * 64 + 4 * (size_t)(64 * R) + 4 * 64 +
+    return 8 * (size_t)hyper_union_doubles(R, C) + 8 * (size_t)((k + 1) & ~1) + 8 * 64 + 4 * (size_t)(64 * R) + 4 * 64 +
            4 * 64 + 2 * kmaxp + 4 * (kmaxp + 4);
 }
-size_t hyper_lds_bytes(int R, int ncol, int kmax, int k) { return (size_t)kWavesPerBlock * hyper_slice_bytes(R, ncol, kmax, k); }
+size_t hyper_lds_bytes(int R, int C, int kmax, int k) { return (size_t)kWavesPerBlock * hyper_slice_bytes(R, C, kmax, k); }
 
 // min waves per SIMD (VGPR budget 256 / 168): measured on MI355X, storm (R=9) is fastest
 // at 2 waves/SIMD, ssn (R=4) at 3 (tools/lp_speed.py)
-// loads in flight per memory round trip: etas per group (BTRAN / rho / FTRAN), W rows per
-// pricing group (A/B knobs of the development builds)
+// loads in flight per memory round trip: etas per group (BTRAN / FTRAN)
 #ifndef TWOSD_ETA_G
 #define TWOSD_ETA_G 2
 #endif
-#ifndef TWOSD_PRICE_G
-#define TWOSD_PRICE_G 4
-#endif
 constexpr int EG = TWOSD_ETA_G;
-// scatters into LDS (pricing, rho, FTRAN) as ds_add_f64 (1) or as read-fma-write chains (0)
-#ifndef TWOSD_LDS_ADD
-#define TWOSD_LDS_ADD 1
-#endif
-// pricing as a segmented scatter, 64 W entries per wave step (1), or one W row per step (0)
-#ifndef TWOSD_PRICE_SEG
-#define TWOSD_PRICE_SEG 1
-#endif
-// FTRAN: B0^{-1} a_q as one segmented scatter (1) or column group by column group (0)
-#ifndef TWOSD_FTRAN_SEG
-#define TWOSD_FTRAN_SEG 1
-#endif
-// rho = u' B0^{-1} as one segmented scatter (1) or row group by row group (0)
-#ifndef TWOSD_RHO_SEG
-#define TWOSD_RHO_SEG 1
-#endif
 // unroll of the per-scenario gathers (x_B warm start, vertex recovery): loads in flight
 #ifndef TWOSD_XB_UNROLL
 #define TWOSD_XB_UNROLL 2
-#endif
-// FTRAN: B0^{-1} columns of this many nonzeros of a_q loaded per round trip (1: one at a time)
-#ifndef TWOSD_FTRAN_G
-#define TWOSD_FTRAN_G 2
 #endif
 #ifndef TWOSD_REC_UNROLL
 #define TWOSD_REC_UNROLL 1
@@ -215,19 +191,38 @@ constexpr int EG = TWOSD_ETA_G;
 #ifndef TWOSD_HYPER_WPE
 #define TWOSD_HYPER_WPE(R) ((R) >= 9 ? 2 : 3)
 #endif
-template <int R, int C>
+
+// Reduced costs are kept SIGN-FOLDED: d'_j = s_j d_j with s_j = -1 for the columns nonbasic at
+// their upper bound (the slacks of G rows, [-inf, 0]) and +1 otherwise, and the pricing writes
+// alpha'_j = s_j alpha~_j (the structural columns have s_j = +1, so only the slack entry of a G
+// row flips).  Sign flips are exact and commute with every rounding, so the ratio test on
+// (d', alpha') takes exactly the decisions of the unfolded one (C oracle rules):
+//   eligible  <=>  s_j a_j > tol              (a_j = sg alpha~_j; was: at lb a > tol, at ub a < -tol)
+//   pass 1    nu = d'_j + tol, de = a'_j      (was: d + tol / tol - d, |a|)
+//   pass 2    d'_j <= thmax a'_j              (was: a > 0 ? d <= thmax a : d >= thmax a)
+//   theta_D = d'_q / a'_q = d_q / a_q,  d'_j -= theta_D a'_j.
+// The dual update runs over every slot: basic columns' d' are never read (candidates exclude
+// them, an entering column is set to 0, a leaving one to its new value, the dual key masks
+// them), and a nonbasic column with alpha = 0 keeps its value (d + 0).
+//
+// FULL = false: the main solve of solve_push / solve_batch without pi, y, heads, basis keys or
+// eta files -- the vertex recovery and the refresh outputs are compiled out (a smaller kernel:
+// fewer registers and instruction-cache lines).
+template <int R, int C, bool FULL>
 __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(HyperParams P) {
     extern __shared__ double lds_raw[];
+    using Mask = typename std::conditional<(C > 32), uint64_t, uint32_t>::type;
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     constexpr int MP = 64 * R;
+    constexpr int UD = 128 * R > 64 * C ? 128 * R : 64 * C;
     const int kmaxp = (P.kmax + 3) & ~3;
     const int ncol = P.n + P.m;
-    char *slice = reinterpret_cast<char *>(lds_raw) + (size_t)wid * hyper_slice_bytes(R, ncol, P.kmax, P.k);
+    char *slice = reinterpret_cast<char *>(lds_raw) + (size_t)wid * hyper_slice_bytes(R, C, P.kmax, P.k);
     double *ut = reinterpret_cast<double *>(slice);        // dense scratch vector (u, then alpha_q)
     double *rho = ut + MP;                                  // pivot row of B^{-1}
-    double *alpha = ut;                                     // pricing: alpha~_j over the same space
-    double *dvl = ut + hyper_union_doubles(R, ncol);        // this scenario's coef_e(x) dv_e
+    double *alpha = ut;                                     // pricing: alpha'_j over the same space
+    double *dvl = ut + UD;                                  // this scenario's coef_e(x) dv_e
     double *lstv = dvl + ((P.k + 1) & ~1);                  // pricing list: rho values
     float *w = reinterpret_cast<float *>(lstv + 64);        // dual Devex weights (row i at w[i])
     int *lsti = reinterpret_cast<int *>(w + MP);            // pricing list: rows
@@ -242,17 +237,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
     const uint64_t fixedm = P.fixedmask[lane];
     const uint64_t ubm = P.ubmask[lane];
 
-    // alpha back to zero over the ncol real columns: full slots unconditionally, the one
-    // partial slot by lane (uniform slot predicates: scalar branches, no exec-mask pairs)
-    const int ncol_full = ncol >> 6, ncol_rem = ncol & 63;
-    auto zero_alpha = [&]() {
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-            if (c < ncol_full) alpha[64 * c + lane] = 0.0;
-            else if (c == ncol_full && lane < ncol_rem) alpha[64 * c + lane] = 0.0;
-        }
-    };
-    for (int j = lane; j < hyper_union_doubles(R, ncol); j += 64) ut[j] = 0.0;
+    for (int j = lane; j < UD; j += 64) ut[j] = 0.0;
     smark[lane] = 0;
     h_wave_sync();
     STAMP_DECL
@@ -298,7 +283,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         int pb = P.npool > 1 ? __builtin_amdgcn_readfirstlane(P.pool_pick[s]) : 0;
         double xB[R];
         int hb[R];
-        double d[C];
+        double d[C];   // sign-folded reduced costs d'_j, j = 64c + lane
         uint64_t bmask;
         const int *brptr, *bcp;
         int K = 0, it = 0, status = TWOSD_LP_OPTIMAL;
@@ -316,7 +301,8 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             w[64 * t + lane] = 1.0f;
         }
 #pragma unroll
-        for (int c = 0; c < C; ++c) d[c] = P.d0[(size_t)pb * 64 * C + 64 * c + lane];
+        for (int c = 0; c < C; ++c)
+            d[c] = h_flip(P.d0[(size_t)pb * 64 * C + 64 * c + lane], ((ubm >> c) & 1) << 63);
         bmask = P.basic0[pb * 64 + lane];
         K = 0; status = TWOSD_LP_OPTIMAL; eoff = 0;
         nops += (long long)(P.kslot[pb * (R + 1) + R] - P.kslot[pb * (R + 1)]) * 64;
@@ -332,7 +318,6 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             int br = 0x7fffffff;
 #pragma unroll
             for (int t = 0; t < R; ++t) {
-                // h_infeas as flags, not per-bound-type branches (-2.2 % LP time, same pivots):
                 // below -tol counts unless the row is G, above +tol only for G / E (bt & 1);
                 // padding rows (hb < 0) never
                 const int bt = hb[t] & 3;
@@ -343,7 +328,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                     if (num * bden > bnum * den) { bnum = num; bden = den; br = 64 * t + lane; bdel = dl; }
                 }
             }
-            const ArgBest lr = warg_max(bnum / bden, br, bdel, 0.0);
+            const ArgBest1 lr = warg_max1(bnum / bden, br, bdel);
             const int r = lr.idx;
             STAMP(1)
             if (lr.key == 0.0) break;
@@ -353,8 +338,8 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             // ---- 2. BTRAN: u = e_r' E_K..E_1 (u dense in LDS), rho = u' B0^{-1}
             if (lane == (r & 63)) ut[r] = 1.0;
             h_wave_sync();
-            // etas in groups of 4: the group's entries (first 64 of each) are loaded together,
-            // so one memory round trip serves four sequential steps
+            // etas in groups of EG: the group's entries (first 64 of each) are loaded together,
+            // so one memory round trip serves EG sequential steps
             for (int tg = K - 1; tg >= 0; tg -= EG) {
                 int gi[EG], gn[EG], go[EG];
                 double gv[EG];
@@ -381,13 +366,10 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 }
             }
             STAMP(2)
-            // rho = u' B0^{-1} as a row scatter over the nonzeros of u, which sit at r and at
-            // the eta pivot rows; each row is consumed once (then zeroed), in the fixed order
-            // r, etap[K-1], ..., etap[0], so the accumulation order is deterministic.
-#if TWOSD_RHO_SEG
-            // as one segmented scatter over the rows of u in that order, 64 rows per batch; a row
-            // that appears again later (pivoted more than once) contributes at its first position
-            // only, as the zeroing does in the row-by-row form
+            // rho = u' B0^{-1} as one segmented scatter over the nonzero rows of u, which sit at r
+            // and at the eta pivot rows, in the fixed order r, etap[K-1], ..., etap[0] (64 rows per
+            // batch; deterministic accumulation order).  A row that appears again later (pivoted
+            // more than once) contributes at its first position only; each row is zeroed after.
             for (int b0 = 0; b0 <= K; b0 += 64) {
                 const int jj = b0 + lane;
                 const int gp = jj <= K ? (jj == 0 ? r : (int)etap[K - jj]) : -1;
@@ -408,48 +390,11 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 if (gp >= 0) ut[gp] = 0.0;
                 h_wave_sync();
             }
-#else
-            for (int tg = K; tg >= 0; tg -= EG) {
-                int gi[EG], gn[EG], gp[EG], go[EG];
-                double gv[EG];
-#pragma unroll
-                for (int g = 0; g < EG; ++g) {
-                    const int tt = tg - g;
-                    gi[g] = 0; gv[g] = 0.0; gn[g] = 0; go[g] = 0; gp[g] = 0;
-                    if (tt >= 0) {
-                        gp[g] = (tt == K) ? r : (int)etap[tt];
-                        go[g] = brptr[gp[g]];
-                        gn[g] = brptr[gp[g] + 1] - go[g];
-                        if (lane < gn[g]) { gi[g] = P.brcol[go[g] + lane]; gv[g] = P.brval[go[g] + lane]; }
-                    }
-                }
-#pragma unroll
-                for (int g = 0; g < EG; ++g) {
-                    const int tt = tg - g;
-                    if (tt < 0) break;
-                    const double up = ut[gp[g]];
-                    if (up != 0.0) {
-#if TWOSD_LDS_ADD
-                        if (lane < gn[g]) lds_add(&rho[gi[g]], up * gv[g]);
-                        for (int e = 64 + lane; e < gn[g]; e += 64) lds_add(&rho[P.brcol[go[g] + e]], up * P.brval[go[g] + e]);
-#else
-                        if (lane < gn[g]) rho[gi[g]] = fma(up, gv[g], rho[gi[g]]);
-                        for (int e = 64 + lane; e < gn[g]; e += 64)
-                            rho[P.brcol[go[g] + e]] = fma(up, P.brval[go[g] + e], rho[P.brcol[go[g] + e]]);
-#endif
-                        nops += gn[g];
-                        h_wave_sync();
-                        if (lane == 0) ut[gp[g]] = 0.0;
-                    }
-                    h_wave_sync();
-                }
-            }
-#endif
             STAMP(3)
 
-            // ---- 3. pricing: alpha~_j = rho' a_j for every column as a scatter over the nonzeros
-            // of rho (~6 % of the rows on storm).  alpha lives in LDS over the ut/rho space (both
-            // zero here once rho is in registers).
+            // ---- 3. pricing: alpha'_j = s_j rho' a_j for every column as a scatter over the
+            // nonzeros of rho (~6 % of the rows on storm).  alpha lives in LDS over the ut/rho space
+            // (both zero here once rho is in registers).
             double rv[R];
 #pragma unroll
             for (int t = 0; t < R; ++t) rv[t] = rho[64 * t + lane];
@@ -457,10 +402,8 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
 #pragma unroll
             for (int t = 0; t < R; ++t) rho[64 * t + lane] = 0.0;
             h_wave_sync();
-#if TWOSD_PRICE_SEG
-            // Segmented: the nonzero rows of rho (ascending) are compacted into the LDS list, 64
-            // per batch, and the batch's W rows (CSR) scattered 64 entries per wave step
-            // (h_seg_scatter; a row of ~6 entries no longer occupies a whole step).
+            // the nonzero rows of rho (ascending) are compacted into the LDS list, 64 per batch, and
+            // the batch's W rows (CSR) scattered 64 entries per wave step (h_seg_scatter)
             {
                 uint64_t mk[R];
                 int tot = 0;
@@ -489,130 +432,93 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                         gr = lstv[lane];
                         p0 = P.wcp[gi];
                         len = P.wcp[gi + 1] - p0;
-                        alpha[n + gi] = gr;   // slack of row i: entry 1 in row i only
+                        // slack of row i: entry 1 in row i only, folded by its sign (G row: -1)
+                        alpha[n + gi] = P.btype[n + gi] == BT_G ? -gr : gr;
                     }
                     nops += h_seg_scatter(p0, len, gr, P.wcc, P.wcv, alpha, smark, lane) + nb;
                     h_wave_sync();   // the list is rewritten by the next batch
                 }
             }
-#else
-            // Row by row: one W row (row-ELL of width WR <= 64, padding column -1) per wave step,
-            // rows ascending, PRICE_G rows per load round trip.  A row longer than 64 keeps 63
-            // entries here; slot 63 holds column -2 - o and value n_rest: its remaining entries
-            // sit in an overflow CSR at o.
-            {
-                const int WR = P.wr_width;
-                constexpr int G = TWOSD_PRICE_G;
-#pragma unroll
-                for (int t = 0; t < R; ++t) {
-                    uint64_t msk = __ballot(rv[t] != 0.0);
-                    while (msk) {
-                        int gi[G], gc[G];
-                        double gr[G], gw[G];
-#pragma unroll
-                        for (int g = 0; g < G; ++g) {
-                            gi[g] = -1; gc[g] = -1; gr[g] = 0.0; gw[g] = 0.0;
-                            if (msk) {
-                                const int l = __builtin_ctzll(msk);
-                                msk &= msk - 1;
-                                gi[g] = 64 * t + l;
-                                gr[g] = readlane_dbl(rv[t], l);
-                                if (lane < WR) { gc[g] = P.wr_col[(size_t)gi[g] * WR + lane]; gw[g] = P.wr_val[(size_t)gi[g] * WR + lane]; }
-                            }
-                        }
-#pragma unroll
-                        for (int g = 0; g < G; ++g) {
-                            if (gi[g] < 0) break;
-                            if (gc[g] >= 0) lds_add(&alpha[gc[g]], gr[g] * gw[g]);
-                            if (__ballot(gc[g] < -1)) {   // long row (rare): the rest, columns ascending
-                                const int o = -2 - __builtin_amdgcn_readlane(gc[g], 63);
-                                const int nr = (int)readlane_dbl(gw[g], 63);
-                                for (int e = lane; e < nr; e += 64) lds_add(&alpha[P.wr_ocol[o + e]], gr[g] * P.wr_oval[o + e]);
-                            }
-                            if (lane == 0) alpha[n + gi[g]] = gr[g];   // slack of row i: entry 1 in row i only
-                            nops += WR + 1;
-                        }
-                    }
-                }
-            }
-#endif
             h_wave_sync();
             STAMP(4)
 
-            // Harris ratio test over the nonbasic columns (d in registers, alpha~ from LDS); the
-            // alpha~ of slot c + 1 is read while slot c is tested (software pipelined)
-            // pass 1: thmax = min over the eligible columns of (d_j +- tol) / |alpha_j|, compared as
-            // fractions within the lane (nu * den_best < nu_best * den), one division per lane
-            const double sg = delta > 0 ? 1.0 : -1.0;
+            // Harris ratio test over the nonbasic columns (d' in registers, alpha' from LDS), branch
+            // free per slot; the alpha' of slot c + 1 is read while slot c is tested.
+            // pass 1: thmax = min over the eligible columns of (d'_j + tol) / a'_j, compared as
+            // fractions within the lane (nu * de_best < nu_best * de), one division per lane
+            const uint64_t sgm = delta > 0 ? 0ull : (1ull << 63);   // a = sg alpha
+            const Mask cand = (Mask)~(bmask | fixedm);
             double bnu = INFINITY, bde = 1.0;
-            uint64_t nzm = 0, elm = 0;
+            Mask elm = 0;
             double apf = alpha[lane];
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 const double av = apf;
                 if (c + 1 < C) apf = alpha[64 * (c + 1) + lane];
-                const uint64_t bit = 1ull << c;
-                if (bmask & bit) continue;
-                const double a = sg * av;
-                if (a != 0.0) nzm |= bit;   // fixed columns too: their d_j (slack: -pi_i) stay current
-                if (fixedm & bit) continue;
-                const bool atlb = !(ubm & bit);
-                if (atlb ? a > HTOL_PIV : a < -HTOL_PIV) {
-                    elm |= bit;
-                    const double nu = atlb ? d[c] + HTOL_D : HTOL_D - d[c];
-                    const double de = fabs(a);
-                    if (nu * bde < bnu * de) { bnu = nu; bde = de; }
-                }
+                const double a = h_flip(av, sgm);
+                const bool el = (((cand >> c) & 1) != 0) & (a > HTOL_PIV);
+                const double nu = d[c] + HTOL_D;
+                const bool better = el & (nu * bde < bnu * a);
+                bnu = better ? nu : bnu;
+                bde = better ? a : bde;
+                elm |= (Mask)el << c;
+                // one slot at a time: unscheduled, the 28 slots' LDS reads are hoisted together and
+                // the register pressure spills d[] for the whole pivot loop
+                __builtin_amdgcn_sched_barrier(0);
             }
             const double thmax = wmin(bnu / bde);
             if (thmax == INFINITY) {
                 status = TWOSD_LP_INFEASIBLE;
                 h_wave_sync();
-                zero_alpha();
+#pragma unroll
+                for (int c = 0; c < C; ++c) alpha[64 * c + lane] = 0.0;
                 break;
             }
-            double bA = 0.0, bD = 0.0, bAs = 0.0;
+            // pass 2: among the eligible columns with d'_j <= thmax a'_j the largest a'_j (lowest
+            // column on ties)
+            double bA = 0.0, bD = 0.0;
             int bq = 0x7fffffff;
             apf = alpha[lane];
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 const double av = apf;
                 if (c + 1 < C) apf = alpha[64 * (c + 1) + lane];
-                if (!(elm & (1ull << c))) continue;
-                const double a = sg * av;
-                // d_j / a <= thmax, as a product (a != 0, its sign known)
-                if ((a > 0.0 ? d[c] <= thmax * a : d[c] >= thmax * a) && fabs(a) > bA) { bA = fabs(a); bq = 64 * c + lane; bD = d[c]; bAs = a; }
+                const double a = h_flip(av, sgm);
+                const bool ok = (((elm >> c) & 1) != 0) & (d[c] <= thmax * a) & (a > bA);
+                bA = ok ? a : bA;
+                bD = ok ? d[c] : bD;
+                bq = ok ? 64 * c + lane : bq;
+                __builtin_amdgcn_sched_barrier(0);
             }
-            const ArgBest eq = warg_max(bA, bq, bD, bAs);
+            const ArgBest1 eq = warg_max1(bA, bq, bD);
             const int q = eq.idx;
             STAMP(5)
             if (eq.key == 0.0) {
                 status = TWOSD_LP_NUMERIC;
                 h_wave_sync();
-                zero_alpha();
+#pragma unroll
+                for (int c = 0; c < C; ++c) alpha[64 * c + lane] = 0.0;
                 break;
             }
-            const double thetaD = eq.p0 / eq.p1;
-            // d_j -= thetaD * alpha~_j for every nonbasic column with alpha_j != 0
+            const double thetaD = eq.p0 / eq.key;   // d'_q / a'_q = d_q / a_q
+            // d'_j -= thetaD a'_j over every slot, alpha back to zero (ut / rho all zero after)
             apf = alpha[lane];
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 const double av = apf;
                 if (c + 1 < C) apf = alpha[64 * (c + 1) + lane];
-                if (nzm & (1ull << c)) d[c] = fma(-thetaD, sg * av, d[c]);
+                alpha[64 * c + lane] = 0.0;
+                d[c] = fma(-thetaD, h_flip(av, sgm), d[c]);
+                __builtin_amdgcn_sched_barrier(0);
             }
-            h_wave_sync();
-            zero_alpha();   // back to all-zero ut / rho
             h_wave_sync();
             STAMP(6)
 
             // ---- 4. FTRAN: ut = E_K..E_1 B0^{-1} a_q (ut is all zeros here): the CSC columns of
-            // B0^{-1} under the nonzeros of a_q, lanes over a column's entries (distinct rows)
+            // B0^{-1} under the nonzeros of a_q as one segmented scatter (lane j: nonzero np0 + j),
+            // 64 nonzeros per batch, then the etas
             {
                 const int np0 = q >= n ? 0 : P.colptr[q], np1 = q >= n ? 1 : P.colptr[q + 1];
-#if TWOSD_FTRAN_SEG
-                // the B0^{-1} columns under the nonzeros of a_q as one segmented scatter (lane j:
-                // nonzero np0 + j), 64 nonzeros per batch
                 for (int pw0 = np0; pw0 < np1; pw0 += 64) {
                     const int pw = pw0 + lane;
                     int p0 = 0, len = 0;
@@ -625,56 +531,6 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                     }
                     nops += h_seg_scatter(p0, len, fa, P.bci, P.bcv, ut, smark, lane);
                 }
-#elif TWOSD_FTRAN_G > 1
-                // the B0^{-1} columns of FG nonzeros of a_q per memory round trip (pointers and
-                // first 64 entries loaded together), applied in pw order as below
-                constexpr int FG = TWOSD_FTRAN_G;
-                for (int pw0 = np0; pw0 < np1; pw0 += FG) {
-                    int fo[FG], fn[FG], fi[FG];
-                    double fa[FG], fv[FG];
-#pragma unroll
-                    for (int g = 0; g < FG; ++g) {
-                        const int pw = pw0 + g;
-                        fo[g] = 0; fn[g] = 0; fi[g] = 0; fa[g] = 0.0; fv[g] = 0.0;
-                        if (pw < np1) {
-                            const int cc = q >= n ? q - n : P.rowidx[pw];
-                            fa[g] = q >= n ? 1.0 : P.val[pw];
-                            fo[g] = bcp[cc];
-                            fn[g] = bcp[cc + 1] - fo[g];
-                            if (lane < fn[g]) { fi[g] = P.bci[fo[g] + lane]; fv[g] = P.bcv[fo[g] + lane]; }
-                        }
-                    }
-#pragma unroll
-                    for (int g = 0; g < FG; ++g) {
-                        if (pw0 + g >= np1) break;
-#if TWOSD_LDS_ADD
-                        if (lane < fn[g]) lds_add(&ut[fi[g]], fa[g] * fv[g]);
-                        for (int e = 64 + lane; e < fn[g]; e += 64) lds_add(&ut[P.bci[fo[g] + e]], fa[g] * P.bcv[fo[g] + e]);
-                        nops += fn[g];
-#else
-                        if (lane < fn[g]) ut[fi[g]] = fma(fa[g], fv[g], ut[fi[g]]);
-                        for (int e = 64 + lane; e < fn[g]; e += 64) {
-                            const int i = P.bci[fo[g] + e];
-                            ut[i] = fma(fa[g], P.bcv[fo[g] + e], ut[i]);
-                        }
-                        nops += fn[g];
-                        h_wave_sync();
-#endif
-                    }
-                }
-#else
-                for (int pw = np0; pw < np1; ++pw) {
-                    const int cc = q >= n ? q - n : P.rowidx[pw];
-                    const double aw = q >= n ? 1.0 : P.val[pw];
-                    const int e0 = bcp[cc], e1 = bcp[cc + 1];
-                    for (int e = e0 + lane; e < e1; e += 64) {
-                        const int i = P.bci[e];
-                        ut[i] = fma(aw, P.bcv[e], ut[i]);
-                    }
-                    nops += e1 - e0;
-                    h_wave_sync();
-                }
-#endif
             }
             h_wave_sync();
             for (int tg = 0; tg < K; tg += EG) {
@@ -697,7 +553,6 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                     const int p = etap[tt];
                     const double vp = ut[p];
                     if (vp != 0.0) {
-#if TWOSD_LDS_ADD
                         // the pivot row p is replaced, the others accumulate (distinct rows)
                         if (lane < gn[g]) {
                             if (gi[g] == p) ut[p] = gv[g] * vp;
@@ -709,14 +564,6 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                             if (i == p) ut[p] = ev * vp;
                             else lds_add(&ut[i], ev * vp);
                         }
-#else
-                        if (lane < gn[g]) ut[gi[g]] = (gi[g] == p) ? gv[g] * vp : fma(gv[g], vp, ut[gi[g]]);
-                        for (int e = 64 + lane; e < gn[g]; e += 64) {
-                            const int i = eidx[go[g] + e];
-                            const double ev = evals[go[g] + e];
-                            ut[i] = (i == p) ? ev * vp : fma(ev, vp, ut[i]);
-                        }
-#endif
                         nops += gn[g];
                     }
                     h_wave_sync();
@@ -770,30 +617,30 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 etaoff[K + 1] = eoff;
             }
             ++K;
-            const int leaving = h_get_row_i<R>(hb, r) >> 2;
-            // reduced cost of the leaving variable: -sg * thetaD; of q: 0
-            if (lane == (leaving & 63)) {
-                const int ls = leaving >> 6;
-                bmask &= ~(1ull << ls);
+            const int lh = h_get_row_i<R>(hb, r);
+            const int leaving = lh >> 2;
+            // reduced cost of the leaving variable: -sg thetaD, folded by its sign (a G-row
+            // slack leaves to its upper bound 0: s = -1); of q: 0
+            {
+                const int ls = leaving >> 6, qs = q >> 6;
+                const double dlv = (delta > 0) == ((lh & 3) == BT_G) ? thetaD : -thetaD;
+                const bool lme = lane == (leaving & 63), qme = lane == (q & 63);
 #pragma unroll
-                for (int c = 0; c < C; ++c)
-                    if (c == ls) d[c] = -sg * thetaD;
-            }
-            if (lane == (q & 63)) {
-                const int qs = q >> 6;
-                bmask |= 1ull << qs;
+                for (int c = 0; c < C; ++c) {
+                    if (lme && c == ls) d[c] = dlv;
+                    if (qme && c == qs) d[c] = 0.0;
+                }
+                if (lme) bmask &= ~(1ull << ls);
+                if (qme) bmask |= 1ull << qs;
+                if (lane == (r & 63)) {
+                    const int rs = r >> 6;
+                    const int nh = q * 4 + (int)P.btype[q];
 #pragma unroll
-                for (int c = 0; c < C; ++c)
-                    if (c == qs) d[c] = 0.0;
-            }
-            if (lane == (r & 63)) {
-                const int rs = r >> 6;
-                const int nh = q * 4 + (int)P.btype[q];
-#pragma unroll
-                for (int t = 0; t < R; ++t) {
-                    int v = (t == rs) ? nh : hb[t];
-                    asm volatile("" : "+v"(v));   // per-slot select kept: no dynamic store into hb
-                    hb[t] = v;
+                    for (int t = 0; t < R; ++t) {
+                        int v = (t == rs) ? nh : hb[t];
+                        asm volatile("" : "+v"(v));   // per-slot select kept: no dynamic store into hb
+                        hb[t] = v;
+                    }
                 }
             }
             ++it;
@@ -816,21 +663,24 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             objv = wsum(ob);
             if (P.vkey) {
                 // key of the dual: pi_i = -d_{n+i} is the reduced cost of row i's slack, kept
-                // current in registers by every pivot (fixed E-row slacks included).  Components
-                // at or below key_zero (1 + max) are snapped to zero -- the threshold of the exact
-                // recovery below (HPI_ZERO), so a component the recovered pi keeps also separates
-                // the keys -- and the rest rounded to 24 significant bits; the key is the
-                // order-independent sum of mix64(row, bits).
+                // current in registers by every pivot (fixed E-row slacks included; unfolded here,
+                // basic slacks 0).  Components at or below key_zero (1 + max) are snapped to zero --
+                // the threshold of the exact recovery (HPI_ZERO), so a component the recovered pi
+                // keeps also separates the keys -- and the rest rounded to 24 significant bits; the
+                // key is the order-independent sum of mix64(row, bits).
                 // Scenarios with equal keys have duals equal to ~2^-23 relative -- the same vertex
                 // up to rounding noise, so their exactly recovered pi push as equal vectors
                 // (16-bit rule, dual_set.jl:24-53).  A vertex split over two keys only costs one
                 // more re-solved representative; the push dedup still merges it.
+                // d_j of row i's slack (nonbasic; basic: 0), unfolded
+                auto dk = [&](int c) -> double {
+                    const int j = 64 * c + lane;
+                    const bool slack = (j >= n) & (j < ncol) & (((bmask >> c) & 1) == 0);
+                    return slack ? h_flip(d[c], ((ubm >> c) & 1) << 63) : 0.0;
+                };
                 double pm = 0.0;
 #pragma unroll
-                for (int c = 0; c < C; ++c) {
-                    const int j = 64 * c + lane;
-                    if (j >= n && j < ncol) pm = fmax(pm, fabs(d[c]));
-                }
+                for (int c = 0; c < C; ++c) pm = fmax(pm, fabs(dk(c)));
                 pm = wmax(pm);
                 const double zt = P.key_zero * (1.0 + pm);
                 unsigned long long h = 0;
@@ -838,7 +688,8 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 for (int c = 0; c < C; ++c) {
                     const int j = 64 * c + lane;
                     if (j >= n && j < ncol) {
-                        const double v = fabs(d[c]) <= zt ? 0.0 : d[c];
+                        const double dc = dk(c);
+                        const double v = fabs(dc) <= zt ? 0.0 : dc;
                         // sign, exponent and 23 mantissa bits (35 bits) next to the row (< 2^24)
                         const unsigned long long b = ((unsigned long long)__double_as_longlong(v) + (1ull << 28)) >> 29;
                         h += mix64(((unsigned long long)(j - n) << 35) | b);
@@ -849,7 +700,8 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 if (lane == 0) P.vkey[s] = h;
             }
         }
-        if (status == TWOSD_LP_OPTIMAL && (P.pi || P.y || !P.vkey)) {
+        if constexpr (FULL) {
+        if (status == TWOSD_LP_OPTIMAL && (P.pi || P.y)) {
 #pragma unroll
             for (int t = 0; t < R; ++t) {
                 const int j = hb[t] >> 2;
@@ -947,6 +799,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 P.eo_pb[erow] = pb;
             }
         }
+        }   // FULL
         if (lane == 0) {
             P.obj[s] = objv;
             P.status[s] = status;
@@ -1274,21 +1127,26 @@ int hyper_cols_per_lane(int ncols) {
 
 template <int R, int C>
 static hipError_t hl(const HyperParams &p, int nb, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((lp_hyper_kernel<R, C>), dim3(nb), dim3(256), lds, s, p);
+    // the lean kernel when the launch asks for none of the recovery / refresh outputs
+    if (p.pi || p.y || p.head_out || p.bkey || p.eo_K)
+        hipLaunchKernelGGL((lp_hyper_kernel<R, C, true>), dim3(nb), dim3(256), lds, s, p);
+    else
+        hipLaunchKernelGGL((lp_hyper_kernel<R, C, false>), dim3(nb), dim3(256), lds, s, p);
     return hipGetLastError();
 }
 template <int R, int C>
 static int ho(size_t lds) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lp_hyper_kernel<R, C>, 256, lds) != hipSuccess) return 1;
+    int nb = 0, nb2 = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lp_hyper_kernel<R, C, true>, 256, lds) != hipSuccess) return 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb2, lp_hyper_kernel<R, C, false>, 256, lds) != hipSuccess) return 1;
+    nb = std::min(nb, nb2);   // one grid size for both (the eta arena is sized by it)
     return nb > 0 ? nb : 1;
 }
 
-#ifdef HYP_DEV_STORM_ONLY   // development builds: the storm instance (R = 9, C = 32) only
+#ifdef HYP_DEV_STORM_ONLY   // development builds: the storm instance (R = 9, C = 28) only
 #define HYPER_C_SWITCH(R, FN, ...)                  \
     switch (C) {                                    \
         case 28: if (R == 9) return FN<9, 28>(__VA_ARGS__); \
-        case 32: if (R == 9) return FN<9, 32>(__VA_ARGS__); \
     }
 #else
 #define HYPER_C_SWITCH(R, FN, ...)                  \
@@ -1315,8 +1173,8 @@ hipError_t launch_hyper(int R, int C, const HyperParams &p, int nblocks, size_t 
     return hipErrorInvalidValue;
 }
 
-int hyper_max_blocks_per_cu(int R, int C, int ncol, int kmax, int k) {
-    const size_t lds = hyper_lds_bytes(R, ncol, kmax, k);
+int hyper_max_blocks_per_cu(int R, int C, int kmax, int k) {
+    const size_t lds = hyper_lds_bytes(R, C, kmax, k);
     switch (R) {
         case 1: HYPER_C_SWITCH(1, ho, lds); break;
         case 2: HYPER_C_SWITCH(2, ho, lds); break;

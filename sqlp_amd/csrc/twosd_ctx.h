@@ -39,6 +39,7 @@ struct twosd_ctx {
     int kmax_override = 0;
     int train_kcap = 0;           // pivot cap of the refresh training solves (> 0; 0: auto; < 0: none)
     double piv_mean_ref = 0.0;    // mean pivots of the last large batch solve (the auto cap's scale)
+    int64_t piv_ref_sum = 0, piv_ref_n = 0;   // that batch's pivot sum and size (ranks agree on one cap)
     int last_train_opt = 0;       // optimal training scenarios of the last refresh
     double t_us[5] = {0, 0, 0, 0, 0};   // LP kernel, dedup, cut partial, cut finalize, pool select
     // template
@@ -130,6 +131,9 @@ struct twosd_ctx {
     int last_lp_N = 0, last_lp_blocks = 0;
     int64_t last_pivots_sum = 0;
     int last_pivots_max = 0;
+    // weighted objective sum of the last batch (sum_s w_s obj_s, fixed-order reduction) and its weight
+    double last_obj_wsum = 0.0, last_obj_w = 0.0;
+    double *d_objpart = nullptr;
     // scenario distributions (on-device sampler)
     bool has_dist = false;
     int *d_dist_kind = nullptr, *d_dist_off = nullptr;
@@ -169,6 +173,7 @@ struct twosd_ctx {
     std::vector<int> rt_counts, rt_reps;
     std::vector<double> rt_lo, rt_hi;     // training box of this rank's slice
     int rt_epi = -1, rt_first = -1, rt_count = -1, rt_n = -1, rt_nown = -1;
+    bool rt_trained = false;              // a twosd_refresh_train* ran since the last assemble
     long long rt_nz0 = 0;                 // intermediate entries of the primary (local source 0)
     int rt_nsrc_local = 0;
     char *d_rt_pack = nullptr;

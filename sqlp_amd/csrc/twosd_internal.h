@@ -160,11 +160,11 @@ int pool_refine_split(int N, int ncand);
 // stable sort of scenarios [0, N) by pool pick -> order (pool_sort.hip); tmp == nullptr: size query
 hipError_t sort_by_pool(const int *pick, int *order, int N, int npool, void *tmp, size_t *tmp_bytes, hipStream_t s);
 hipError_t launch_pool_select(const PoolSelParams &p, hipStream_t s);
-size_t hyper_lds_bytes(int R, int ncol, int kmax, int k);   // ncol = n + m
+size_t hyper_lds_bytes(int R, int C, int kmax, int k);   // C = column slots (hyper_cols_per_lane(n + m))
 int hyper_rows_per_lane(int m);
 int hyper_cols_per_lane(int ncols);
 hipError_t launch_hyper(int R, int C, const HyperParams &p, int nblocks, size_t lds, hipStream_t s);
-int hyper_max_blocks_per_cu(int R, int C, int ncol, int kmax, int k);
+int hyper_max_blocks_per_cu(int R, int C, int kmax, int k);
 
 
 // ---- on-device scenario sampler (sampler.hip)

@@ -94,4 +94,34 @@ __device__ __forceinline__ ArgBest warg_max(double key, int idx, double p0, doub
     return b;
 }
 
+// the same with one payload value
+struct ArgBest1 {
+    double key;
+    int idx;
+    double p0;
+};
+template <int CTRL>
+__device__ __forceinline__ void arg_step1(double &key, int &idx, double &p0) {
+    const double k2 = dpp_d<CTRL>(key);
+    const int i2 = dpp_i<CTRL>(idx);
+    const double a2 = dpp_d<CTRL>(p0);
+    if (k2 > key || (k2 == key && i2 < idx)) { key = k2; idx = i2; p0 = a2; }
+}
+__device__ __forceinline__ ArgBest1 warg_max1(double key, int idx, double p0) {
+    arg_step1<kDppXor1>(key, idx, p0);
+    arg_step1<kDppXor2>(key, idx, p0);
+    arg_step1<kDppHalfMirror>(key, idx, p0);
+    arg_step1<kDppMirror>(key, idx, p0);
+    ArgBest1 b{readlane_dbl(key, 0), __builtin_amdgcn_readlane(idx, 0), readlane_dbl(p0, 0)};
+#pragma unroll
+    for (int l = 16; l < 64; l += 16) {
+        const double k2 = readlane_dbl(key, l);
+        const int i2 = __builtin_amdgcn_readlane(idx, l);
+        if (k2 > b.key || (k2 == b.key && i2 < b.idx)) {
+            b.key = k2; b.idx = i2; b.p0 = readlane_dbl(p0, l);
+        }
+    }
+    return b;
+}
+
 }  // namespace twosd

@@ -96,39 +96,48 @@ class CutExchange:
         self.hist = None
         self.sums = None
 
-    def _buffers(self):
+    def _buffers(self, n_extra=0):
         n_u64, n_f64 = self.ctx.cut_partial_len()
         if self.hist is None or self.hist.numel() < n_u64:
             self.hist = torch.zeros(max(n_u64, 1024), dtype=torch.int64, device=self.device)
             self._sync()
-        if self.sums is None or self.sums.numel() < n_f64:
-            self.sums = torch.zeros(max(n_f64, 256), dtype=torch.float64, device=self.device)
+        if self.sums is None or self.sums.numel() < n_f64 + n_extra:
+            self.sums = torch.zeros(max(n_f64 + n_extra, 256), dtype=torch.float64, device=self.device)
             self._sync()     # torch's fill must land before the library's stream touches the buffer
-        return self.hist[:n_u64], self.sums[:n_f64]
+        return self.hist[:n_u64], self.sums[:n_f64 + n_extra], n_f64
 
     def _sync(self):
         if self.hist is not None and self.hist.is_cuda:
             torch.cuda.synchronize(self.device)
 
-    def build_cut(self, epi, x, total_weight, tie_rel, verify=True):
+    def build_cut(self, epi, x, total_weight, tie_rel, verify=True, extra=None):
         """build_sasa_cut over the scenarios of every rank: local partial on this GPU (the
         library zero-fills and writes the buffers on its stream, synchronously), all-reduce,
-        identical finalize on every rank.  Returns (alpha, beta)."""
+        identical finalize on every rank.  Returns (alpha, beta), or (alpha, beta, sums of
+        `extra`) when extra (a few fp64 per rank, e.g. the incumbent objective's sum_s w_s obj_s
+        and sum_s w_s) is given: those travel in the same all-reduce as the cut's fp64 sums."""
         if verify:
             check_vertex_sets_agree(self.ctx)
-        hist, sums = self._buffers()
+        n_extra = 0 if extra is None else len(extra)
+        hist, sums, n_f64 = self._buffers(n_extra)
         self.ctx.cut_partial(epi, x, tie_rel, total_weight, hist.data_ptr(), sums.data_ptr())
+        if n_extra:
+            sums[n_f64:] = torch.tensor(np.asarray(extra, dtype=np.float64), device=sums.device)
         allreduce_cut_partials(hist, sums)
         self._sync()         # the collective runs on torch / RCCL streams, finalize on the library's
-        return self.ctx.cut_finalize(x, hist.data_ptr(), sums.data_ptr())
+        cut = self.ctx.cut_finalize(x, hist.data_ptr(), sums.data_ptr())
+        if extra is None:
+            return cut
+        return cut[0], cut[1], sums[n_f64:].cpu().numpy()
 
 
-def build_cut_sharded(ctx, epi, x, total_weight, tie_rel, device, verify=True):
-    """build_sasa_cut over the scenarios of every rank (one CutExchange per context)."""
+def build_cut_sharded(ctx, epi, x, total_weight, tie_rel, device, verify=True, extra=None):
+    """build_sasa_cut over the scenarios of every rank (one CutExchange per context); `extra`:
+    see CutExchange.build_cut."""
     ex = getattr(ctx, "_cut_exchange", None)
     if ex is None:
         ex = ctx._cut_exchange = CutExchange(ctx, device)
-    return ex.build_cut(epi, x, total_weight, tie_rel, verify=verify)
+    return ex.build_cut(epi, x, total_weight, tie_rel, verify=verify, extra=extra)
 
 
 def check_vertex_sets_agree(ctx):
@@ -225,74 +234,181 @@ def _allgather_1d(arr: np.ndarray, device=None):
     return np.concatenate([b[:k].cpu().numpy() for b, k in zip(bufs, ns)]), ns
 
 
+def _gather_fixed(arr: np.ndarray, device=None) -> np.ndarray:
+    """One all-gather of an equal-length int64 row per rank -> (G, len) host array.  Over RCCL a
+    single all_gather_into_tensor of a device buffer, one host synchronisation."""
+    G = dist.get_world_size()
+    t = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int64))
+    if dist.get_backend() == "nccl":
+        t = t.to(device)
+        out = torch.empty(G * t.numel(), dtype=torch.int64, device=device)
+        dist.all_gather_into_tensor(out, t)
+        return out.cpu().numpy().reshape(G, -1)
+    parts = [torch.empty_like(t) for _ in range(G)]
+    dist.all_gather(parts, t)
+    return torch.stack(parts).numpy()
+
+
+def _allreduce_i64(arr, device=None, op=None) -> np.ndarray:
+    t = torch.tensor(np.asarray(arr, dtype=np.int64))
+    if dist.get_backend() == "nccl":
+        t = t.to(device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM if op is None else op)
+    return t.cpu().numpy()
+
+
+def exchange_training_bases(keys, counts, reps, lo, hi, ns, device=None):
+    """Exchange 2 of refresh_sharded: every rank's distinct training bases (u64 keys, counts,
+    first scenarios; ns[r] of them on rank r, known from the header exchange) and delta box in
+    ONE all-gather of an int64 row padded to the longest rank.  Returns the rank-order
+    concatenations and the union box."""
+    G = dist.get_world_size()
+    k = np.asarray(lo).size
+    U = max(max(ns), 1)
+    n = len(keys)
+    row = np.zeros(3 * U + 2 * k, dtype=np.int64)
+    row[:n] = np.asarray(keys, dtype=np.uint64).view(np.int64)
+    row[U:U + n] = counts
+    row[2 * U:2 * U + n] = reps
+    row[3 * U:3 * U + k] = np.ascontiguousarray(lo, dtype=np.float64).view(np.int64)
+    row[3 * U + k:] = np.ascontiguousarray(hi, dtype=np.float64).view(np.int64)
+    g = _gather_fixed(row, device)
+    all_keys = np.concatenate([g[r, :ns[r]] for r in range(G)]).view(np.uint64)
+    all_counts = np.concatenate([g[r, U:U + ns[r]] for r in range(G)])
+    all_reps = np.concatenate([g[r, 2 * U:2 * U + ns[r]] for r in range(G)])
+    boxes = np.ascontiguousarray(g[:, 3 * U:]).view(np.float64).reshape(G, 2, k)
+    return all_keys, all_counts, all_reps, boxes[:, 0].min(axis=0), boxes[:, 1].max(axis=0)
+
+
+def refresh_training_cap(ctx, device=None) -> int:
+    """The training pivot cap every rank uses (twosd_refresh_train_ex): the context's explicit
+    setting, else twosd_pool_refresh's auto rule -- 3 x the mean pivots of the last batch of
+    >= 4096 scenarios, at least 32 -- over every rank's last batch (one all-reduce of two int64),
+    so all ranks train under the same cap whatever their own batches were.  0: none."""
+    import math
+    import os
+    env = os.environ.get("TWOSD_TRAIN_KCAP")
+    setting = int(env) if env else getattr(ctx, "refresh_kcap", 0)
+    if setting > 0:
+        return setting
+    if setting < 0:
+        return 0
+    ps, pn = ctx.refresh_cap_stats()
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        ps, pn = (int(v) for v in _allreduce_i64([ps, pn], device))
+    return max(32, math.ceil(3.0 * ps / pn)) if pn > 0 else 0
+
+
 def refresh_sharded(ctx, train_epi, x, first, count, max_pool, level1=0, ncand=0, device=None):
     """twosd_pool_refresh of the training scenarios of every rank (this rank: [first,
     first + count) of train_epi, the ranks' slices contiguous in rank order) -- the same pool on
     every rank, equal to one rank refreshing from all of them:
-      1. each rank solves its slice (twosd_refresh_train);
-      2. exchange 1: all-gather of the distinct bases (key, count, first scenario) and of the
-         delta boxes; select_refresh_bases on every rank;
+      0. one training pivot cap for all ranks (refresh_training_cap);
+      1. each rank solves its slice under it (twosd_refresh_train_ex); exchange 1: a fixed header
+         per rank (distinct bases, optimal training scenarios, slice size).  When fewer than half
+         of ALL training scenarios ended optimal, every rank solves again uncapped (the
+         single-rank rule, decided once from the global count);
+      2. exchange 2: one all-gather of (keys, counts, first scenarios, delta box) padded to the
+         longest rank; select_refresh_bases on every rank;
       3. each rank composes the picks it owns (twosd_refresh_build_local);
-      4. exchange 2: all-gather of the packs (one all_gather_into_tensor of device buffers,
-         padded to the largest pack); every rank assembles the pool (twosd_refresh_assemble);
-      5. the two-level candidate lists from every rank's picks (exchange 3: the picks).
+      4. exchange 3: the pack size (max) and the packs (one all_gather_into_tensor of device
+         buffers); every rank assembles the pool (twosd_refresh_assemble; no pick on any rank:
+         the current pool stays);
+      5. the two-level candidate lists from every rank's picks (exchange 4: one fixed all-gather).
+    Exchanges 1-4 are 5-6 collectives in all, each followed by one host synchronisation.
+    A template the device build does not fit (TWOSD_E_UNSUPPORTED) or a primary basis failing
+    the device checks (TWOSD_E_STATE) -- both the same on every rank -- falls back to a per-rank
+    twosd_pool_refresh of the rank's own slice (pools then differ between ranks; only pivots
+    depend on the pool).
     Returns (pool size, phase milliseconds)."""
     import time
+    from ._lib import TwoSDError
     rank, G = world()
     t = [time.perf_counter()]
-    keys, counts, reps, lo, hi = ctx.refresh_train(train_epi, x, first, count)
+    cap = refresh_training_cap(ctx, device)
+    keys, counts, reps, lo, hi, nopt = ctx.refresh_train_ex(train_epi, x, first, count, cap)
     t.append(time.perf_counter())
+    k = lo.size
     if G == 1:
+        if cap > 0 and 2 * nopt < count:
+            keys, counts, reps, lo, hi, nopt = ctx.refresh_train_ex(train_epi, x, first, count, 0)
         all_keys, all_counts, all_reps, ns = keys, counts, reps, [len(keys)]
         box_lo, box_hi = lo, hi
+        counts_r = [count]
     else:
-        all_keys, ns = _allgather_1d(keys.view(np.int64), device)
-        all_keys = all_keys.view(np.uint64)
-        all_counts, _ = _allgather_1d(counts.astype(np.int64), device)
-        all_reps, _ = _allgather_1d(reps.astype(np.int64), device)
-        boxes, _ = _allgather_1d(np.concatenate([lo, hi]), device)
-        boxes = boxes.reshape(G, 2, -1)
-        box_lo, box_hi = boxes[:, 0].min(axis=0), boxes[:, 1].max(axis=0)
+        hdr = _gather_fixed([len(keys), nopt, count], device)
+        if cap > 0 and 2 * int(hdr[:, 1].sum()) < int(hdr[:, 2].sum()):
+            keys, counts, reps, lo, hi, nopt = ctx.refresh_train_ex(train_epi, x, first, count, 0)
+            hdr = _gather_fixed([len(keys), nopt, count], device)
+        ns = [int(v) for v in hdr[:, 0]]
+        counts_r = [int(v) for v in hdr[:, 2]]
+        all_keys, all_counts, all_reps, box_lo, box_hi = exchange_training_bases(keys, counts, reps, lo, hi, ns, device)
     rank_of = np.repeat(np.arange(G), ns)
     owner, orep = select_refresh_bases(all_keys, all_counts, all_reps, rank_of, max_pool)
     mine = orep[owner == rank]
     pos = pack_positions(owner, G)
     t.append(time.perf_counter())
-    nbytes = ctx.refresh_build_local(mine)
+    try:
+        nbytes = ctx.refresh_build_local(mine)
+    except TwoSDError as e:
+        if e.code != -5:
+            raise
+        return _refresh_local_fallback(ctx, train_epi, x, first, count, max_pool, level1, ncand, t)
     t.append(time.perf_counter())
-    if G == 1:
-        buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
-        torch.cuda.synchronize(device)
-        ctx.refresh_pack(buf.data_ptr())
-        size = ctx.refresh_assemble(1, buf.data_ptr(), nbytes, pos, box_lo, box_hi)
-    else:
-        mx = torch.tensor([nbytes], dtype=torch.int64, device=device if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        stride = (int(mx.item()) + 255) // 256 * 256
-        buf = torch.empty(stride, dtype=torch.uint8, device=device)
-        torch.cuda.synchronize(device)
-        ctx.refresh_pack(buf.data_ptr())
-        if dist.get_backend() == "nccl":
-            out = torch.empty(G * stride, dtype=torch.uint8, device=device)
-            dist.all_gather_into_tensor(out, buf)
+    try:
+        if G == 1:
+            buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
             torch.cuda.synchronize(device)
-        else:   # gloo (tests, rehearsal): through host memory
-            parts = [torch.empty(stride, dtype=torch.uint8) for _ in range(G)]
-            dist.all_gather(parts, buf.cpu())
-            out = torch.cat(parts).to(device)
+            ctx.refresh_pack(buf.data_ptr())
+            size = ctx.refresh_assemble(1, buf.data_ptr(), nbytes, pos, box_lo, box_hi)
+        else:
+            mx = int(_allreduce_i64([nbytes], device, dist.ReduceOp.MAX)[0])
+            stride = (mx + 255) // 256 * 256
+            buf = torch.empty(stride, dtype=torch.uint8, device=device)
             torch.cuda.synchronize(device)
-        size = ctx.refresh_assemble(G, out.data_ptr(), stride, pos, box_lo, box_hi)
+            ctx.refresh_pack(buf.data_ptr())
+            if dist.get_backend() == "nccl":
+                out = torch.empty(G * stride, dtype=torch.uint8, device=device)
+                dist.all_gather_into_tensor(out, buf)
+                torch.cuda.synchronize(device)
+            else:   # gloo (tests, rehearsal): through host memory
+                parts = [torch.empty(stride, dtype=torch.uint8) for _ in range(G)]
+                dist.all_gather(parts, buf.cpu())
+                out = torch.cat(parts).to(device)
+                torch.cuda.synchronize(device)
+            size = ctx.refresh_assemble(G, out.data_ptr(), stride, pos, box_lo, box_hi)
+    except TwoSDError as e:
+        if e.code != -3 or "primary basis failed" not in str(e):
+            raise
+        return _refresh_local_fallback(ctx, train_epi, x, first, count, max_pool, level1, ncand, t)
     t.append(time.perf_counter())
     if level1 > 0 and ncand > 0 and size > level1:
         p1, pf = ctx.pool_candidate_picks(train_epi, x, first, count, level1)
         if G > 1:
-            p1, _ = _allgather_1d(p1.astype(np.int64), device)
-            pf, _ = _allgather_1d(pf.astype(np.int64), device)
+            M = max(counts_r)
+            row = np.zeros(2 * M, dtype=np.int64)
+            row[:count] = p1
+            row[M:M + count] = pf
+            g = _gather_fixed(row, device)
+            p1 = np.concatenate([g[r, :counts_r[r]] for r in range(G)])
+            pf = np.concatenate([g[r, M:M + counts_r[r]] for r in range(G)])
         ctx.pool_set_candidates(level1, ncand, p1, pf)
     t.append(time.perf_counter())
     ms = dict(zip(("train", "select", "build", "exchange_assemble", "candidates"),
                   (1e3 * (b - a) for a, b in zip(t[:-1], t[1:]))))
+    ms["kcap"] = cap
     return size, ms
+
+
+def _refresh_local_fallback(ctx, train_epi, x, first, count, max_pool, level1, ncand, t):
+    """The device pool build does not fit (the same on every rank): each rank refreshes alone
+    from its own slice (twosd_pool_refresh composes on the host then)."""
+    import time
+    size = ctx.pool_refresh(train_epi, x, first, count, max_pool)
+    if level1 > 0 and ncand > 0 and size > level1:
+        ctx.pool_build_candidates(train_epi, x, first, count, level1, ncand)
+    t.append(time.perf_counter())
+    return size, {"local_fallback": 1e3 * (t[-1] - t[0])}
 
 
 def finalize_from_partials(hist: np.ndarray, sums: np.ndarray, V: np.ndarray, r: np.ndarray, T: np.ndarray,

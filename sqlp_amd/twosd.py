@@ -180,6 +180,38 @@ class SDContext:
         check(self.lib.twosd_refresh_train_bases(self.h, ptr(keys), ptr(counts), ptr(reps)))
         return keys, counts, reps, lo[:self.k], hi[:self.k]
 
+    def refresh_train_ex(self, epi, x, first, count, kcap):
+        """Training solves of this rank's slice under the pivot cap kcap (> 0; <= 0 none), one
+        launch, no retry (twosd_refresh_train_ex); returns (keys u64, counts, first scenarios,
+        box lo, box hi, optimal training scenarios)."""
+        U = C.c_int()
+        nopt = C.c_int()
+        lo = np.zeros(max(self.k, 1))
+        hi = np.zeros(max(self.k, 1))
+        check(self.lib.twosd_refresh_train_ex(self.h, epi.index, ptr(_f64(x)), int(first), int(count), int(kcap),
+                                              C.byref(U), C.byref(nopt), ptr(lo), ptr(hi)))
+        keys = np.zeros(U.value, dtype=np.uint64)
+        counts = np.zeros(U.value, dtype=np.int32)
+        reps = np.zeros(U.value, dtype=np.int32)
+        check(self.lib.twosd_refresh_train_bases(self.h, ptr(keys), ptr(counts), ptr(reps)))
+        return keys, counts, reps, lo[:self.k], hi[:self.k], nopt.value
+
+    def refresh_cap_stats(self):
+        """(pivot sum, scenarios) of the last LP batch of >= 4096 scenarios: the scale of the
+        training pivot cap (twosd_refresh_cap_stats)."""
+        s = C.c_int64()
+        n = C.c_int64()
+        check(self.lib.twosd_refresh_cap_stats(self.h, C.byref(s), C.byref(n)))
+        return s.value, n.value
+
+    def last_objective(self):
+        """(sum_s w_s obj_s, sum_s w_s) of the last solve_batch / solve_push / solve_values batch
+        (twosd_last_objective): the incumbent objective at x is their quotient."""
+        a = C.c_double()
+        b = C.c_double()
+        check(self.lib.twosd_last_objective(self.h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
     def refresh_build_local(self, reps) -> int:
         """Compose the bases this rank owns (first scenarios `reps`, selection order); returns the
         pack size in bytes."""
@@ -211,8 +243,10 @@ class SDContext:
         check(self.lib.twosd_pool_set_candidates(self.h, int(level1), int(ncand), len(p1), ptr(p1), ptr(pf)))
 
     def set_refresh_kcap(self, kcap: int):
-        """Pivot cap of the refresh's training solves (0: none below kmax)."""
+        """Pivot cap of the refresh's training solves: > 0 explicit, 0 auto (3 x the mean pivots of
+        the last batch of >= 4096 scenarios, at least 32), < 0 none (the kernel's kmax)."""
         check(self.lib.twosd_set_refresh_kcap(self.h, int(kcap)))
+        self.refresh_kcap = int(kcap)
 
     def last_lp_iters(self, N):
         """(pivots, status) of the first N scenarios of the last LP launch."""

@@ -69,10 +69,13 @@ def _worker(rank, world, port, out):
         keys = _stream()
         lo, hi = sdist.shard_range(len(keys), rank, world)
         k, c, f = _slice_bases(keys[lo:hi])
-        all_k, ns = sdist._allgather_1d(k.view(np.int64))
-        all_c, _ = sdist._allgather_1d(c.astype(np.int64))
-        all_f, _ = sdist._allgather_1d(f.astype(np.int64))
-        owner, rep = sdist.select_refresh_bases(all_k.view(np.uint64), all_c, all_f, np.repeat(np.arange(world), ns), 64)
+        # refresh_sharded's exchanges 1 and 2: a fixed header per rank, then one padded row
+        hdr = sdist._gather_fixed([len(k), hi - lo, hi - lo])
+        ns = [int(v) for v in hdr[:, 0]]
+        blo, bhi = np.array([-1.0 - rank, 2.0]), np.array([3.0, 4.0 + rank])   # slice delta boxes
+        all_k, all_c, all_f, box_lo, box_hi = sdist.exchange_training_bases(k, c, f, blo, bhi, ns)
+        assert box_lo.tolist() == [-world, 2.0] and box_hi.tolist() == [3.0, 3.0 + world]
+        owner, rep = sdist.select_refresh_bases(all_k, all_c, all_f, np.repeat(np.arange(world), ns), 64)
         out[rank] = (owner.tolist(), rep.tolist(), ns)
     finally:
         dist.destroy_process_group()
@@ -93,3 +96,38 @@ def test_selection_exchange_gloo(world):
         assert (owner, rep) == (res[0][0], res[0][1])
         glob = [sdist.shard_range(T, o, world)[0] + p for o, p in zip(owner, rep)]
         assert glob == ref.tolist()
+
+
+class _CapStats:
+    """Stand-in for SDContext.refresh_cap_stats: one rank's last large batch."""
+    def __init__(self, piv, n):
+        self.stats = (piv, n)
+        self.refresh_kcap = 0
+
+    def refresh_cap_stats(self):
+        return self.stats
+
+
+def _cap_worker(rank, world, port, stats, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.pop("TWOSD_TRAIN_KCAP", None)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out[rank] = sdist.refresh_training_cap(_CapStats(*stats[rank]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("stats,cap", [([(40960, 4096), (163840, 8192)], 50),     # global mean 16.67
+                                       ([(4096, 4096), (0, 0)], 32),              # floor 32
+                                       ([(0, 0), (0, 0)], 0)])                     # no batch yet: none
+def test_training_cap_is_global(stats, cap):
+    """Every rank trains under one cap: 3 x the mean pivots of ALL ranks' last large batches (at
+    least 32), whatever each rank's own batch was (per-rank caps broke the pool's
+    rank-count independence)."""
+    port = _free_port()
+    with mp.get_context("spawn").Manager() as mgr:
+        out = mgr.dict()
+        mp.start_processes(_cap_worker, args=(2, port, stats, out), nprocs=2, join=True, start_method="spawn")
+        res = dict(out)
+    assert res[0] == res[1] == cap

@@ -220,3 +220,64 @@ def test_refresh_sharded_equals_single_rank():
         np.testing.assert_array_equal(o["picks"], picks)
         assert o["piv"] == piv
     print(f"refresh_sharded: pool {size}, phases (rank 0) {res[0]['ms']}")
+
+
+def _refresh_worker_capped(rank, world, port, x, out):
+    """As _refresh_worker, but each rank first solves a batch of >= 4096 scenarios of its own
+    size (4096 + 2048 rank), so the ranks' last-batch pivot means differ."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    os.environ.pop("TWOSD_TRAIN_KCAP", None)
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from sqlp_amd import dist as sdist
+        from sqlp_amd import twosd
+        ctx = _storm_ctx()
+        warm = twosd.sdEpigraph(ctx, 1.0, 0.0)
+        nw = 4096 + 2048 * rank
+        twosd.add_sampled_scenarios(warm, nw, 777, first_index=100000 * rank)
+        twosd.solve_batch(warm, I.x_ev("storm"), 0, nw, want_pi=False)
+        lo, hi = sdist.shard_range(R_TRAIN, rank, world)
+        tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+        twosd.add_sampled_scenarios(tr, hi - lo, 4242, first_index=lo)
+        size, ms = sdist.refresh_sharded(ctx, tr, x, 0, hi - lo, R_POOL, 128, 160, torch.device("cuda", 0))
+        heads, obj, st, picks, piv = _pool_state(ctx, x)
+        out[rank] = dict(size=size, heads=heads, obj=obj, st=st, picks=picks, piv=piv, kcap=ms["kcap"],
+                         own=ctx.refresh_cap_stats())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_refresh_sharded_capped_equals_single_rank():
+    """After batches of different sizes on the two ranks, both train under ONE cap (3 x the mean
+    pivots over both ranks' batches) and hold the pool a single rank builds under that cap."""
+    import math
+    import torch.multiprocessing as mp
+    from sqlp_amd import twosd
+    x = _refresh_x()
+    port = _free_port()
+    with mp.get_context("spawn").Manager() as mgr:
+        out = mgr.dict()
+        mp.start_processes(_refresh_worker_capped, args=(2, port, x, out), nprocs=2, join=True, start_method="spawn")
+        res = dict(out)
+    (s0, n0), (s1, n1) = res[0]["own"], res[1]["own"]
+    assert (n0, n1) == (4096, 6144)
+    cap = max(32, math.ceil(3.0 * (s0 + s1) / (n0 + n1)))
+    assert res[0]["kcap"] == res[1]["kcap"] == cap
+    ctx = _storm_ctx()
+    ctx.set_refresh_kcap(cap)
+    tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_sampled_scenarios(tr, R_TRAIN, 4242)
+    size = ctx.pool_refresh(tr, x, 0, R_TRAIN, R_POOL)
+    ctx.pool_build_candidates(tr, x, 0, R_TRAIN, 128, 160)
+    heads, obj, st, picks, piv = _pool_state(ctx, x)
+    for r in (0, 1):
+        o = res[r]
+        assert o["size"] == size
+        np.testing.assert_array_equal(o["heads"], heads)
+        np.testing.assert_array_equal(o["obj"], obj)
+        np.testing.assert_array_equal(o["picks"], picks)
+        assert o["piv"] == piv
+    print(f"capped refresh_sharded: cap {cap}, pool {size}")
