@@ -354,18 +354,20 @@ def main():
     for i in range(args.warmup):
         step(xs[(i - args.warmup) % X])
     barrier()
-    acc = {"lp": 0.0, "dd": 0.0, "cut": 0.0, "fin": 0.0, "sel": 0.0, "flops": 0.0, "piv": 0, "pmax": 0}
-    per_x = [{"piv": 0, "n": 0, "lp": 0.0, "wall": 0.0, "steps": 0, "alpha": None, "refresh": 0.0} for _ in xs]
+    acc = {"lp": 0.0, "dd": 0.0, "cut": 0.0, "fin": 0.0, "sel": 0.0, "flops": 0.0, "piv": 0, "pmax": 0, "eta": 0}
+    per_x = [{"piv": 0, "n": 0, "lp": 0.0, "wall": 0.0, "steps": 0, "alpha": None, "refresh": 0.0, "eta": 0} for _ in xs]
     cur = {"xi": 0, "piv": 0, "lp": 0.0}
 
     def record():
         tm = ctx.timings_us()
         acc["lp"] += tm[0]; acc["dd"] += tm[1]; acc["cut"] += tm[2]; acc["fin"] += tm[3]; acc["sel"] += tm[4]
         acc["flops"] += ctx.lp_flops()
+        eta = ctx.lp_eta_entries()
+        acc["eta"] += eta
         ps, pm = ctx.lp_stats()
         acc["piv"] += ps; acc["pmax"] = max(acc["pmax"], pm)
         px = per_x[cur["xi"]]
-        px["piv"] += ps; px["n"] += n_local; px["lp"] += tm[0]
+        px["piv"] += ps; px["n"] += n_local; px["lp"] += tm[0]; px["eta"] += eta
         cur["piv"] += ps; cur["lp"] += tm[0]
     t0 = time.perf_counter()
     step_log = []    # per timed step: x index, wall ms, refresh ms, LP kernel ms, mean pivots
@@ -444,6 +446,7 @@ def main():
                  "pool_refresh_parts_ms": px.get("refresh_parts"),
                  "lp_kernel_ms": px["lp"] / 1e3 / max(px["steps"], 1),
                  "lp_pivots_mean": px["piv"] / max(px["n"], 1),
+                 "lp_eta_entries": px["eta"] / max(px["steps"], 1),
                  "alpha": px["alpha"],
                  "incumbent_objective": px.get("objective")}
                 for it, xx, px in zip(x_iters, xs, per_x)]
@@ -490,7 +493,10 @@ def main():
         "roofline": {"kernel": "lp_hyper_kernel", "bound": "mfma",
                      "note": "fp64 peak (vector == matrix on gfx950); achieved = counted fp64 FLOPs of the executed pivot path / LP kernel time",
                      "achieved": lp_tflops, "peak": PEAK_FP64_TFS, "unit": "TFLOP/s",
-                     "frac": lp_tflops / PEAK_FP64_TFS, "traffic": None},
+                     "frac": lp_tflops / PEAK_FP64_TFS, "traffic": None,
+                     # the main launch's eta-arena stores (row index + value per entry): the algorithmic
+                     # part of its HBM writes, next to the PMC WRITE_SIZE of the same launch
+                     "eta_write_bytes_per_launch": 12.0 * acc["eta"] / passes},
         "cutgen": {"kernel": "cut_argmax2_kernel (+pktc/vbase/fixup/reduce)", "hbm_gbs": cut_gbs,
                    "bytes_alg": bytes_alg, "flops_alg": flops_alg, "t_roof_ms": t_roof * 1e3,
                    "t_ms": cut_us / 1e3, "frac": t_roof / (cut_us * 1e-6),

@@ -230,7 +230,7 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_fixedmask); dfree(c->d_ubmask);
     dfree(c->d_hb0); dfree(c->d_basic0);
     dfree(c->d_xbase); dfree(c->d_queue); dfree(c->d_lpstats);
-    dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_ops);
+    dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_ops); dfree(c->d_etan);
     dfree(c->d_dvtmp);
     dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); c->sel_code_cap = 0; dfree(c->d_head_out); dfree(c->d_pool_pick); dfree(c->d_order); dfree(c->d_sort_tmp);
     dfree(c->d_cand); dfree(c->d_sel_key); dfree(c->d_sel_pkey); dfree(c->d_sel_ppick); c->sel_pcap = 0; c->key_cap = 0; c->pool_l1 = c->pool_ncand = 0; c->order_cap = 0; c->sort_tmp_bytes = 0; c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
@@ -2066,8 +2066,9 @@ __global__ void __launch_bounds__(kSelStreamThreads) pool_selstream_kernel(
         for (int cpy = 0; cpy < ncopy; ++cpy) {
             const float sg = (t == BT_Y || t == BT_L || cpy == 1) ? -1.0f : 1.0f;
             int2 *o = out + cpy * (1 + q1 - q0);
-            if (lane == 0) o[0] = make_int2(-1, __float_as_int(sg * (float)xbase[(size_t)p * MP + i]));
-            for (int q = q0 + lane; q < q1; q += 64) o[1 + q - q0] = make_int2(ke[q], __float_as_int(sg * (float)kraw[q]));
+            // record (value bits, byte offset of the element's staged pair row e * 65 * 8; -1: row start)
+            if (lane == 0) o[0] = make_int2(__float_as_int(sg * (float)xbase[(size_t)p * MP + i]), -1);
+            for (int q = q0 + lane; q < q1; q += 64) o[1 + q - q0] = make_int2(__float_as_int(sg * (float)kraw[q]), ke[q] * 65 * 8);
         }
     }
 }
@@ -2239,7 +2240,7 @@ int twosd::run_lp_ex(twosd_ctx *c, const double *x, const double *d_dv, int N, c
     if (N > c->out_cap) {
         size_t cap = std::max<size_t>(N, 1024);
         if ((rc = dalloc(&c->d_obj, cap)) || (rc = dalloc(&c->d_status, cap)) || (rc = dalloc(&c->d_iters, cap)) ||
-            (rc = dalloc(&c->d_ops, cap)))
+            (rc = dalloc(&c->d_ops, cap)) || (rc = dalloc(&c->d_etan, cap)))
             return rc;
         dfree(c->d_pi); dfree(c->d_y);
         c->pi_cap = c->y_cap = 0;
@@ -2331,7 +2332,7 @@ int twosd::run_lp_ex(twosd_ctx *c, const double *x, const double *d_dv, int N, c
             H.head_out = c->d_head_out;
         }
         H.pi_by_pos = list ? 1 : 0;
-        H.status = c->d_status; H.iters = c->d_iters; H.ops = c->d_ops;
+        H.status = c->d_status; H.iters = c->d_iters; H.ops = c->d_ops; H.etan = c->d_etan;
         if (!c->d_stamps) {
             if ((rc = dalloc(&c->d_stamps, 16))) return rc;
             HIPCHK(hipMemset(c->d_stamps, 0, sizeof(unsigned long long) * 16));
@@ -2380,19 +2381,21 @@ int twosd::run_lp_ex(twosd_ctx *c, const double *x, const double *d_dv, int N, c
 // batch statistics on the device (integer sums: exact, order independent): [0] pivots,
 // [1] executed FMAs, [2] max pivots, [3] non-optimal scenarios
 __global__ void lp_stats_kernel(int N, const int *__restrict__ its, const long long *__restrict__ ops,
-                                const int *__restrict__ st, unsigned long long *out) {
-    unsigned long long a = 0, b = 0, d = 0;
+                                const int *__restrict__ st, const int *__restrict__ etan, unsigned long long *out) {
+    unsigned long long a = 0, b = 0, d = 0, e = 0;
     unsigned long long mx = 0;
     for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < N; s += gridDim.x * blockDim.x) {
         a += (unsigned long long)its[s];
         b += (unsigned long long)ops[s];
         mx = its[s] > (int)mx ? (unsigned long long)its[s] : mx;
         d += st[s] != TWOSD_LP_OPTIMAL;
+        e += (unsigned long long)etan[s];
     }
     for (int o = 32; o > 0; o >>= 1) {
         a += __shfl_down(a, o);
         b += __shfl_down(b, o);
         d += __shfl_down(d, o);
+        e += __shfl_down(e, o);
         const unsigned long long m2 = __shfl_down(mx, o);
         mx = m2 > mx ? m2 : mx;
     }
@@ -2401,6 +2404,7 @@ __global__ void lp_stats_kernel(int N, const int *__restrict__ its, const long l
         atomicAdd(&out[1], b);
         atomicMax(&out[2], mx);
         atomicAdd(&out[3], d);
+        atomicAdd(&out[4], e);
     }
 }
 
@@ -2436,20 +2440,20 @@ __global__ void __launch_bounds__(256) lp_obj_kernel(int N, const double *__rest
 // d_w: the batch's scenario weights (nullable: 1.0), for the objective sum
 static int copy_lp_outputs(twosd_ctx *c, int N, double *obj, double *pi, double *y, int *status, const double *d_w) {
     if (!c->d_lpstats) {
-        int rc = dalloc(&c->d_lpstats, 4);
+        int rc = dalloc(&c->d_lpstats, 5);
         if (rc) return rc;
     }
     if (!c->d_objpart) {
         int rc = dalloc(&c->d_objpart, (size_t)2 * kObjBlocks);
         if (rc) return rc;
     }
-    HIPCHK(hipMemsetAsync(c->d_lpstats, 0, 4 * sizeof(unsigned long long), c->stream));
+    HIPCHK(hipMemsetAsync(c->d_lpstats, 0, 5 * sizeof(unsigned long long), c->stream));
     hipLaunchKernelGGL(lp_stats_kernel, dim3((unsigned)std::min(1024, (N + 255) / 256)), dim3(256), 0, c->stream, N,
-                       c->d_iters, c->d_ops, c->d_status, c->d_lpstats);
+                       c->d_iters, c->d_ops, c->d_status, c->d_etan, c->d_lpstats);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(lp_obj_kernel, dim3(kObjBlocks), dim3(256), 0, c->stream, N, c->d_obj, d_w, c->d_objpart);
     HIPCHK(hipGetLastError());
-    unsigned long long stv[4];
+    unsigned long long stv[5];
     double part[2 * kObjBlocks];
     HIPCHK(hipMemcpyAsync(stv, c->d_lpstats, sizeof(stv), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(part, c->d_objpart, sizeof(part), hipMemcpyDeviceToHost, c->stream));
@@ -2459,6 +2463,7 @@ static int copy_lp_outputs(twosd_ctx *c, int N, double *obj, double *pi, double 
     if (y) HIPCHK(hipMemcpy(y, c->d_y, sizeof(double) * N * c->L.n, hipMemcpyDeviceToHost));
     if (status) HIPCHK(hipMemcpy(status, c->d_status, sizeof(int) * N, hipMemcpyDeviceToHost));
     c->last_pivots_sum = (int64_t)stv[0]; c->last_ops_sum = (int64_t)stv[1]; c->last_pivots_max = (int)stv[2];
+    c->last_eta_entries = (int64_t)stv[4];
     if (N >= 4096) {
         c->piv_mean_ref = (double)stv[0] / N;
         c->piv_ref_sum = (int64_t)stv[0];
@@ -2529,6 +2534,12 @@ extern "C" int twosd_last_timings(twosd_ctx *c, double *us5) {
     return TWOSD_OK;
 }
 
+extern "C" int twosd_last_lp_eta_entries(twosd_ctx *c, int64_t *entries) {
+    if (!c || !entries) return fail(TWOSD_E_ARG, "last_lp_eta_entries: NULL");
+    *entries = c->last_eta_entries;
+    return TWOSD_OK;
+}
+
 extern "C" int twosd_last_lp_stats(twosd_ctx *c, int64_t *sum, int *mx) {
     if (!c) return fail(TWOSD_E_ARG, "last_lp_stats: NULL");
     if (sum) *sum = c->last_pivots_sum;
@@ -2596,7 +2607,7 @@ extern "C" int twosd_solve_push(twosd_ctx *c, int epi, const double *x, int firs
     rc = copy_lp_outputs(c, count, obj, nullptr, nullptr, status, E.d_w + first);
     if (rc) return rc;   // some LP not optimal: nothing pushed
     const double obj_wsum = c->last_obj_wsum, obj_w = c->last_obj_w;
-    const int64_t piv_sum = c->last_pivots_sum, ops_sum = c->last_ops_sum;
+    const int64_t piv_sum = c->last_pivots_sum, ops_sum = c->last_ops_sum, eta_sum = c->last_eta_entries;
     const int piv_max = c->last_pivots_max;
     float ms = 0, ms_key = 0;
     if (all) {
@@ -2642,6 +2653,7 @@ extern "C" int twosd_solve_push(twosd_ctx *c, int epi, const double *x, int firs
         }
         c->t_us[4] = t_sel;
         c->last_pivots_sum = piv_sum; c->last_ops_sum = ops_sum; c->last_pivots_max = piv_max;
+        c->last_eta_entries = eta_sum;
     }
     c->last_obj_wsum = obj_wsum; c->last_obj_w = obj_w;   // of the batch, not of the representatives' re-solve
     c->t_us[1] = 1e3 * (ms + ms_key);

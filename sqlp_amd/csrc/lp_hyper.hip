@@ -162,15 +162,15 @@ __device__ __forceinline__ int h_prefix_count(uint64_t m) {
 // per-wave LDS slice: a union of {ut, rho} (MP doubles each) and alpha (the pivot row over the
 // 64C column slots during pricing; the columns past n + m are never scattered to, so every slot
 // can be read and zeroed unconditionally), the scenario deltas (k doubles), the pricing list
-// values (64 doubles), the dual Devex weights (MP floats), the pricing list rows and row-start
-// marks (64 ints each), etap (u16), etaoff (int)
+// values (64 doubles), the pricing list rows and row-start marks (64 ints each), etap (u16),
+// etaoff (int)
 static __host__ __device__ inline int hyper_union_doubles(int R, int C) {
     return 128 * R > 64 * C ? 128 * R : 64 * C;
 }
 static __host__ __device__ inline size_t hyper_slice_bytes(int R, int C, int kmax, int k) {
     const int kmaxp = (kmax + 3) & ~3;
-    return 8 * (size_t)hyper_union_doubles(R, C) + 8 * (size_t)((k + 1) & ~1) + 8 * 64 + 4 * (size_t)(64 * R) + 4 * 64 +
-           4 * 64 + 2 * kmaxp + 4 * (kmaxp + 4);
+    return 8 * (size_t)hyper_union_doubles(R, C) + 8 * (size_t)((k + 1) & ~1) + 8 * 64 + 4 * 64 + 4 * 64 + 2 * kmaxp +
+           4 * (kmaxp + 4);
 }
 size_t hyper_lds_bytes(int R, int C, int kmax, int k) { return (size_t)kWavesPerBlock * hyper_slice_bytes(R, C, kmax, k); }
 
@@ -224,8 +224,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
     double *alpha = ut;                                     // pricing: alpha'_j over the same space
     double *dvl = ut + UD;                                  // this scenario's coef_e(x) dv_e
     double *lstv = dvl + ((P.k + 1) & ~1);                  // pricing list: rho values
-    float *w = reinterpret_cast<float *>(lstv + 64);        // dual Devex weights (row i at w[i])
-    int *lsti = reinterpret_cast<int *>(w + MP);            // pricing list: rows
+    int *lsti = reinterpret_cast<int *>(lstv + 64);         // pricing list: rows
     int *smark = lsti + 64;                                 // pricing: row starts within a wave step
     unsigned short *etap = reinterpret_cast<unsigned short *>(smark + 64);
     int *etaoff = reinterpret_cast<int *>(etap + kmaxp);
@@ -282,6 +281,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         // warm-start basis: chosen per scenario by pool_select_kernel (0 without a pool)
         int pb = P.npool > 1 ? __builtin_amdgcn_readfirstlane(P.pool_pick[s]) : 0;
         double xB[R];
+        float wd[R];   // dual Devex weights, row 64t + lane (registers: no LDS round trip per update)
         int hb[R];
         double d[C];   // sign-folded reduced costs d'_j, j = 64c + lane
         uint64_t bmask;
@@ -298,7 +298,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         for (int t = 0; t < R; ++t) {
             xB[t] = xb_row(pb, t);
             hb[t] = P.hb0[(size_t)pb * MP + 64 * t + lane];
-            w[64 * t + lane] = 1.0f;
+            wd[t] = 1.0f;
         }
 #pragma unroll
         for (int c = 0; c < C; ++c)
@@ -324,7 +324,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 const bool inf = (hb[t] >= 0) & (((xB[t] < -HTOL_P) & (bt != BT_G)) | ((xB[t] > HTOL_P) & ((bt & 1) != 0)));
                 if (inf) {
                     const double dl = xB[t];
-                    const double num = dl * dl, den = (double)w[64 * t + lane];
+                    const double num = dl * dl, den = (double)wd[t];
                     if (num * bden > bnum * den) { bnum = num; bden = den; br = 64 * t + lane; bdel = dl; }
                 }
             }
@@ -582,33 +582,37 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             // ---- 5. updates: primal, Devex, sparse eta, basis, reduced costs of q / leaving
             const double thetaP = delta / arq;
             const double inv_arq = 1.0 / arq;
-            const float wrr = w[r];
+            float wrr = 0.0f;
+#pragma unroll
+            for (int t = 0; t < R; ++t) {
+                const float u = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, wd[t]), r & 63));
+                wrr = (t == (r >> 6)) ? u : wrr;
+            }
             int cnt = 0;
 #pragma unroll
             for (int t = 0; t < R; ++t) cnt += __popcll(__ballot(col[t] != 0.0));
             if (eoff + cnt > P.ecap) { status = TWOSD_LP_ITER_LIMIT; h_wave_sync(); break; }
+            // per slot: the eta entry (stores under the nonzero mask), x_B and the Devex weight by
+            // selects (row r: thetaP and max(wrr / arq^2, 1); others with col != 0: x_B - thetaP col,
+            // max(w, ratio^2 wrr))
             int base = eoff;
 #pragma unroll
             for (int t = 0; t < R; ++t) {
                 const int i = 64 * t + lane;
                 const bool nz = col[t] != 0.0;
+                const bool isr = i == r;
                 const uint64_t bal = __ballot(nz);
+                const double ratio = col[t] * inv_arq;
                 if (nz) {
                     const int pos = base + h_prefix_count(bal);
-                    const double ratio = col[t] * inv_arq;
                     eidx[pos] = i;
-                    evals[pos] = (i == r) ? inv_arq : -ratio;
-                    if (i == r) {
-                        xB[t] = thetaP;
-                        const float nw = (float)((double)wrr * inv_arq * inv_arq);
-                        w[i] = nw > 1.0f ? nw : 1.0f;
-                    } else {
-                        xB[t] = fma(-thetaP, col[t], xB[t]);
-                        const float cand = (float)(ratio * ratio * (double)wrr);
-                        const float wo = w[i];
-                        w[i] = cand > wo ? cand : wo;
-                    }
+                    evals[pos] = isr ? inv_arq : -ratio;
                 }
+                const float nw = (float)((double)wrr * inv_arq * inv_arq);
+                const float cand = (float)(ratio * ratio * (double)wrr);
+                const double xo = fma(-thetaP, col[t], xB[t]);
+                xB[t] = isr ? thetaP : (nz ? xo : xB[t]);
+                wd[t] = isr ? (nw > 1.0f ? nw : 1.0f) : ((nz & (cand > wd[t])) ? cand : wd[t]);
                 base += __popcll(bal);
             }
             eoff += cnt;
@@ -805,6 +809,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             P.status[s] = status;
             P.iters[s] = it;
             if (P.ops) P.ops[s] = nops;
+            if (P.etan) P.etan[s] = eoff;   // the eta-arena entries this solve wrote (12 B each)
             if (P.npool > 1) P.pool_pick[s] = pb;   // 0 if the pool start was retried
         }
         h_wave_sync();
@@ -855,12 +860,23 @@ __device__ __forceinline__ void h_stage_pairs(float *dvt, const double *__restri
         dvt[2 * (e * 65 + (sl & 63)) + (sl >> 6)] = sl < nv ? (float)(kcoef[e] * dv[(size_t)srow(sl) * k + e]) : 0.0f;
     }
 }
-// one basis' record stream for both scenarios of the lane (code < 0: row start), pruned once no
-// scenario of the wave can still win (alive2); returns the pair's keys (inf when pruned)
+// byte address of the staged pair of element `off` (the record's byte offset e * 65 * 8; row starts
+// carry -1 and read element 0) for this lane, computed on the VALU: the record streams are
+// wave-uniform, so on the scalar unit every record's address would add two SALU instructions to
+// a loop that is SALU-bound already
+__device__ __forceinline__ const sel_f2 *h_pair_addr(const sel_f2 *dvt2, int off, int lane8) {
+    int o;
+    asm("v_max_i32 %0, %1, 0" : "=v"(o) : "s"(off));
+    return reinterpret_cast<const sel_f2 *>(reinterpret_cast<const char *>(dvt2) + o + lane8);
+}
+// one basis' record stream for both scenarios of the lane (records (value bits, byte offset); offset
+// < 0: row start), pruned once no scenario of the wave can still win (alive2); returns the pair's
+// keys (inf when pruned)
 template <typename Alive>
 __device__ __forceinline__ sel_f2 h_stream2(const int2 *__restrict__ rec, int j0, int j1, float cinf, float cw,
                                             const sel_f2 *dvt2, int lane, Alive alive2) {
     sel_f2 inf = {cinf, cinf}, x = {0.0f, 0.0f};
+    const int lane8 = 8 * lane;
     auto step = [&](int code, float v, sel_f2 dl) {
         if (code < 0) {   // next row: close the previous one
             inf += h_viol_f2(x, cw);
@@ -876,16 +892,16 @@ __device__ __forceinline__ sel_f2 h_stream2(const int2 *__restrict__ rec, int j0
 #pragma unroll
         for (int u = 0; u < kSelB; ++u) rc[u] = rec[j + u];
 #pragma unroll
-        for (int u = 0; u < kSelB; ++u) dl[u] = dvt2[(rc[u].x < 0 ? 0 : rc[u].x) * 65 + lane];
+        for (int u = 0; u < kSelB; ++u) dl[u] = *h_pair_addr(dvt2, rc[u].y, lane8);
 #pragma unroll
-        for (int u = 0; u < kSelB; ++u) step(rc[u].x, __int_as_float(rc[u].y), dl[u]);
+        for (int u = 0; u < kSelB; ++u) step(rc[u].y, __int_as_float(rc[u].x), dl[u]);
         // exact pruning: inf only grows, so once no scenario of the wave can still beat its best,
         // this basis cannot win for any of them
         if (__ballot(alive2(inf)) == 0) return (sel_f2){INFINITY, INFINITY};
     }
     for (; j < j1; ++j) {
         const int2 r = rec[j];
-        step(r.x, __int_as_float(r.y), dvt2[(r.x < 0 ? 0 : r.x) * 65 + lane]);
+        step(r.y, __int_as_float(r.x), *h_pair_addr(dvt2, r.y, lane8));
     }
     inf += h_viol_f2(x, cw);
     return inf;

@@ -119,10 +119,12 @@ struct twosd_ctx {
     int last_ops_width = 1;
     // LP workspace + outputs
     int *d_queue = nullptr;
-    unsigned long long *d_lpstats = nullptr;   // lp_stats_kernel output (4 words)
+    unsigned long long *d_lpstats = nullptr;   // lp_stats_kernel output (5 words)
     double *d_obj = nullptr, *d_pi = nullptr, *d_y = nullptr;
     int *d_status = nullptr, *d_iters = nullptr;
     long long *d_ops = nullptr;
+    int *d_etan = nullptr;
+    int64_t last_eta_entries = 0;
     int64_t last_ops_sum = 0;
     int out_cap = 0;
     size_t pi_cap = 0, y_cap = 0;

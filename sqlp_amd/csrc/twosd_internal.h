@@ -51,6 +51,7 @@ struct HyperParams {
     double *obj, *pi, *y;
     int *status, *iters;
     long long *ops;                                     // executed FMAs
+    int *etan;                                          // N: eta-file entries of the final solve (nullable)
     unsigned long long *stamps;                         // [10] phase cycles (TWOSD_STAMPS builds only)
     // basis pool: xbase, hb0 (npool x MP), brptr / bcp (npool x (MP+1), absolute offsets),
     // basic0 (npool x 64), d0 (npool x 64C) are pool-strided
@@ -131,8 +132,8 @@ struct PoolSelParams {
     const double *kcoef;                                // k: coef_e(x)
     const float *cinf;                                  // npool: infeasibility of the constant rows
     const int *sptr, *send;                             // npool: [sptr[p], send[p]) = records of basis p
-    const int2 *rec;                                    // (code, float bits): row start (-1, sign-folded
-                                                        //   xbase_i); entry (e, sign * B^{-1}[i][row_e])
+    const int2 *rec;                                    // (float bits, code): row start (sign-folded xbase_i,
+                                                        //   -1); entry (sign * B^{-1}[i][row_e], e * 65 * 8)
     int *pick;                                          // N out
     float cw;                                           // key = sum |infeas| + cw * #infeasible rows
     float *key;                                         // N out (nullable): key of the pick

@@ -315,6 +315,12 @@ class SDContext:
         check(self.lib.twosd_last_lp_stats(self.h, C.byref(s), C.byref(mx)))
         return s.value, mx.value
 
+    def lp_eta_entries(self) -> int:
+        """Eta-arena entries (12 B each) the last LP batch wrote (twosd_last_lp_eta_entries)."""
+        e = C.c_int64()
+        check(self.lib.twosd_last_lp_eta_entries(self.h, C.byref(e)))
+        return e.value
+
     def last_push_reps(self) -> int:
         """Scenarios whose dual the last solve_push recovered and pushed (first scenario of
         each distinct optimal dual vertex of the batch)."""

@@ -22,6 +22,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 LINK_GBS = 153.0 * 0.5       # xGMI link, half of the per-link figure (RCCL efficiency assumed)
+COLLECTIVE_MS = 0.05         # latency of one small RCCL collective + its host synchronisation (assumed)
+REFRESH_COLLECTIVES = 6      # collectives of one distributed refresh (sqlp_amd.dist.refresh_sharded)
+STEP_COLLECTIVES = 5         # per step besides the refresh: V-set check, 2 for the vertex all-gather, 2 for the
+                             # cut partials (histogram, sums + incumbent objective)
 
 
 def main():
@@ -77,11 +81,25 @@ def main():
         """the distributed refresh, phase by phase per rank; returns per-rank ms and pack bytes"""
         ms = [dict() for _ in range(G)]
         lists = []
+        # one training cap for all ranks (sqlp_amd.dist.refresh_training_cap: 3 x the mean pivots
+        # of every rank's last large batch, at least 32)
+        ps = sum(rk["ctx"].refresh_cap_stats()[0] for rk in ranks)
+        pn = sum(rk["ctx"].refresh_cap_stats()[1] for rk in ranks)
+        cap = max(32, int(np.ceil(3.0 * ps / pn))) if pn > 0 else 0
+        nopt = []
         for r, rk in enumerate(ranks):
             t = time.perf_counter()
-            k, c, f, lo_, hi_ = rk["ctx"].refresh_train(rk["tr"], xx, 0, rk["nt"])
+            k, c, f, lo_, hi_, no = rk["ctx"].refresh_train_ex(rk["tr"], xx, 0, rk["nt"], cap)
             ms[r]["train"] = 1e3 * (time.perf_counter() - t)
             lists.append((k, c, f, lo_, hi_))
+            nopt.append(no)
+        if cap > 0 and 2 * sum(nopt) < sum(rk["nt"] for rk in ranks):    # the global uncapped retry
+            lists = []
+            for r, rk in enumerate(ranks):
+                t = time.perf_counter()
+                k, c, f, lo_, hi_, no = rk["ctx"].refresh_train_ex(rk["tr"], xx, 0, rk["nt"], 0)
+                ms[r]["train"] += 1e3 * (time.perf_counter() - t)
+                lists.append((k, c, f, lo_, hi_))
         t = time.perf_counter()
         kk = np.concatenate([l[0] for l in lists])
         cc = np.concatenate([l[1] for l in lists]).astype(np.int64)
@@ -118,8 +136,11 @@ def main():
             t = time.perf_counter()
             rk["ctx"].pool_set_candidates(L1, NC, p1, pf)
             ms[r]["cand_lists"] = 1e3 * (time.perf_counter() - t)
-            # exchanges: basis lists (tiny), packs, picks (tiny) -- estimated
-            ms[r]["xgmi_est"] = 1e3 * (max(nbytes[q] for q in range(G) if q != r) if G > 1 else 0) / (LINK_GBS * 1e9) + 0.1
+            # exchanges: the packs by bandwidth (each GPU receives the G - 1 other packs over its
+            # G - 1 links in parallel) plus a fixed latency per collective and host synchronisation
+            # (sqlp_amd.dist.refresh_sharded: cap all-reduce, header, payload, pack size, packs, picks)
+            ms[r]["xgmi_est"] = (1e3 * (max(nbytes[q] for q in range(G) if q != r) if G > 1 else 0) / (LINK_GBS * 1e9) +
+                                 REFRESH_COLLECTIVES * COLLECTIVE_MS)
         return ms, nbytes, int(ranks[0]["ctx"].pool_size())
 
     def solve_cut(rk, xx):
@@ -127,7 +148,7 @@ def main():
         twosd.solve_push(rk["epi"], xx, 0, rk["n"], want_obj=False)
         rk["V"].truncate(nv)
         piv = rk["ctx"].lp_stats()[0] / rk["n"]
-        twosd.build_sasa_cut(rk["epi"], xx, rk["V"], 1e-12)
+        twosd.build_sasa_cut(rk["epi"], xx, rk["V"], 0.0)
         return 1e3 * (time.perf_counter() - t), piv
 
     refresh(xs[-1])       # warmup: the pool at the last x point
@@ -139,6 +160,7 @@ def main():
         for r, rk in enumerate(ranks):
             t_sc, piv = solve_cut(rk, xx)
             ms[r]["solve_cut"] = t_sc
+            ms[r]["step_collectives_est"] = STEP_COLLECTIVES * COLLECTIVE_MS
             per.append((sum(ms[r].values()), piv))
         worst = max(range(G), key=lambda r: per[r][0])
         rows.append((i % len(xs), per[worst][0], np.mean([p[0] for p in per]), np.mean([p[1] for p in per]), P,
@@ -148,7 +170,9 @@ def main():
     step_ms = float(np.mean([r[1] for r in rows]))
     print(json.dumps({"G": G, "scenarios": N, "pool": POOL, "train": TRAIN, "per_rank_step_ms": step_ms,
                       "subproblems_per_s_projected": N / (step_ms * 1e-3),
-                      "note": f"emulated on one GPU; xGMI all-gather estimated at {LINK_GBS} GB/s per link"}), flush=True)
+                      "note": f"emulated on one GPU; xGMI all-gather estimated at {LINK_GBS} GB/s per link, "
+                              f"{COLLECTIVE_MS} ms per collective ({REFRESH_COLLECTIVES} per refresh, "
+                              f"{STEP_COLLECTIVES} per step besides)"}), flush=True)
 
 
 if __name__ == "__main__":
