@@ -354,7 +354,7 @@ def main():
     for i in range(args.warmup):
         step(xs[(i - args.warmup) % X])
     barrier()
-    acc = {"lp": 0.0, "dd": 0.0, "cut": 0.0, "fin": 0.0, "sel": 0.0, "flops": 0.0, "piv": 0, "pmax": 0, "eta": 0}
+    acc = {"lp": 0.0, "dd": 0.0, "cut": 0.0, "fin": 0.0, "sel": 0.0, "flops": 0.0, "piv": 0, "pmax": 0, "eta": 0, "retries": 0}
     per_x = [{"piv": 0, "n": 0, "lp": 0.0, "wall": 0.0, "steps": 0, "alpha": None, "refresh": 0.0, "eta": 0} for _ in xs]
     cur = {"xi": 0, "piv": 0, "lp": 0.0}
 
@@ -362,8 +362,9 @@ def main():
         tm = ctx.timings_us()
         acc["lp"] += tm[0]; acc["dd"] += tm[1]; acc["cut"] += tm[2]; acc["fin"] += tm[3]; acc["sel"] += tm[4]
         acc["flops"] += ctx.lp_flops()
-        eta = ctx.lp_eta_entries()
+        eta, retries = ctx.lp_counts()
         acc["eta"] += eta
+        acc["retries"] += retries
         ps, pm = ctx.lp_stats()
         acc["piv"] += ps; acc["pmax"] = max(acc["pmax"], pm)
         px = per_x[cur["xi"]]
@@ -485,6 +486,9 @@ def main():
         "phases_ms_per_step": {"pool_select": t_sel / K / 1e3, "lp_kernel": t_lp / K / 1e3, "dedup": t_dd / K / 1e3,
                                "cut_partial": t_cut / K / 1e3, "cut_finalize": t_fin / K / 1e3},
         "lp_pivots_mean": piv_sum / (passes * n_local), "lp_pivots_max": piv_max,
+        # scenarios of the timed steps whose pool start hit the iteration cap (or numerics) and were
+        # solved again from the primary basis
+        "lp_iter_limit_retries": acc["retries"],
         "x_points": x_points,
         "steps_log": {"columns": ["x_index", "ms", "refresh_ms", "lp_kernel_ms", "lp_pivots_mean"], "rows": step_log},
         "tie_rule": ("strict '>' (the reference's argmax_procedure, subprob.jl:156)" if args.tie_rel == 0 else

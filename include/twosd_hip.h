@@ -273,8 +273,10 @@ int twosd_last_timings(twosd_ctx *ctx, double *us5);
 /* Statistics of the last LP batch: sum of simplex pivots, max pivots. */
 int twosd_last_lp_stats(twosd_ctx *ctx, int64_t *pivots_sum, int *pivots_max);
 /* Eta-file entries the last LP batch wrote to the per-wavefront eta arena (12 bytes each: row index
- * and value), summed over its scenarios: the algorithmic share of the LP kernel's HBM writes. */
-int twosd_last_lp_eta_entries(twosd_ctx *ctx, int64_t *entries);
+ * and value), summed over its scenarios: the algorithmic share of the LP kernel's HBM writes.
+ * *retries (nullable): its scenarios whose pool start ended non-optimal (iteration cap, numerics)
+ * and were solved again from the primary basis. */
+int twosd_last_lp_eta_entries(twosd_ctx *ctx, int64_t *entries, int64_t *retries);
 
 /* Incumbent objective of the last twosd_solve_batch / twosd_solve_push / twosd_solve_values
  * batch: *weighted_sum = sum_s w_s obj_s and *weight_sum = sum_s w_s over its scenarios (the

@@ -66,7 +66,7 @@ SIGNATURES = [
     ("twosd_cut_finalize", I, [P, P, P, P, P, P]),
     ("twosd_last_timings", I, [P, P]),
     ("twosd_last_lp_stats", I, [P, P, P]),
-    ("twosd_last_lp_eta_entries", I, [P, P]),
+    ("twosd_last_lp_eta_entries", I, [P, P, P]),
     ("twosd_last_lp_ops", I, [P, P, P]),
     ("twosd_debug_stamps", I, [P, P, I]),
     ("twosd_last_lp_iters", I, [P, I, P, P]),

@@ -232,7 +232,7 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_xbase); dfree(c->d_queue); dfree(c->d_lpstats);
     dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_ops); dfree(c->d_etan);
     dfree(c->d_dvtmp);
-    dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); c->sel_code_cap = 0; dfree(c->d_head_out); dfree(c->d_pool_pick); dfree(c->d_order); dfree(c->d_sort_tmp);
+    dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); c->sel_code_cap = 0; dfree(c->d_head_out); dfree(c->d_pool_pick); dfree(c->d_cpick); dfree(c->d_order); dfree(c->d_sort_tmp);
     dfree(c->d_cand); dfree(c->d_sel_key); dfree(c->d_sel_pkey); dfree(c->d_sel_ppick); c->sel_pcap = 0; c->key_cap = 0; c->pool_l1 = c->pool_ncand = 0; c->order_cap = 0; c->sort_tmp_bytes = 0; c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
     dfree(c->d_dist_kind); dfree(c->d_dist_off); dfree(c->d_dist_val); dfree(c->d_dist_prob); dfree(c->d_dist_p0);
     dfree(c->d_dist_p1); dfree(c->d_dist_tmpl); c->has_dist = false;
@@ -1514,8 +1514,8 @@ static int candidate_picks(twosd_ctx *c, const EpiDevice &E, const double *x, in
                            int *p1, int *pf) {
     int rc;
     if ((rc = prepare_x(c, x))) return rc;
-    int *d_p = nullptr;
-    if ((rc = dalloc(&d_p, (size_t)count))) return rc;
+    if ((rc = dev_reserve(c, &c->d_cpick, (size_t)count))) return rc;   // grow-only: no hipMalloc / hipFree per refresh
+    int *d_p = c->d_cpick;
     const double *dv = E.d_dv + (size_t)first * c->k;
     auto picks = [&](int np, int *out) {   // selection runs on c->stream
         int r = select_pool(c, dv, count, d_p, np);
@@ -1526,7 +1526,6 @@ static int candidate_picks(twosd_ctx *c, const EpiDevice &E, const double *x, in
     };
     rc = picks(level1, p1);
     if (!rc) rc = picks((int)c->pool.size(), pf);
-    hipFree(d_p);
     return rc;
 }
 
@@ -1563,7 +1562,7 @@ static int set_candidates(twosd_ctx *c, int level1, int ncand, int n, const int 
                 c->pool.size(), level1, diff, n, filled);
     }
     int rc;
-    if ((rc = upload(&c->d_cand, cand))) return rc;
+    if ((rc = upload_big(c, &c->d_cand, cand))) return rc;
     c->pool_l1 = level1;
     c->pool_ncand = ncand;
     return TWOSD_OK;
@@ -2333,6 +2332,9 @@ int twosd::run_lp_ex(twosd_ctx *c, const double *x, const double *d_dv, int N, c
         }
         H.pi_by_pos = list ? 1 : 0;
         H.status = c->d_status; H.iters = c->d_iters; H.ops = c->d_ops; H.etan = c->d_etan;
+        if (!c->d_lpstats && (rc = dalloc(&c->d_lpstats, 6))) return rc;
+        if (!list) HIPCHK(hipMemsetAsync(c->d_lpstats + 5, 0, sizeof(unsigned long long), c->stream));
+        H.retries = list ? nullptr : c->d_lpstats + 5;   // a list re-solve repeats recorded picks: no retries
         if (!c->d_stamps) {
             if ((rc = dalloc(&c->d_stamps, 16))) return rc;
             HIPCHK(hipMemset(c->d_stamps, 0, sizeof(unsigned long long) * 16));
@@ -2440,7 +2442,7 @@ __global__ void __launch_bounds__(256) lp_obj_kernel(int N, const double *__rest
 // d_w: the batch's scenario weights (nullable: 1.0), for the objective sum
 static int copy_lp_outputs(twosd_ctx *c, int N, double *obj, double *pi, double *y, int *status, const double *d_w) {
     if (!c->d_lpstats) {
-        int rc = dalloc(&c->d_lpstats, 5);
+        int rc = dalloc(&c->d_lpstats, 6);
         if (rc) return rc;
     }
     if (!c->d_objpart) {
@@ -2453,7 +2455,7 @@ static int copy_lp_outputs(twosd_ctx *c, int N, double *obj, double *pi, double 
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(lp_obj_kernel, dim3(kObjBlocks), dim3(256), 0, c->stream, N, c->d_obj, d_w, c->d_objpart);
     HIPCHK(hipGetLastError());
-    unsigned long long stv[5];
+    unsigned long long stv[6];
     double part[2 * kObjBlocks];
     HIPCHK(hipMemcpyAsync(stv, c->d_lpstats, sizeof(stv), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(part, c->d_objpart, sizeof(part), hipMemcpyDeviceToHost, c->stream));
@@ -2464,6 +2466,7 @@ static int copy_lp_outputs(twosd_ctx *c, int N, double *obj, double *pi, double 
     if (status) HIPCHK(hipMemcpy(status, c->d_status, sizeof(int) * N, hipMemcpyDeviceToHost));
     c->last_pivots_sum = (int64_t)stv[0]; c->last_ops_sum = (int64_t)stv[1]; c->last_pivots_max = (int)stv[2];
     c->last_eta_entries = (int64_t)stv[4];
+    c->last_retries = (int64_t)stv[5];
     if (N >= 4096) {
         c->piv_mean_ref = (double)stv[0] / N;
         c->piv_ref_sum = (int64_t)stv[0];
@@ -2534,9 +2537,10 @@ extern "C" int twosd_last_timings(twosd_ctx *c, double *us5) {
     return TWOSD_OK;
 }
 
-extern "C" int twosd_last_lp_eta_entries(twosd_ctx *c, int64_t *entries) {
+extern "C" int twosd_last_lp_eta_entries(twosd_ctx *c, int64_t *entries, int64_t *retries) {
     if (!c || !entries) return fail(TWOSD_E_ARG, "last_lp_eta_entries: NULL");
     *entries = c->last_eta_entries;
+    if (retries) *retries = c->last_retries;
     return TWOSD_OK;
 }
 
@@ -2608,6 +2612,7 @@ extern "C" int twosd_solve_push(twosd_ctx *c, int epi, const double *x, int firs
     if (rc) return rc;   // some LP not optimal: nothing pushed
     const double obj_wsum = c->last_obj_wsum, obj_w = c->last_obj_w;
     const int64_t piv_sum = c->last_pivots_sum, ops_sum = c->last_ops_sum, eta_sum = c->last_eta_entries;
+    const int64_t retries = c->last_retries;
     const int piv_max = c->last_pivots_max;
     float ms = 0, ms_key = 0;
     if (all) {
@@ -2654,6 +2659,7 @@ extern "C" int twosd_solve_push(twosd_ctx *c, int epi, const double *x, int firs
         c->t_us[4] = t_sel;
         c->last_pivots_sum = piv_sum; c->last_ops_sum = ops_sum; c->last_pivots_max = piv_max;
         c->last_eta_entries = eta_sum;
+        c->last_retries = retries;
     }
     c->last_obj_wsum = obj_wsum; c->last_obj_w = obj_w;   // of the batch, not of the representatives' re-solve
     c->t_us[1] = 1e3 * (ms + ms_key);

@@ -652,6 +652,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             STAMP(8)
         }
         if (status == TWOSD_LP_OPTIMAL || pb == 0 || !P.retry) break;
+        if (lane == 0 && P.retries) atomicAdd(P.retries, 1ull);   // rare: counted for the bench line
         pb = 0;
         }   // attempt
 

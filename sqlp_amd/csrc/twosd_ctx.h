@@ -81,6 +81,7 @@ struct twosd_ctx {
     // level 2 over the candidate bases of the level-1 pick (d_cand: pool_l1 x pool_ncand)
     int pool_l1 = 0, pool_ncand = 0;
     int *d_cand = nullptr;
+    int *d_cpick = nullptr;       // candidate picks of the training scenarios (grow-only)
     float *d_sel_key = nullptr;
     float *d_sel_pkey = nullptr;          // chunked selection partials (split x N)
     int *d_sel_ppick = nullptr;
@@ -125,6 +126,7 @@ struct twosd_ctx {
     long long *d_ops = nullptr;
     int *d_etan = nullptr;
     int64_t last_eta_entries = 0;
+    int64_t last_retries = 0;     // pool starts of the last batch retried from the primary basis
     int64_t last_ops_sum = 0;
     int out_cap = 0;
     size_t pi_cap = 0, y_cap = 0;

@@ -52,6 +52,7 @@ struct HyperParams {
     int *status, *iters;
     long long *ops;                                     // executed FMAs
     int *etan;                                          // N: eta-file entries of the final solve (nullable)
+    unsigned long long *retries;                        // pool starts retried from the primary basis (nullable)
     unsigned long long *stamps;                         // [10] phase cycles (TWOSD_STAMPS builds only)
     // basis pool: xbase, hb0 (npool x MP), brptr / bcp (npool x (MP+1), absolute offsets),
     // basic0 (npool x 64), d0 (npool x 64C) are pool-strided

@@ -317,9 +317,14 @@ class SDContext:
 
     def lp_eta_entries(self) -> int:
         """Eta-arena entries (12 B each) the last LP batch wrote (twosd_last_lp_eta_entries)."""
+        return self.lp_counts()[0]
+
+    def lp_counts(self):
+        """(eta-arena entries, pool starts retried from the primary basis) of the last LP batch."""
         e = C.c_int64()
-        check(self.lib.twosd_last_lp_eta_entries(self.h, C.byref(e)))
-        return e.value
+        r = C.c_int64()
+        check(self.lib.twosd_last_lp_eta_entries(self.h, C.byref(e), C.byref(r)))
+        return e.value, r.value
 
     def last_push_reps(self) -> int:
         """Scenarios whose dual the last solve_push recovered and pushed (first scenario of
