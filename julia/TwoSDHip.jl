@@ -114,6 +114,14 @@ function solve_push!(epi::HipEpigraph, x::Vector{Float64}, first::Integer, count
     return Int(n[])
 end
 
+# incumbent objective of the last solve_push! / solve batch: (sum_s w_s obj_s, sum_s w_s) over its
+# scenarios (fixed-order device reduction); across ranks the caller sums both before dividing
+function last_objective(ctx::HipContext)
+    a = Ref(0.0); b = Ref(0.0)
+    check(ccall((:twosd_last_objective, LIB), Cint, (Ptr{Cvoid}, Ref{Float64}, Ref{Float64}), ctx.h, a, b))
+    return a[], b[]
+end
+
 # build_sasa_cut(epi, x, V) -> sdCut (epigraph.jl:125-146; argmax_procedure subprob.jl:141-169).
 # tie_rel = 0 is the reference's strict '>' (first maximum in insertion order).
 function build_sasa_cut(epi::HipEpigraph, x::Vector{Float64}; tie_rel::Float64=0.0)

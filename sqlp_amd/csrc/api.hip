@@ -141,13 +141,28 @@ static T *stage_buf(twosd_ctx *c, int slot, size_t n) {
 // refresh of 4096 bases would otherwise spend ~2 ms building host heads nobody reads)
 static const std::vector<int> &head_of(twosd_ctx *c, int p) {
     PoolBasis &B = c->pool[p];
-    if (B.hb_row >= 0) {
+    if (B.hb_row >= 0 && !c->pool_hb_valid) {
+        // the heads of a device-built pool are fetched on the first host use, not by the refresh
+        // (at N = 8 every rank would copy 9 MB per step that only tests and the CPU baseline read)
+        const size_t need = c->pool.size() * (size_t)c->MP;
+        if (need > c->pool_hb_cap) {
+            if (c->pool_hb) hipHostFree(c->pool_hb);
+            c->pool_hb = nullptr;
+            c->pool_hb_cap = 0;
+            if (hipHostMalloc((void **)&c->pool_hb, sizeof(int) * need * 5 / 4) == hipSuccess) c->pool_hb_cap = need * 5 / 4;
+        }
+        if (c->pool_hb && hipMemcpyAsync(c->pool_hb, c->d_hb0, sizeof(int) * need, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+            hipStreamSynchronize(c->stream) == hipSuccess)
+            c->pool_hb_valid = true;
+    }
+    if (B.hb_row >= 0 && c->pool_hb_valid) {
         const int m = c->L.m;
         const int *r = c->pool_hb + (size_t)B.hb_row * c->MP;
         B.head.resize(m);
         for (int i = 0; i < m; ++i) B.head[i] = r[i] >> 2;
         B.hb_row = -1;
     }
+    if (B.hb_row >= 0) B.head.assign(c->L.m, -1);   // the device read failed: no valid head (never a short vector)
     return B.head;
 }
 static void materialize_heads(twosd_ctx *c) {
@@ -947,21 +962,9 @@ static int pg_assemble(twosd_ctx *c, PgArgs &A, const int *h_tot, const int *h_v
     F.hb0 = c->d_hb0; F.basic0 = c->d_basic0; F.bnnz = c->d_bnnz; F.d0 = c->d_d0; F.sel_ptr = c->d_sel_ptr;
     F.P0 = 0;
     if (pg_launch_fill(A, F, P, c->stream) != hipSuccess) return broken(fail(TWOSD_E_DEVICE, "pool refresh: fill launch failed"));
-    // the pool's heads (hb0 = 4 head + type) into a pinned buffer of their own; a host head is
-    // materialised from it on first use (head_of)
-    // (the old pool's bases that refer to the buffer are dropped below; only the primary,
-    // a host basis, is kept)
-    if ((size_t)P * MP > c->pool_hb_cap) {
-        if (c->pool_hb) hipHostFree(c->pool_hb);
-        c->pool_hb = nullptr;
-        c->pool_hb_cap = 0;
-        if (hipHostMalloc((void **)&c->pool_hb, sizeof(int) * (size_t)P * MP * 5 / 4) != hipSuccess)
-            return broken(fail(TWOSD_E_DEVICE, "pool refresh: pinned allocation of the pool heads failed"));
-        c->pool_hb_cap = (size_t)P * MP * 5 / 4;
-    }
-    if (hipMemcpyAsync(c->pool_hb, c->d_hb0, sizeof(int) * P * MP, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-        hipStreamSynchronize(c->stream) != hipSuccess)
-        return broken(fail(TWOSD_E_DEVICE, "pool refresh: reading the built pool heads failed"));
+    // the pool's heads (hb0 = 4 head + type) stay on the device; a host head is fetched on first
+    // use (head_of)
+    c->pool_hb_valid = false;
     const auto t1 = std::chrono::steady_clock::now();
     // host pool: the primary keeps its host forms; the new bases refer to their head rows
     std::vector<PoolBasis> keep(P);

@@ -190,6 +190,7 @@ struct twosd_ctx {
     // no unmapping per refresh, page-locked copies)
     int *pool_hb = nullptr;       // pinned: the heads of the last device-built pool (P x MP, 4 head + type)
     size_t pool_hb_cap = 0;
+    bool pool_hb_valid = false;   // pool_hb holds d_hb0 of the current pool
     void *stage[16] = {};
     size_t stage_bytes[16] = {};
     std::map<const void *, size_t> dcap;   // element capacity of grow-only device arrays (by member address)

@@ -47,6 +47,7 @@ CCALLS = {
     "twosd_dvs_push": (Cint, [P, Cint, PF64, PI32, PI32]),
     "twosd_dvs_size": (Cint, [P, PI32]),
     "twosd_dvs_fingerprint": (Cint, [P, C.POINTER(C.c_uint64)]),
+    "twosd_last_objective": (Cint, [P, PF64, PF64]),
 }
 
 _LIB = None
@@ -157,6 +158,12 @@ def solve_push(epi: HipEpigraph, x, first, count) -> int:
     n = Cint()
     check(LIB().twosd_solve_push(epi.ctx.h, epi.index, _p(f64(x), PF64), first, count, None, None, C.byref(n)))
     return n.value
+
+
+def last_objective(ctx: HipContext):
+    a, b = F64(), F64()
+    check(LIB().twosd_last_objective(ctx.h, C.byref(a), C.byref(b)))
+    return a.value, b.value
 
 
 def build_sasa_cut(epi: HipEpigraph, x, tie_rel=0.0) -> twosd.sdCut:

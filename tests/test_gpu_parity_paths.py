@@ -249,3 +249,32 @@ def test_iteration_limit_status_and_pool_retry(monkeypatch):
     failed = st3 == LP_ITER_LIMIT
     assert failed.any()
     assert (picks[failed] == 0).all()                  # retried from the primary basis
+    retried = tiny.lp_counts()[1]                      # pool starts solved again from the primary basis
+    assert 0 < retried <= len(vals)
+
+
+@pytest.mark.parametrize("name", ["storm", "transship"])
+def test_last_objective_is_weighted_sum(name):
+    """twosd_last_objective: the batch's sum_s w_s obj_s and sum_s w_s (add_scenario! weights), a
+    fixed-order device reduction -- the same bits for solve_batch and solve_push of the same
+    batch, and the host sum of the returned objectives to rounding."""
+    from sqlp_amd import twosd
+    ctx, x = _ctx(name)
+    N = 3000
+    vals = I.sample(name, N, seed=23)
+    w = np.random.default_rng(4).uniform(0.5, 2.0, size=N)
+    epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(epi, vals, w)
+    obj, _, _, st = twosd.solve_batch(epi, x, 0, N, want_pi=False)
+    assert (st == 0).all()
+    a, b = ctx.last_objective()
+    assert b == pytest.approx(w.sum(), rel=1e-14)
+    assert a == pytest.approx(float(np.dot(w, obj)), rel=1e-12)
+    twosd.sdDualVertexSet(ctx)
+    twosd.solve_push(epi, x, 0, N, want_obj=False)
+    assert ctx.last_objective() == (a, b)
+    # a sub-range: weights first..first+count
+    twosd.solve_batch(epi, x, 100, 500, want_pi=False)
+    a2, b2 = ctx.last_objective()
+    assert b2 == pytest.approx(w[100:600].sum(), rel=1e-14)
+    assert a2 == pytest.approx(float(np.dot(w[100:600], obj[100:600])), rel=1e-12)

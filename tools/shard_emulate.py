@@ -146,9 +146,13 @@ def main():
     def solve_cut(rk, xx):
         t = time.perf_counter()      # the refresh prepared x (its candidate picks): no invalidate
         twosd.solve_push(rk["epi"], xx, 0, rk["n"], want_obj=False)
+        tm = rk["ctx"].timings_us()
         rk["V"].truncate(nv)
         piv = rk["ctx"].lp_stats()[0] / rk["n"]
         twosd.build_sasa_cut(rk["epi"], xx, rk["V"], 0.0)
+        tc = rk["ctx"].timings_us()
+        # device phases of the solve + cut (HIP events): selection, LP, dedup, cut
+        rk["phases"] = {"sel": tm[4] / 1e3, "lp": tm[0] / 1e3, "dedup": tm[1] / 1e3, "cut": (tc[2] + tc[3]) / 1e3}
         return 1e3 * (time.perf_counter() - t), piv
 
     refresh(xs[-1])       # warmup: the pool at the last x point
@@ -160,11 +164,12 @@ def main():
         for r, rk in enumerate(ranks):
             t_sc, piv = solve_cut(rk, xx)
             ms[r]["solve_cut"] = t_sc
+            ms[r]["solve_cut_device"] = {k: round(v, 2) for k, v in rk["phases"].items()}
             ms[r]["step_collectives_est"] = STEP_COLLECTIVES * COLLECTIVE_MS
-            per.append((sum(ms[r].values()), piv))
+            per.append((sum(v for v in ms[r].values() if not isinstance(v, dict)), piv))
         worst = max(range(G), key=lambda r: per[r][0])
         rows.append((i % len(xs), per[worst][0], np.mean([p[0] for p in per]), np.mean([p[1] for p in per]), P,
-                     {k: round(v, 2) for k, v in ms[worst].items()}, max(nbytes)))
+                     {k: (round(v, 2) if not isinstance(v, dict) else v) for k, v in ms[worst].items()}, max(nbytes)))
         print(f"x{rows[-1][0]}: per-rank step max {rows[-1][1]:.2f} ms (mean {rows[-1][2]:.2f}), pivots {rows[-1][3]:.2f}, "
               f"pool {P}, pack {max(nbytes) / 1e6:.1f} MB, slowest rank {rows[-1][5]}", flush=True)
     step_ms = float(np.mean([r[1] for r in rows]))
