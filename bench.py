@@ -115,6 +115,9 @@ def main():
                     help="N > 1: 1 = the ranks split the refresh (each trains on 1/N of the training scenarios and "
                          "composes its share of the pool, packs all-gathered: sqlp_amd.dist.refresh_sharded); "
                          "0 = every rank refreshes alone from all training scenarios with a pool sized by its shard")
+    ap.add_argument("--refresh-passes", type=int, default=1,
+                    help="refreshes per new x: 2 = refresh again from the pool the first pass built (its training "
+                         "solves start closer), both inside the timed step")
     ap.add_argument("--cpu-pool", type=int, default=128, help="bases of the pooled CPU baseline (0: off)")
     ap.add_argument("--pool", type=int, default=0,
                     help="warm-start basis pool size (1 = primary basis only; 0 = by the per-rank shard: "
@@ -281,12 +284,14 @@ def main():
             return 0.0
         t0 = time.perf_counter()
         if dist_refresh:
-            _, ms = sdist.refresh_sharded(ctx, rtr, xx, 0, t_hi - t_lo, args.refresh_pool, args.pool_level1,
-                                          args.pool_cands, device)
+            for _ in range(max(1, args.refresh_passes)):
+                _, ms = sdist.refresh_sharded(ctx, rtr, xx, 0, t_hi - t_lo, args.refresh_pool, args.pool_level1,
+                                              args.pool_cands, device)
             pool_at["x"] = xx.copy()
             pool_at["last_ms"] = ms
             return time.perf_counter() - t0
-        ctx.pool_refresh(rtr, xx, 0, args.refresh_train, args.refresh_pool)
+        for _ in range(max(1, args.refresh_passes)):
+            ctx.pool_refresh(rtr, xx, 0, args.refresh_train, args.refresh_pool)
         t1 = time.perf_counter()
         if args.pool_level1 > 0 and ctx.pool_size() > args.pool_level1:
             ctx.pool_build_candidates(rtr, xx, 0, args.refresh_train, args.pool_level1, args.pool_cands)

@@ -1535,22 +1535,27 @@ static int candidate_picks(twosd_ctx *c, const EpiDevice &E, const double *x, in
 // candidate lists from the picks of the training scenarios (any order): the ncand bases the flat
 // selection picks most often among the scenarios of each level-1 pick (ties: lower index)
 static int set_candidates(twosd_ctx *c, int level1, int ncand, int n, const int *p1, const int *pf) {
-    // (level-1 pick, flat pick) pairs that differ, sorted, then counted by runs
-    std::vector<long long> pr;
-    pr.reserve(n);
-    const long long P = (long long)c->pool.size();
+    // the differing (level-1 pick, flat pick) pairs bucketed by level-1 pick (counting sort), then
+    // per bucket the flat picks sorted and counted by runs; the ncand most frequent kept (ties:
+    // lower basis)
+    std::vector<int> start(level1 + 1, 0);
     for (int s = 0; s < n; ++s)
-        if (pf[s] != p1[s] && p1[s] >= 0 && p1[s] < level1) pr.push_back((long long)p1[s] * P + pf[s]);
-    std::sort(pr.begin(), pr.end());
+        if (pf[s] != p1[s] && p1[s] >= 0 && p1[s] < level1) ++start[p1[s] + 1];
+    for (int p = 0; p < level1; ++p) start[p + 1] += start[p];
+    std::vector<int> fill(start.begin(), start.end() - 1), bucket(start[level1]);
+    for (int s = 0; s < n; ++s)
+        if (pf[s] != p1[s] && p1[s] >= 0 && p1[s] < level1) bucket[fill[p1[s]]++] = pf[s];
     std::vector<int> cand((size_t)level1 * ncand, -1);
     std::vector<std::pair<int, int>> v;   // (-count, basis) of one level-1 pick
-    for (size_t a = 0; a < pr.size();) {
-        const long long p = pr[a] / P;
+    for (int p = 0; p < level1; ++p) {
+        int *b0 = bucket.data() + start[p], *b1 = bucket.data() + start[p + 1];
+        if (b0 == b1) continue;
+        std::sort(b0, b1);
         v.clear();
-        while (a < pr.size() && pr[a] / P == p) {
-            size_t b = a;
-            while (b < pr.size() && pr[b] == pr[a]) ++b;
-            v.push_back({-(int)(b - a), (int)(pr[a] % P)});
+        for (int *a = b0; a < b1;) {
+            int *b = a;
+            while (b < b1 && *b == *a) ++b;
+            v.push_back({-(int)(b - a), *a});
             a = b;
         }
         const size_t nk = std::min<size_t>(v.size(), ncand);
