@@ -159,6 +159,18 @@ __device__ __forceinline__ int h_prefix_count(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
+// The kernel's argument block read where a field is used: an s_load through a pointer the
+// compiler cannot see through, so the per-scenario (prologue / epilogue) fields are not held in
+// registers across the pivot loop.  Held there, they outgrow the 102 SGPRs, spill into VGPR lanes
+// and from there to scratch, which the 2048 waves' 55 MB of scratch then re-read from HBM on every
+// scenario.
+__device__ __forceinline__ const __attribute__((address_space(4))) HyperParams *h_args() {
+    uint64_t a = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(a));
+    return (const __attribute__((address_space(4))) HyperParams *)a;
+}
+#define CP (*h_args())
+
 // per-wave LDS slice: a union of {ut, rho} (MP doubles each) and alpha (the pivot row over the
 // 64C column slots during pricing; the columns past n + m are never scattered to, so every slot
 // can be read and zeroed unconditionally), the scenario deltas (k doubles), the pricing list
@@ -233,8 +245,8 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
     const int slot_id = blockIdx.x * kWavesPerBlock + wid;
     int *eidx = P.eidx + (size_t)slot_id * P.ecap;
     double *evals = P.evals + (size_t)slot_id * P.ecap;
-    const uint64_t fixedm = P.fixedmask[lane];
-    const uint64_t ubm = P.ubmask[lane];
+    const uint64_t fixedm = CP.fixedmask[lane];
+    const uint64_t ubm = CP.ubmask[lane];
 
     for (int j = lane; j < UD; j += 64) ut[j] = 0.0;
     smark[lane] = 0;
@@ -245,41 +257,53 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
     // served first by the blocks with blockIdx % qgroups == g (one XCD under the round-robin
     // block placement, speed only), so the waves that share a pool basis share one L2.  A wave
     // whose range is exhausted moves on to the next range (never back: exhausted stays exhausted).
-    const int G = P.qgroups;
+    // The claim of the next queue position, its scenario (order) and its pool pick are three
+    // dependent global round trips; they are software-pipelined across scenarios: the claim is
+    // issued when a scenario starts and resolved after its x_B loads (which it overlaps), the
+    // order load is issued then and resolved after the pivot loop, where the pick load is issued.
+    const int G = CP.qgroups;
     const int g0 = blockIdx.x % G;
     int gt = 0;
-    for (;;) {
-        int s = -1;
+    auto group_of = [&](int gi) { return g0 + gi < G ? g0 + gi : g0 + gi - G; };
+    auto claim_sync = [&]() -> int {   // next position, moving on to the next range when one is exhausted
         for (; gt < G; ++gt) {
-            const int g = g0 + gt < G ? g0 + gt : g0 + gt - G;
+            const int g = group_of(gt);
             const int lo = (int)(((long long)P.N * g) / G), hi = (int)(((long long)P.N * (g + 1)) / G);
             int t = 0;
-            if (lane == 0) t = atomicAdd(P.queue + g * kQueueStride, 1);
+            if (lane == 0) t = atomicAdd(CP.queue + g * kQueueStride, 1);
             t = __builtin_amdgcn_readfirstlane(__shfl(t, 0));
-            if (lo + t < hi) {
-                s = lo + t;
-                break;
-            }
+            if (lo + t < hi) return lo + t;
         }
-        if (s < 0) break;
-        const int qpos = s;
-        if (P.order) s = __builtin_amdgcn_readfirstlane(P.order[s]);   // grouped by pool basis
+        return -1;
+    };
+    int q_nx = claim_sync();
+    int s_nx = q_nx < 0 ? -1 : (CP.order ? __builtin_amdgcn_readfirstlane(CP.order[q_nx]) : q_nx);
+    int pb_nx = (s_nx >= 0 && CP.npool > 1) ? __builtin_amdgcn_readfirstlane(CP.pool_pick[s_nx]) : 0;
+    for (;;) {
+        if (q_nx < 0) break;
+        const int qpos = q_nx;
+        int s = s_nx;                                    // grouped by pool basis
+        int pb = pb_nx;                                  // warm-start basis (pool_select_kernel; 0 without a pool)
+        // claim of the following position, resolved after this scenario's x_B loads
+        int t_claim = 0;
+        if (lane == 0 && gt < G) t_claim = atomicAdd(CP.queue + group_of(gt) * kQueueStride, 1);
 
-        const double *dvs = P.dv + (size_t)s * P.k;
-        for (int e = lane; e < P.k; e += 64) dvl[e] = P.kcoef[e] * dvs[e];   // coef_e(x) dv_e
+        const double *dvs = CP.dv + (size_t)s * P.k;
+        for (int e = lane; e < P.k; e += 64) dvl[e] = CP.kcoef[e] * dvs[e];   // coef_e(x) dv_e
         h_wave_sync();
         // x_B of pool basis p at this scenario: xbase_p + sum_e coef_e B_p^{-1}[i][row_e] dv_e
         // (sliced ELL by row: independent coalesced loads, deltas gathered from LDS)
+        int lnx = lane;   // opaque copy: per-lane address terms of the gathers stay inside the scenario loop
+        asm volatile("" : "+v"(lnx));
         auto xb_row = [&](int p, int t) -> double {
+            const int lane = lnx;
             const int i = 64 * t + lane;
-            double x = P.xbase[(size_t)p * MP + i];
-            const int e0 = P.kslot[p * (R + 1) + t], e1 = P.kslot[p * (R + 1) + t + 1];
+            double x = CP.xbase[(size_t)p * MP + i];
+            const int e0 = CP.kslot[p * (R + 1) + t], e1 = CP.kslot[p * (R + 1) + t + 1];
 #pragma unroll TWOSD_XB_UNROLL
-            for (int e = e0; e < e1; ++e) x = fma(P.kv[(size_t)e * 64 + lane], dvl[P.kix[(size_t)e * 64 + lane]], x);
+            for (int e = e0; e < e1; ++e) x = fma(CP.kv[(size_t)e * 64 + lane], dvl[CP.kix[(size_t)e * 64 + lane]], x);
             return x;
         };
-        // warm-start basis: chosen per scenario by pool_select_kernel (0 without a pool)
-        int pb = P.npool > 1 ? __builtin_amdgcn_readfirstlane(P.pool_pick[s]) : 0;
         double xB[R];
         float wd[R];   // dual Devex weights, row 64t + lane (registers: no LDS round trip per update)
         int hb[R];
@@ -292,22 +316,42 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         // a pool start that ends non-optimal (numerics, iteration cap) is retried from the
         // primary basis, so the pool never changes which scenarios solve
         for (int attempt = 0; attempt < 2; ++attempt) {
-        brptr = P.brptr + (size_t)pb * (MP + 1);
-        bcp = P.bcp + (size_t)pb * (MP + 1);
+        brptr = CP.brptr + (size_t)pb * (MP + 1);
+        bcp = CP.bcp + (size_t)pb * (MP + 1);
 #pragma unroll
         for (int t = 0; t < R; ++t) {
             xB[t] = xb_row(pb, t);
-            hb[t] = P.hb0[(size_t)pb * MP + 64 * t + lane];
+            hb[t] = CP.hb0[(size_t)pb * MP + 64 * t + lane];
             wd[t] = 1.0f;
         }
+        {
+            // the per-slot sign masks from an opaque copy of ubm: hoisted out of the scenario loop
+            // they would be 28 loop-invariant 64-bit values, spilled and re-read every scenario
+            uint64_t ub = ubm;
+            asm volatile("" : "+v"(ub));
 #pragma unroll
-        for (int c = 0; c < C; ++c)
-            d[c] = h_flip(P.d0[(size_t)pb * 64 * C + 64 * c + lane], ((ubm >> c) & 1) << 63);
-        bmask = P.basic0[pb * 64 + lane];
+            for (int c = 0; c < C; ++c)
+                d[c] = h_flip(CP.d0[(size_t)pb * 64 * C + 64 * c + lane], ((ub >> c) & 1) << 63);
+        }
+        bmask = CP.basic0[pb * 64 + lane];
         K = 0; status = TWOSD_LP_OPTIMAL; eoff = 0;
-        nops += (long long)(P.kslot[pb * (R + 1) + R] - P.kslot[pb * (R + 1)]) * 64;
+        nops += (long long)(CP.kslot[pb * (R + 1) + R] - CP.kslot[pb * (R + 1)]) * 64;
         if (lane == 0) etaoff[0] = 0;
         h_wave_sync();
+        if (attempt == 0) {
+            // the claim has returned with the x_B loads: the next position (a range exhausted:
+            // claim from the next one, rare), then its scenario's order entry in flight
+            if (gt < G) {
+                const int g = group_of(gt);
+                const int hi = (int)(((long long)P.N * (g + 1)) / G), lo = (int)(((long long)P.N * g) / G);
+                const int t = __builtin_amdgcn_readfirstlane(__shfl(t_claim, 0));
+                if (lo + t < hi) q_nx = lo + t;
+                else { ++gt; q_nx = claim_sync(); }
+            } else {
+                q_nx = -1;
+            }
+            if (q_nx >= 0) s_nx = CP.order ? CP.order[q_nx] : q_nx;   // resolved after the pivot loop
+        }
         STAMP(0)
 
         for (;;) {
@@ -651,8 +695,12 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             h_wave_sync();
             STAMP(8)
         }
-        if (status == TWOSD_LP_OPTIMAL || pb == 0 || !P.retry) break;
-        if (lane == 0 && P.retries) atomicAdd(P.retries, 1ull);   // rare: counted for the bench line
+        if (attempt == 0 && q_nx >= 0) {   // the next scenario and its pool pick (in flight over the epilogue)
+            s_nx = __builtin_amdgcn_readfirstlane(s_nx);
+            if (CP.npool > 1) pb_nx = CP.pool_pick[s_nx];
+        }
+        if (status == TWOSD_LP_OPTIMAL || pb == 0 || !CP.retry) break;
+        if (lane == 0 && CP.retries) atomicAdd(CP.retries, 1ull);   // rare: counted for the bench line
         pb = 0;
         }   // attempt
 
@@ -663,10 +711,10 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
 #pragma unroll
             for (int t = 0; t < R; ++t) {
                 const int j = hb[t] >> 2;
-                if (hb[t] >= 0 && j < n) ob = fma(P.q[j], xB[t], ob);
+                if (hb[t] >= 0 && j < n) ob = fma(CP.q[j], xB[t], ob);
             }
             objv = wsum(ob);
-            if (P.vkey) {
+            if (CP.vkey) {
                 // key of the dual: pi_i = -d_{n+i} is the reduced cost of row i's slack, kept
                 // current in registers by every pivot (fixed E-row slacks included; unfolded here,
                 // basic slacks 0).  Components at or below key_zero (1 + max) are snapped to zero --
@@ -677,17 +725,20 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 // up to rounding noise, so their exactly recovered pi push as equal vectors
                 // (16-bit rule, dual_set.jl:24-53).  A vertex split over two keys only costs one
                 // more re-solved representative; the push dedup still merges it.
-                // d_j of row i's slack (nonbasic; basic: 0), unfolded
+                // d_j of row i's slack (nonbasic; basic: 0), unfolded (ub: opaque copy, as at the load)
+                uint64_t ub = ubm;
+                int lane = threadIdx.x & 63;   // opaque copies: the per-slot column terms of the key are
+                asm volatile("" : "+v"(ub), "+v"(lane));   // not hoisted out of the scenario loop (spills)
                 auto dk = [&](int c) -> double {
                     const int j = 64 * c + lane;
                     const bool slack = (j >= n) & (j < ncol) & (((bmask >> c) & 1) == 0);
-                    return slack ? h_flip(d[c], ((ubm >> c) & 1) << 63) : 0.0;
+                    return slack ? h_flip(d[c], ((ub >> c) & 1) << 63) : 0.0;
                 };
                 double pm = 0.0;
 #pragma unroll
                 for (int c = 0; c < C; ++c) pm = fmax(pm, fabs(dk(c)));
                 pm = wmax(pm);
-                const double zt = P.key_zero * (1.0 + pm);
+                const double zt = CP.key_zero * (1.0 + pm);
                 unsigned long long h = 0;
 #pragma unroll
                 for (int c = 0; c < C; ++c) {
@@ -702,7 +753,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 }
 #pragma unroll
                 for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o);
-                if (lane == 0) P.vkey[s] = h;
+                if (lane == 0) CP.vkey[s] = h;
             }
         }
         if constexpr (FULL) {
@@ -710,7 +761,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
 #pragma unroll
             for (int t = 0; t < R; ++t) {
                 const int j = hb[t] >> 2;
-                ut[64 * t + lane] = (hb[t] >= 0 && j < n) ? P.q[j] : 0.0;
+                ut[64 * t + lane] = (hb[t] >= 0 && j < n) ? CP.q[j] : 0.0;
             }
             h_wave_sync();
             for (int tt = K - 1; tt >= 0; --tt) {
@@ -806,14 +857,15 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         }
         }   // FULL
         if (lane == 0) {
-            P.obj[s] = objv;
-            P.status[s] = status;
-            P.iters[s] = it;
-            if (P.ops) P.ops[s] = nops;
-            if (P.etan) P.etan[s] = eoff;   // the eta-arena entries this solve wrote (12 B each)
-            if (P.npool > 1) P.pool_pick[s] = pb;   // 0 if the pool start was retried
+            CP.obj[s] = objv;
+            CP.status[s] = status;
+            CP.iters[s] = it;
+            if (CP.ops) CP.ops[s] = nops;
+            if (CP.etan) CP.etan[s] = eoff;   // the eta-arena entries this solve wrote (12 B each)
+            if (CP.npool > 1) CP.pool_pick[s] = pb;   // 0 if the pool start was retried
         }
         h_wave_sync();
+        pb_nx = __builtin_amdgcn_readfirstlane(pb_nx);
         STAMP(9)
     }
     STAMP_FLUSH
