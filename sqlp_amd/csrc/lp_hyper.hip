@@ -78,27 +78,30 @@ __device__ __forceinline__ void lds_add(double *p, double v) {
     __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 // inclusive scans over the 64 lanes: DPP row shifts within each 16-lane row (lanes shifted in
-// from outside the row read 0, bound_ctrl), then the carries of the rows before (v_readlane)
+// from outside the row read 0, bound_ctrl), then the carries of the rows before (row broadcasts)
 template <int K>
 __device__ __forceinline__ int h_row_shr(int v) {
     return __builtin_amdgcn_update_dpp(0, v, 0x110 + K, 0xF, 0xF, true);
 }
-__device__ __forceinline__ int h_scan_add(int v, int lane) {
+// the row totals carried across rows (GFX9 DPP row_bcast): lane 15 of rows 0 / 2 into rows 1 / 3,
+// then lane 31 into rows 2 and 3; rows outside the row mask read 0
+__device__ __forceinline__ int h_bcast15(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false); }
+__device__ __forceinline__ int h_bcast31(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false); }
+__device__ __forceinline__ int h_scan_add(int v) {
     v += h_row_shr<1>(v);
     v += h_row_shr<2>(v);
     v += h_row_shr<4>(v);
     v += h_row_shr<8>(v);
-    const int r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31), r2 = __builtin_amdgcn_readlane(v, 47);
-    return v + (lane >= 16 ? r0 : 0) + (lane >= 32 ? r1 : 0) + (lane >= 48 ? r2 : 0);
+    v += h_bcast15(v);
+    return v + h_bcast31(v);
 }
-__device__ __forceinline__ int h_scan_max(int v, int lane) {   // v >= 0
+__device__ __forceinline__ int h_scan_max(int v) {   // v >= 0
     v = max(v, h_row_shr<1>(v));
     v = max(v, h_row_shr<2>(v));
     v = max(v, h_row_shr<4>(v));
     v = max(v, h_row_shr<8>(v));
-    const int r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31), r2 = __builtin_amdgcn_readlane(v, 47);
-    const int c = lane >= 48 ? max(max(r0, r1), r2) : lane >= 32 ? max(r0, r1) : lane >= 16 ? r0 : 0;
-    return max(v, c);
+    v = max(v, h_bcast15(v));
+    return max(v, h_bcast31(v));
 }
 // Segmented scatter-add: lane j holds a row (entries p0 .. p0 + len - 1 of cidx / cval) and its
 // multiplier v; target[cidx[p]] += v * cval[p] over every entry of every row.  The rows are laid
@@ -110,7 +113,7 @@ __device__ __forceinline__ int h_scan_max(int v, int lane) {   // v >= 0
 // Returns the number of entries.
 __device__ __forceinline__ int h_seg_scatter(int p0, int len, double v, const int *__restrict__ cidx,
                                              const double *__restrict__ cval, double *target, int *smark, int lane) {
-    const int incl = h_scan_add(len, lane);
+    const int incl = h_scan_add(len);
     const int excl = incl - len;
     const int T = __builtin_amdgcn_readlane(incl, 63);
     const int dd = p0 - excl;   // entry e of the concatenation sits at cidx[dd_row + e]
@@ -120,7 +123,7 @@ __device__ __forceinline__ int h_seg_scatter(int p0, int len, double v, const in
         h_wave_sync();
         int mv = smark[lane];
         smark[lane] = 0;
-        mv = h_scan_max(mv, lane);
+        mv = h_scan_max(mv);
         mv = mv > carry ? mv : carry;
         carry = __builtin_amdgcn_readlane(mv, 63);
         const int j = mv > 0 ? mv - 1 : 0;
@@ -130,7 +133,12 @@ __device__ __forceinline__ int h_seg_scatter(int p0, int len, double v, const in
         const uint32_t vhi = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * j, (int)(uint32_t)(vb >> 32));
         const double vj = __longlong_as_double((long long)(((uint64_t)vhi << 32) | vlo));
         const int e = c0 + lane;
-        if (e < T) lds_add(&target[cidx[dj + e]], vj * cval[dj + e]);
+        if (e < T) {
+            int ci = cidx[dj + e];
+            double cv = cval[dj + e];
+            asm volatile("" : "+v"(ci), "+v"(cv));   // both loads in flight before either is used
+            lds_add(&target[ci], vj * cv);
+        }
     }
     return T;
 }
@@ -139,6 +147,12 @@ __device__ __forceinline__ double h_flip(double v, uint64_t signmask) {
     return __longlong_as_double(__double_as_longlong(v) ^ (long long)signmask);
 }
 
+// a wave-uniform value pinned to SGPRs
+__device__ __forceinline__ uint32_t h_uniform(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t h_uniform(uint64_t v) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+}
 // register-array element p = 64 * slot + lane (p uniform)
 template <int R>
 __device__ __forceinline__ int h_get_row_i(const int (&a)[R], int p) {
@@ -194,9 +208,6 @@ size_t hyper_lds_bytes(int R, int C, int kmax, int k) { return (size_t)kWavesPer
 #endif
 constexpr int EG = TWOSD_ETA_G;
 // unroll of the per-scenario gathers (x_B warm start, vertex recovery): loads in flight
-#ifndef TWOSD_XB_UNROLL
-#define TWOSD_XB_UNROLL 2
-#endif
 #ifndef TWOSD_REC_UNROLL
 #define TWOSD_REC_UNROLL 1
 #endif
@@ -279,6 +290,15 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
     int q_nx = claim_sync();
     int s_nx = q_nx < 0 ? -1 : (CP.order ? __builtin_amdgcn_readfirstlane(CP.order[q_nx]) : q_nx);
     int pb_nx = (s_nx >= 0 && CP.npool > 1) ? __builtin_amdgcn_readfirstlane(CP.pool_pick[s_nx]) : 0;
+    // coef_e(x) dv_e of a scenario into LDS (dvl is read by the x_B gathers only).  With k <= 128
+    // the next scenario's deltas are loaded when its index is known (after the pivot loop) and
+    // written at the end of the epilogue, so the load overlaps the epilogue
+    auto dv_fill = [&](int sn) {
+        const double *dvs = CP.dv + (size_t)sn * P.k;
+        for (int e = lane; e < P.k; e += 64) dvl[e] = CP.kcoef[e] * dvs[e];
+    };
+    const bool dv_pf = P.k <= 128;
+    if (s_nx >= 0 && dv_pf) dv_fill(s_nx);
     for (;;) {
         if (q_nx < 0) break;
         const int qpos = q_nx;
@@ -288,22 +308,14 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         int t_claim = 0;
         if (lane == 0 && gt < G) t_claim = atomicAdd(CP.queue + group_of(gt) * kQueueStride, 1);
 
-        const double *dvs = CP.dv + (size_t)s * P.k;
-        for (int e = lane; e < P.k; e += 64) dvl[e] = CP.kcoef[e] * dvs[e];   // coef_e(x) dv_e
+        if (!dv_pf) dv_fill(s);
         h_wave_sync();
         // x_B of pool basis p at this scenario: xbase_p + sum_e coef_e B_p^{-1}[i][row_e] dv_e
-        // (sliced ELL by row: independent coalesced loads, deltas gathered from LDS)
+        // (sliced ELL by row: independent coalesced loads, deltas gathered from LDS).  The slot
+        // bounds arrive in one load; the ELL columns are walked for all slots together (column u
+        // of every slot that has one), so each round trip carries up to R independent loads.
         int lnx = lane;   // opaque copy: per-lane address terms of the gathers stay inside the scenario loop
         asm volatile("" : "+v"(lnx));
-        auto xb_row = [&](int p, int t) -> double {
-            const int lane = lnx;
-            const int i = 64 * t + lane;
-            double x = CP.xbase[(size_t)p * MP + i];
-            const int e0 = CP.kslot[p * (R + 1) + t], e1 = CP.kslot[p * (R + 1) + t + 1];
-#pragma unroll TWOSD_XB_UNROLL
-            for (int e = e0; e < e1; ++e) x = fma(CP.kv[(size_t)e * 64 + lane], dvl[CP.kix[(size_t)e * 64 + lane]], x);
-            return x;
-        };
         double xB[R];
         float wd[R];   // dual Devex weights, row 64t + lane (registers: no LDS round trip per update)
         int hb[R];
@@ -316,26 +328,56 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         // a pool start that ends non-optimal (numerics, iteration cap) is retried from the
         // primary basis, so the pool never changes which scenarios solve
         for (int attempt = 0; attempt < 2; ++attempt) {
-        brptr = CP.brptr + (size_t)pb * (MP + 1);
-        bcp = CP.bcp + (size_t)pb * (MP + 1);
-#pragma unroll
-        for (int t = 0; t < R; ++t) {
-            xB[t] = xb_row(pb, t);
-            hb[t] = CP.hb0[(size_t)pb * MP + 64 * t + lane];
-            wd[t] = 1.0f;
-        }
         {
+            // one opaque argument pointer per start: the field loads below are shared within it and
+            // dead before the pivot loop
+            const auto *A = h_args();
+            const int ln = lnx;
+            brptr = A->brptr + (size_t)pb * (MP + 1);
+            bcp = A->bcp + (size_t)pb * (MP + 1);
+            const double *xb = A->xbase + (size_t)pb * MP;
+            const double *kv = A->kv;
+            const int *kix = A->kix;
+            const int ksv = ln <= R ? A->kslot[pb * (R + 1) + ln] : 0;
+            int eb[R], len[R];
+            int w = 0;
+#pragma unroll
+            for (int t = 0; t < R; ++t) {
+                eb[t] = __builtin_amdgcn_readlane(ksv, t);
+                len[t] = __builtin_amdgcn_readlane(ksv, t + 1) - eb[t];
+                w = len[t] > w ? len[t] : w;
+                xB[t] = xb[64 * t + ln];
+                hb[t] = A->hb0[(size_t)pb * MP + 64 * t + ln];
+                wd[t] = 1.0f;
+            }
+            nops += (long long)(__builtin_amdgcn_readlane(ksv, R) - eb[0]) * 64;
+            // column u of every slot, in increasing u per row: the same fma order as a per-row walk
+            for (int u = 0; u < w; ++u) {
+                double kvv[R];
+                int kiv[R];
+#pragma unroll
+                for (int t = 0; t < R; ++t) {
+                    kvv[t] = 0.0;
+                    kiv[t] = 0;
+                    if (u < len[t]) {
+                        kvv[t] = kv[(size_t)(eb[t] + u) * 64 + ln];
+                        kiv[t] = kix[(size_t)(eb[t] + u) * 64 + ln];
+                    }
+                }
+#pragma unroll
+                for (int t = 0; t < R; ++t)
+                    if (u < len[t]) xB[t] = fma(kvv[t], dvl[kiv[t]], xB[t]);
+            }
             // the per-slot sign masks from an opaque copy of ubm: hoisted out of the scenario loop
             // they would be 28 loop-invariant 64-bit values, spilled and re-read every scenario
             uint64_t ub = ubm;
             asm volatile("" : "+v"(ub));
 #pragma unroll
             for (int c = 0; c < C; ++c)
-                d[c] = h_flip(CP.d0[(size_t)pb * 64 * C + 64 * c + lane], ((ub >> c) & 1) << 63);
+                d[c] = h_flip(A->d0[(size_t)pb * 64 * C + 64 * c + ln], ((ub >> c) & 1) << 63);
+            bmask = A->basic0[pb * 64 + ln];
         }
-        bmask = CP.basic0[pb * 64 + lane];
         K = 0; status = TWOSD_LP_OPTIMAL; eoff = 0;
-        nops += (long long)(CP.kslot[pb * (R + 1) + R] - CP.kslot[pb * (R + 1)]) * 64;
         if (lane == 0) etaoff[0] = 0;
         h_wave_sync();
         if (attempt == 0) {
@@ -366,7 +408,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 // padding rows (hb < 0) never
                 const int bt = hb[t] & 3;
                 const bool inf = (hb[t] >= 0) & (((xB[t] < -HTOL_P) & (bt != BT_G)) | ((xB[t] > HTOL_P) & ((bt & 1) != 0)));
-                if (inf) {
+                if (__builtin_amdgcn_ballot_w64(inf) != 0 && inf) {   // most slots hold no infeasible row
                     const double dl = xB[t];
                     const double num = dl * dl, den = (double)wd[t];
                     if (num * bden > bnum * den) { bnum = num; bden = den; br = 64 * t + lane; bdel = dl; }
@@ -492,8 +534,11 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             // fractions within the lane (nu * de_best < nu_best * de), one division per lane
             const uint64_t sgm = delta > 0 ? 0ull : (1ull << 63);   // a = sg alpha
             const Mask cand = (Mask)~(bmask | fixedm);
+            // A slot (64 columns) with no eligible column is skipped after its test (wave-uniform
+            // branch), and the slots with any nonzero alpha' are noted for the dual update: on
+            // storm ~9 of the 28 slots hold an eligible column and ~18 a nonzero alpha' per pivot.
             double bnu = INFINITY, bde = 1.0;
-            Mask elm = 0;
+            Mask elm = 0, sel = 0, snz = 0;
             double apf = alpha[lane];
 #pragma unroll
             for (int c = 0; c < C; ++c) {
@@ -501,11 +546,16 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 if (c + 1 < C) apf = alpha[64 * (c + 1) + lane];
                 const double a = h_flip(av, sgm);
                 const bool el = (((cand >> c) & 1) != 0) & (a > HTOL_PIV);
-                const double nu = d[c] + HTOL_D;
-                const bool better = el & (nu * bde < bnu * a);
-                bnu = better ? nu : bnu;
-                bde = better ? a : bde;
-                elm |= (Mask)el << c;
+                // folded now (readfirstlane: an SGPR value): deferred, the 28 ballots stay live and spill
+                snz = h_uniform(snz | ((Mask)(__builtin_amdgcn_ballot_w64(av != 0.0) != 0) << c));
+                if (__builtin_amdgcn_ballot_w64(el) != 0) {
+                    sel |= (Mask)1 << c;
+                    const double nu = d[c] + HTOL_D;
+                    const bool better = el & (nu * bde < bnu * a);
+                    bnu = better ? nu : bnu;
+                    bde = better ? a : bde;
+                    elm |= (Mask)el << c;
+                }
                 // one slot at a time: unscheduled, the 28 slots' LDS reads are hoisted together and
                 // the register pressure spills d[] for the whole pivot loop
                 __builtin_amdgcn_sched_barrier(0);
@@ -527,11 +577,13 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             for (int c = 0; c < C; ++c) {
                 const double av = apf;
                 if (c + 1 < C) apf = alpha[64 * (c + 1) + lane];
-                const double a = h_flip(av, sgm);
-                const bool ok = (((elm >> c) & 1) != 0) & (d[c] <= thmax * a) & (a > bA);
-                bA = ok ? a : bA;
-                bD = ok ? d[c] : bD;
-                bq = ok ? 64 * c + lane : bq;
+                if ((sel >> c) & 1) {
+                    const double a = h_flip(av, sgm);
+                    const bool ok = (((elm >> c) & 1) != 0) & (d[c] <= thmax * a) & (a > bA);
+                    bA = ok ? a : bA;
+                    bD = ok ? d[c] : bD;
+                    bq = ok ? 64 * c + lane : bq;
+                }
                 __builtin_amdgcn_sched_barrier(0);
             }
             const ArgBest1 eq = warg_max1(bA, bq, bD);
@@ -545,14 +597,17 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 break;
             }
             const double thetaD = eq.p0 / eq.key;   // d'_q / a'_q = d_q / a_q
-            // d'_j -= thetaD a'_j over every slot, alpha back to zero (ut / rho all zero after)
+            // d'_j -= thetaD a'_j over the slots with a nonzero alpha', alpha back to zero (ut / rho
+            // all zero after); an all-zero slot would leave d' unchanged but for the sign of a zero
             apf = alpha[lane];
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 const double av = apf;
                 if (c + 1 < C) apf = alpha[64 * (c + 1) + lane];
-                alpha[64 * c + lane] = 0.0;
-                d[c] = fma(-thetaD, h_flip(av, sgm), d[c]);
+                if ((snz >> c) & 1) {
+                    alpha[64 * c + lane] = 0.0;
+                    d[c] = fma(-thetaD, h_flip(av, sgm), d[c]);
+                }
                 __builtin_amdgcn_sched_barrier(0);
             }
             h_wave_sync();
@@ -673,10 +728,11 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 const int ls = leaving >> 6, qs = q >> 6;
                 const double dlv = (delta > 0) == ((lh & 3) == BT_G) ? thetaD : -thetaD;
                 const bool lme = lane == (leaving & 63), qme = lane == (q & 63);
+                // one slot each (ls, qs uniform): scalar branches, two selects in all
 #pragma unroll
                 for (int c = 0; c < C; ++c) {
-                    if (lme && c == ls) d[c] = dlv;
-                    if (qme && c == qs) d[c] = 0.0;
+                    if (c == ls) d[c] = lme ? dlv : d[c];
+                    if (c == qs) d[c] = qme ? 0.0 : d[c];
                 }
                 if (lme) bmask &= ~(1ull << ls);
                 if (qme) bmask |= 1ull << qs;
@@ -703,15 +759,31 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         if (lane == 0 && CP.retries) atomicAdd(CP.retries, 1ull);   // rare: counted for the bench line
         pb = 0;
         }   // attempt
+        // the next scenario's coef_e and dv_e, e = lane, lane + 64 (multiplied at the LDS write)
+        double dvn0 = 0.0, dvn1 = 0.0, kcn0 = 0.0, kcn1 = 0.0;
+        if (dv_pf && q_nx >= 0) {
+            const auto *A = h_args();
+            const double *dvs = A->dv + (size_t)s_nx * P.k;
+            if (lane < P.k) { dvn0 = dvs[lane]; kcn0 = A->kcoef[lane]; }
+            if (lane + 64 < P.k) { dvn1 = dvs[lane + 64]; kcn1 = A->kcoef[lane + 64]; }
+        }
 
         // ---- objective, dual-vertex key, vertex recovery pi = c_B' B^{-1}
         double objv = NAN;
         if (status == TWOSD_LP_OPTIMAL) {
+            // the q_j of all slots loaded together (one pointer, clamped indices), summed in slot order
+            const double *qc = CP.q;
+            double qv[R];
+#pragma unroll
+            for (int t = 0; t < R; ++t) {
+                const int j = hb[t] >> 2;
+                qv[t] = qc[(hb[t] >= 0 && j < n) ? j : 0];
+            }
             double ob = 0.0;
 #pragma unroll
             for (int t = 0; t < R; ++t) {
                 const int j = hb[t] >> 2;
-                if (hb[t] >= 0 && j < n) ob = fma(CP.q[j], xB[t], ob);
+                ob = (hb[t] >= 0 && j < n) ? fma(qv[t], xB[t], ob) : ob;
             }
             objv = wsum(ob);
             if (CP.vkey) {
@@ -758,10 +830,13 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         }
         if constexpr (FULL) {
         if (status == TWOSD_LP_OPTIMAL && (P.pi || P.y)) {
+            const double *qc = CP.q;
 #pragma unroll
             for (int t = 0; t < R; ++t) {
                 const int j = hb[t] >> 2;
-                ut[64 * t + lane] = (hb[t] >= 0 && j < n) ? CP.q[j] : 0.0;
+                const bool bq = hb[t] >= 0 && j < n;
+                const double qj = qc[bq ? j : 0];
+                ut[64 * t + lane] = bq ? qj : 0.0;
             }
             h_wave_sync();
             for (int tt = K - 1; tt >= 0; --tt) {
@@ -863,6 +938,10 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             if (CP.ops) CP.ops[s] = nops;
             if (CP.etan) CP.etan[s] = eoff;   // the eta-arena entries this solve wrote (12 B each)
             if (CP.npool > 1) CP.pool_pick[s] = pb;   // 0 if the pool start was retried
+        }
+        if (dv_pf && q_nx >= 0) {
+            if (lane < P.k) dvl[lane] = kcn0 * dvn0;
+            if (lane + 64 < P.k) dvl[lane + 64] = kcn1 * dvn1;
         }
         h_wave_sync();
         pb_nx = __builtin_amdgcn_readfirstlane(pb_nx);

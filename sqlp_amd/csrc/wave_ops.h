@@ -107,21 +107,48 @@ __device__ __forceinline__ void arg_step1(double &key, int &idx, double &p0) {
     const double a2 = dpp_d<CTRL>(p0);
     if (k2 > key || (k2 == key && i2 < idx)) { key = k2; idx = i2; p0 = a2; }
 }
+// row results carried across rows (GFX9 DPP row_bcast:15 into rows 1 / 3, row_bcast:31 into rows
+// 2 / 3; rows outside the row mask keep their own value): lane 63 ends with the wave result
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_bcast_d(double v) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp((int)(uint32_t)u, (int)(uint32_t)u, CTRL, ROWS, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(uint32_t)(u >> 32), (int)(uint32_t)(u >> 32), CTRL, ROWS, 0xF, false);
+    return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+__device__ __forceinline__ int dpp_bcast_min_i(int v) {
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x142, 0xA, 0xF, false));
+    return min(v, __builtin_amdgcn_update_dpp(v, v, 0x143, 0xC, 0xF, false));
+}
+// maximum over the 64 lanes (uniform)
+__device__ __forceinline__ double wmax_any(double v) {
+    v = fmax(v, dpp_d<kDppXor1>(v));
+    v = fmax(v, dpp_d<kDppXor2>(v));
+    v = fmax(v, dpp_d<kDppHalfMirror>(v));
+    v = fmax(v, dpp_d<kDppMirror>(v));
+    v = fmax(v, dpp_bcast_d<0x142, 0xA>(v));
+    v = fmax(v, dpp_bcast_d<0x143, 0xC>(v));
+    return readlane_dbl(v, 63);
+}
+// The same selection as the pairwise tree (largest key, ties: smallest idx) from the maximum:
+// the lanes holding it by ballot, the lowest such lane, and only when several lanes hold it
+// (rare but for the all-zero keys of a finished solve) a minimum over their idx.
 __device__ __forceinline__ ArgBest1 warg_max1(double key, int idx, double p0) {
-    arg_step1<kDppXor1>(key, idx, p0);
-    arg_step1<kDppXor2>(key, idx, p0);
-    arg_step1<kDppHalfMirror>(key, idx, p0);
-    arg_step1<kDppMirror>(key, idx, p0);
-    ArgBest1 b{readlane_dbl(key, 0), __builtin_amdgcn_readlane(idx, 0), readlane_dbl(p0, 0)};
-#pragma unroll
-    for (int l = 16; l < 64; l += 16) {
-        const double k2 = readlane_dbl(key, l);
-        const int i2 = __builtin_amdgcn_readlane(idx, l);
-        if (k2 > b.key || (k2 == b.key && i2 < b.idx)) {
-            b.key = k2; b.idx = i2; b.p0 = readlane_dbl(p0, l);
-        }
+    const double M = wmax_any(key);
+    const uint64_t hit = __builtin_amdgcn_ballot_w64(key == M);
+    int wl = hit ? (int)__builtin_ctzll(hit) : 0;   // (no hit only for NaN keys)
+    int wi = __builtin_amdgcn_readlane(idx, wl);
+    if (__builtin_popcountll(hit) > 1) {
+        int im = key == M ? idx : 0x7fffffff;
+        im = min(im, dpp_i<kDppXor1>(im));   // quad / mirror moves read within the row: old unused
+        im = min(im, dpp_i<kDppXor2>(im));
+        im = min(im, dpp_i<kDppHalfMirror>(im));
+        im = min(im, dpp_i<kDppMirror>(im));
+        wi = __builtin_amdgcn_readlane(dpp_bcast_min_i(im), 63);
+        const uint64_t h2 = __builtin_amdgcn_ballot_w64((key == M) & (idx == wi));
+        wl = h2 ? (int)__builtin_ctzll(h2) : 0;
     }
-    return b;
+    return ArgBest1{M, wi, readlane_dbl(p0, wl)};
 }
 
 }  // namespace twosd

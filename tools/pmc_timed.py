@@ -17,6 +17,7 @@ and the rest by a least-squares fit over the timed steps.
 """
 import csv
 import glob
+import gzip
 import json
 import os
 import sys
@@ -35,9 +36,10 @@ def short(name):
 
 
 def load_pass(path):
-    """dispatch id -> {name, counters, ms}"""
+    """dispatch id -> {name, counters, ms} (raw counter_collection.csv or prof_reduce.py's .csv.gz)"""
     disp = {}
-    for r in csv.DictReader(open(path)):
+    f = gzip.open(path, "rt", newline="") if path.endswith(".gz") else open(path, newline="")
+    for r in csv.DictReader(f):
         d = int(r["Dispatch_Id"])
         e = disp.setdefault(d, {"name": r["Kernel_Name"], "c": {}, "ms": (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6,
                                 "scratch": int(float(r["Scratch_Size"])), "vgpr": int(float(r["VGPR_Count"]))})
@@ -74,13 +76,16 @@ def main():
     per = defaultdict(lambda: defaultdict(lambda: defaultdict(list)))   # kernel -> x -> counter -> values
     meta = {}
     bench_lines = {}
-    for pdir in sorted(glob.glob(os.path.join(src, "pmc_*"))):
-        if not os.path.isdir(pdir):
-            continue
-        tag = os.path.basename(pdir)
-        fs = glob.glob(os.path.join(pdir, "**", "*counter_collection.csv"), recursive=True)
-        if not fs:
-            continue
+    passes = {}
+    for pdir in glob.glob(os.path.join(src, "pmc_*")):
+        if os.path.isdir(pdir):
+            fs = glob.glob(os.path.join(pdir, "**", "*counter_collection.csv"), recursive=True)
+            if fs:
+                passes[os.path.basename(pdir)] = fs[0]
+        elif pdir.endswith("_counters.csv.gz"):
+            passes[os.path.basename(pdir)[:-len("_counters.csv.gz")]] = pdir
+    for tag, path in sorted(passes.items()):
+        fs = [path]
         disp = load_pass(fs[0])
         steps = timed_steps(disp, K)
         for i, st in enumerate(steps):

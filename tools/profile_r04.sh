@@ -2,7 +2,7 @@
 # Round-4 profile session on the GPU box: the driver's command (bench.py --gpus 1 --steps 20
 # --warmup 5) under rocprofv3 -- a kernel-trace/stats run and separate PMC passes (HBM bytes:
 # FETCH_SIZE, WRITE_SIZE; fp64 MFMA; two SQ instruction / wait passes) -- each step under its own
-# time limit; tools/pmc_timed.py then keeps the timed steps' launches per x point.
+# time limit, reduced on the box by tools/prof_reduce.py; tools/pmc_timed.py then keeps the timed steps' launches per x point.
 # Usage (repo root, GPU box): bash tools/profile_r04.sh <tag>
 set -u
 TAG=${1:-r04}
@@ -14,8 +14,10 @@ run() {   # run <name> <seconds> <rocprofv3 args...>
     local name=$1 secs=$2; shift 2
     timeout -k 10 $secs rocprofv3 "$@" -d $OUT/$name -o run --output-format csv -- python3 bench.py $ARGS > $OUT/${name}_bench.json 2> $OUT/$name.err
     local rc=$?
-    echo "$name rc=$rc"
+    echo "$name rc=$rc $(tail -c 300 $OUT/${name}_bench.json | tr -d '\n' | cut -c1-200)"
+    tail -3 $OUT/$name.err
     [ $rc -eq 0 ] || exit $rc
+    python3 tools/prof_reduce.py $OUT/$name $OUT/$name   # raw per-dispatch CSVs exceed the copy-back limit
 }
 run trace 420 --kernel-trace --stats
 run pmc_fetch 420 --pmc FETCH_SIZE
