@@ -101,8 +101,8 @@ int twosd_pool_build(twosd_ctx *ctx, int epi, const double *x, int first, int co
 /* Two-level pool selection: level 1 over pool[0, level1), level 2 over the ncand bases
  * that a flat selection over the whole pool picks most often for the training scenarios
  * [first, first+count) of epi at x sharing the level-1 pick.  Cuts the selection cost of a
- * large pool to about that of its first level1 bases.  level1 = 0: flat selection.  Reset
- * by any change of the pool. */
+ * large pool to about that of its first level1 bases.  level1 = 0: flat selection;
+ * ncand <= 1024.  Reset by any change of the pool. */
 int twosd_pool_build_candidates(twosd_ctx *ctx, int epi, const double *x, int first, int count, int level1,
                                 int ncand);
 /* Rebuild the pool at x: solve the training scenarios [first, first+count) of epi at x from

@@ -1593,7 +1593,7 @@ extern "C" int twosd_pool_candidate_picks(twosd_ctx *c, int epi, const double *x
 extern "C" int twosd_pool_set_candidates(twosd_ctx *c, int level1, int ncand, int n, const int *p1, const int *pf) {
     if (!c || !c->has_basis) return fail(TWOSD_E_STATE, "pool_set_candidates: no primary basis");
     const int P = (int)c->pool.size();
-    if (level1 < 1 || level1 >= P || ncand < 1 || ncand > 256 || n < 0 || (n > 0 && (!p1 || !pf)))
+    if (level1 < 1 || level1 >= P || ncand < 1 || ncand > 1024 || n < 0 || (n > 0 && (!p1 || !pf)))
         return fail(TWOSD_E_ARG, "pool_set_candidates: bad arguments");
     for (int s = 0; s < n; ++s)
         if (p1[s] < 0 || p1[s] >= P || pf[s] < 0 || pf[s] >= P) return fail(TWOSD_E_ARG, "pool_set_candidates: pick outside the pool");
@@ -1607,7 +1607,7 @@ extern "C" int twosd_pool_build_candidates(twosd_ctx *c, int epi, const double *
     if (epi < 0 || epi >= (int)c->epis.size()) return fail(TWOSD_E_ARG, "pool_build_candidates: epigraph %d does not exist", epi);
     const EpiDevice &E = c->epis[epi];
     const int P = (int)c->pool.size();
-    if (first < 0 || count < 1 || first + count > E.count || level1 < 0 || ncand < 0 || ncand > 256 || (c->n1 > 0 && !x))
+    if (first < 0 || count < 1 || first + count > E.count || level1 < 0 || ncand < 0 || ncand > 1024 || (c->n1 > 0 && !x))
         return fail(TWOSD_E_ARG, "pool_build_candidates: bad arguments");
     c->pool_l1 = c->pool_ncand = 0;
     if (level1 == 0 || ncand == 0 || level1 >= P || P < 2 || c->CH <= 0) return TWOSD_OK;   // flat selection

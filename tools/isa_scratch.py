@@ -2,7 +2,8 @@
 (default storm: R = 9 row slots, C = 28 column slots) and count the scratch loads / stores of
 every loop (a back edge: a branch to an earlier label), plus the kernel's resource usage.
 The pivot loop is the largest loop inside the per-scenario loop.
-Usage: python tools/isa_scratch.py [R] [C]   (CPU only: hipcc cross-compiles)"""
+Usage: python tools/isa_scratch.py [R] [C] [full]   (CPU only: hipcc cross-compiles; full = 1: the
+instantiation with the recovery / eta-file epilogue)"""
 import os
 import re
 import subprocess
@@ -15,6 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main():
     R = int(sys.argv[1]) if len(sys.argv) > 1 else 9
     C = int(sys.argv[2]) if len(sys.argv) > 2 else 28
+    FULL = int(sys.argv[3]) if len(sys.argv) > 3 else 0
     src = os.path.join(ROOT, "sqlp_amd", "csrc", "lp_hyper.hip")
     with tempfile.TemporaryDirectory() as d:
         asm = os.path.join(d, "lp.s")
@@ -22,7 +24,7 @@ def main():
                             "-I" + os.path.join(ROOT, "include"), "-Rpass-analysis=kernel-resource-usage", src, "-o", asm],
                            capture_output=True, text=True)
         text = open(asm).read()
-    sym = f"_ZN5twosd15lp_hyper_kernelILi{R}ELi{C}EEEvNS_11HyperParamsE"
+    sym = f"_ZN5twosd15lp_hyper_kernelILi{R}ELi{C}ELb{FULL}EEEvNS_11HyperParamsE"
     usage = []
     lines_r = r.stderr.splitlines()
     for i, l in enumerate(lines_r):
@@ -49,7 +51,7 @@ def main():
     def ninstr(a, b):
         return sum(1 for l in lines[a:b + 1] if l.startswith("\t") and not l.startswith(("\t.", "\t;")))
 
-    print(f"lp_hyper_kernel<{R}, {C}>: " + "; ".join(usage))
+    print(f"lp_hyper_kernel<{R}, {C}, {'true' if FULL else 'false'}>: " + "; ".join(usage))
     print(f"whole kernel: {ninstr(0, len(lines))} instructions, scratch stores {cnt(0, len(lines), 'scratch_store')}, "
           f"loads {cnt(0, len(lines), 'scratch_load')}")
     scen = loops[0]
