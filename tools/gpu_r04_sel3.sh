@@ -10,3 +10,7 @@ bash tools/gpu_session.sh gpurun_out/sel3 \
   "b|150|python bench.py $A --pool-level1 16 --pool-cands 384 > gpurun_out/sel3/storm_l16c384.json" \
   "sd|200|python bench.py $S > gpurun_out/sel3/ssn_l128c160.json" \
   "sa|200|python bench.py $S --pool-level1 64 --pool-cands 224 > gpurun_out/sel3/ssn_l64c224.json"
+bash tools/gpu_session.sh gpurun_out/sel3 \
+  "ab_main|120|python tools/main_pivots.py" \
+  "ab_eg3|120|TWOSD_LIB=eg3 python tools/main_pivots.py" \
+  "ab_eg4|120|TWOSD_LIB=eg4 python tools/main_pivots.py"

@@ -5,7 +5,7 @@ keyed solve_push), at each of the bench's x points.  Run with TWOSD_LIB=stamps
 schedule, so only the shares and the cycles per scenario are meaningful, never the absolute
 kernel time.
 
-usage: TWOSD_LIB=stamps python tools/lp_phases_bench.py [N] [pool] [train]
+usage: TWOSD_LIB=stamps python tools/lp_phases_bench.py [N] [pool] [train] [instance (storm)]
 """
 import ctypes as C
 import json
@@ -27,12 +27,13 @@ def main():
     N = int(sys.argv[1]) if len(sys.argv) > 1 else 250000
     P = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
     T = int(sys.argv[3]) if len(sys.argv) > 3 else 4 * P
+    inst = sys.argv[4] if len(sys.argv) > 4 else "storm"
     seed = 20250219
-    d = os.path.join(ROOT, "data", "smps", "storm")
-    cor, tim, sto = smps.load_smps(d, "storm")
+    d = os.path.join(ROOT, "data", "smps", inst)
+    cor, tim, sto = smps.load_smps(d, inst)
     sp2 = smps.get_smps_stage_template(cor, tim, 2)
     with open(os.path.join(ROOT, "tests", "golden", "ev_x.json")) as f:
-        x0 = np.array(json.load(f)["storm"]["x"])
+        x0 = np.array(json.load(f)[inst]["x"])
     positions = list(sto.indep.keys())
     its = [0, 4, 12, 30]
     xs = bench.sd_points(cor, tim, sp2, sto, positions, x0, its, seed + 7, torch.device("cuda", 0))
