@@ -254,7 +254,7 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_kslot); dfree(c->d_kix); dfree(c->d_kv); dfree(c->d_kcoef); c->k_valid = false;
     dfree(c->d_sel_end); dfree(c->d_kp); dfree(c->d_ke); dfree(c->d_kraw); dfree(c->d_xaux); c->xaux_cap = 0; c->sel_cap_total = 0;
     dfree(c->d_d0); dfree(c->d_eidx); dfree(c->d_evals); dfree(c->d_stamps);
-    dfree(c->d_wr_col); dfree(c->d_wr_val); dfree(c->d_wr_ocol); dfree(c->d_wr_oval); dfree(c->d_wcp); dfree(c->d_wcc); dfree(c->d_wcv); dfree(c->d_bcp); dfree(c->d_bci); dfree(c->d_bcv);
+    dfree(c->d_wcp); dfree(c->d_wcc); dfree(c->d_wcv); dfree(c->d_bcp); dfree(c->d_bci); dfree(c->d_bcv);
     dfree(c->d_brptr); dfree(c->d_brcol); dfree(c->d_brval);
     c->earena_slots = 0; c->earena_cap = 0;
     for (auto &e : c->epis) { dfree(e.d_dv); dfree(e.d_w); }
@@ -365,31 +365,10 @@ extern "C" int twosd_set_template(twosd_ctx *c, int m2, int n1, int n2, const in
     HIPCHK(hipMemcpy(c->d_btype, bt.data(), n2 + m2, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d_fixedmask, fixedm.data(), sizeof(uint64_t) * 64, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d_ubmask, ubm.data(), sizeof(uint64_t) * 64, hipMemcpyHostToDevice));
-    if (c->CH > 0) {   // W by rows (row-ELL, columns ascending) for the row-wise pricing scatter
+    if (c->CH > 0) {   // W by rows (CSR, columns ascending) for the row-wise pricing scatter
         std::vector<std::vector<std::pair<int, double>>> rows(m2);
         for (int j = 0; j < n2; ++j)
             for (int p = L.colptr[j]; p < L.colptr[j + 1]; ++p) rows[L.rowidx[p]].push_back({j, L.val[p]});
-        int wr = 1;
-        for (auto &r : rows) wr = std::max(wr, (int)r.size());
-        wr = std::min(wr, 64);
-        std::vector<int> wc((size_t)m2 * wr, -1), oc;
-        std::vector<double> wv((size_t)m2 * wr, 0.0), ov;
-        for (int i = 0; i < m2; ++i) {
-            const int len = (int)rows[i].size();
-            const int inl = len > 64 ? 63 : len;   // a row longer than 64: 63 inline + marker
-            for (int e = 0; e < inl; ++e) {
-                wc[(size_t)i * wr + e] = rows[i][e].first;
-                wv[(size_t)i * wr + e] = rows[i][e].second;
-            }
-            if (len > 64) {
-                wc[(size_t)i * wr + 63] = -2 - (int)oc.size();
-                wv[(size_t)i * wr + 63] = (double)(len - 63);
-                for (int e = 63; e < len; ++e) { oc.push_back(rows[i][e].first); ov.push_back(rows[i][e].second); }
-            }
-        }
-        if ((rc = upload(&c->d_wr_ocol, oc)) || (rc = upload(&c->d_wr_oval, ov))) return rc;
-        c->wr_width = wr;
-        if ((rc = upload(&c->d_wr_col, wc)) || (rc = upload(&c->d_wr_val, wv))) return rc;
         std::vector<int> cp(m2 + 1, 0), cc;
         std::vector<double> cv;
         for (int i = 0; i < m2; ++i) {
@@ -2291,8 +2270,6 @@ int twosd::run_lp_ex(twosd_ctx *c, const double *x, const double *d_dv, int N, c
         H.kcap = o.kcap > 0 ? std::min(o.kcap, kmax) : kmax;
         H.retry = o.kcap > 0 ? 0 : 1;
         H.colptr = c->d_colptr; H.rowidx = c->d_rowidx; H.val = c->d_val; H.q = c->d_q; H.btype = c->d_btype;
-        H.wr_width = c->wr_width; H.wr_col = c->d_wr_col; H.wr_val = c->d_wr_val;
-        H.wr_ocol = c->d_wr_ocol; H.wr_oval = c->d_wr_oval;
         H.wcp = c->d_wcp; H.wcc = c->d_wcc; H.wcv = c->d_wcv;
         H.bcp = c->d_bcp; H.bci = c->d_bci; H.bcv = c->d_bcv;
         H.brptr = c->d_brptr; H.brcol = c->d_brcol; H.brval = c->d_brval;

@@ -396,6 +396,27 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         }
         STAMP(0)
 
+        // the first-64 entries of etas t0, t0 + dir, ..., t0 + (EG - 1) dir that exist (0 <= t < K).
+        // The loads are issued unconditionally (entry 0 of the arena where there is none), so every
+        // group issues the same number of them and the wait for a group prefetched one step earlier
+        // leaves the newer group's loads in flight
+        auto eta_group = [&](int t0, int dir, int (&gi)[EG], double (&gv)[EG], int (&gn)[EG], int (&go)[EG]) {
+#pragma unroll
+            for (int g = 0; g < EG; ++g) {
+                const int tt = t0 + dir * g;
+                const bool ok = (tt >= 0) & (tt < K);
+                const int tc = ok ? tt : 0;
+                const int o0 = etaoff[tc], o1 = etaoff[tc + 1];
+                go[g] = ok ? o0 : 0;
+                gn[g] = ok ? o1 - o0 : 0;
+                const bool mine = lane < gn[g];
+                const int at = mine ? go[g] + lane : 0;
+                const int ix = eidx[at];
+                const double vx = evals[at];
+                gi[g] = mine ? ix : 0;
+                gv[g] = mine ? vx : 0.0;
+            }
+        };
         for (;;) {
             // ---- 1. leaving row (dual Devex: max infeas^2 / w, lowest row on ties)
             // within the lane the rows are compared as fractions (dl^2 * w_best > best_num * w:
@@ -424,31 +445,41 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             // ---- 2. BTRAN: u = e_r' E_K..E_1 (u dense in LDS), rho = u' B0^{-1}
             if (lane == (r & 63)) ut[r] = 1.0;
             h_wave_sync();
-            // etas in groups of EG: the group's entries (first 64 of each) are loaded together,
-            // so one memory round trip serves EG sequential steps
-            for (int tg = K - 1; tg >= 0; tg -= EG) {
-                int gi[EG], gn[EG], go[EG];
-                double gv[EG];
+            // etas in groups of EG: the group's entries (first 64 of each) are loaded together, and
+            // the next group's loads are issued before this group is applied (two register sets,
+            // ping-pong), so the memory round trips overlap the sequential steps
+            {
+                auto apply = [&](int tg, const int (&gi)[EG], const double (&gv)[EG], const int (&gn)[EG], const int (&go)[EG]) {
 #pragma unroll
-                for (int g = 0; g < EG; ++g) {
-                    const int tt = tg - g;
-                    gi[g] = 0; gv[g] = 0.0; gn[g] = 0; go[g] = 0;
-                    if (tt >= 0) {
-                        go[g] = etaoff[tt];
-                        gn[g] = etaoff[tt + 1] - go[g];
-                        if (lane < gn[g]) { gi[g] = eidx[go[g] + lane]; gv[g] = evals[go[g] + lane]; }
+                    for (int g = 0; g < EG; ++g) {
+                        const int tt = tg - g;
+                        if (tt < 0) break;
+                        double acc = gv[g] != 0.0 ? ut[gi[g]] * gv[g] : 0.0;
+                        for (int e = 64 + lane; e < gn[g]; e += 64) acc = fma(ut[eidx[go[g] + e]], evals[go[g] + e], acc);
+                        acc = wsum(acc);
+                        nops += gn[g];
+                        if (lane == 0) ut[etap[tt]] = acc;
+                        h_wave_sync();
                     }
-                }
-#pragma unroll
-                for (int g = 0; g < EG; ++g) {
-                    const int tt = tg - g;
-                    if (tt < 0) break;
-                    double acc = gv[g] != 0.0 ? ut[gi[g]] * gv[g] : 0.0;
-                    for (int e = 64 + lane; e < gn[g]; e += 64) acc = fma(ut[eidx[go[g] + e]], evals[go[g] + e], acc);
-                    acc = wsum(acc);
-                    nops += gn[g];
-                    if (lane == 0) ut[etap[tt]] = acc;
-                    h_wave_sync();
+                };
+                int ai[EG], an[EG], ao[EG], bi[EG], bn[EG], bo[EG];
+                double av[EG], bv[EG];
+                if (K <= 2 * EG) {   // short file (storm: most solves): one group in flight at a time
+                    for (int tg = K - 1; tg >= 0; tg -= EG) {
+                        eta_group(tg, -1, ai, av, an, ao);
+                        apply(tg, ai, av, an, ao);
+                    }
+                } else {
+                    eta_group(K - 1, -1, ai, av, an, ao);
+                    for (int tg = K - 1; tg >= 0;) {
+                        eta_group(tg - EG, -1, bi, bv, bn, bo);
+                        apply(tg, ai, av, an, ao);
+                        tg -= EG;
+                        if (tg < 0) break;
+                        eta_group(tg - EG, -1, ai, av, an, ao);
+                        apply(tg, bi, bv, bn, bo);
+                        tg -= EG;
+                    }
                 }
             }
             STAMP(2)
@@ -480,7 +511,8 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
 
             // ---- 3. pricing: alpha'_j = s_j rho' a_j for every column as a scatter over the
             // nonzeros of rho (~6 % of the rows on storm).  alpha lives in LDS over the ut/rho space
-            // (both zero here once rho is in registers).
+            // (both zero here once rho is in registers).  (A column-wise variant -- dot products over
+            // [W I]'s columns -- measured no faster even on ssn's denser rho.)
             double rv[R];
 #pragma unroll
             for (int t = 0; t < R; ++t) rv[t] = rho[64 * t + lane];
@@ -632,40 +664,49 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 }
             }
             h_wave_sync();
-            for (int tg = 0; tg < K; tg += EG) {
-                int gi[EG], gn[EG], go[EG];
-                double gv[EG];
+            {
+                auto apply = [&](int tg, const int (&gi)[EG], const double (&gv)[EG], const int (&gn)[EG], const int (&go)[EG]) {
 #pragma unroll
-                for (int g = 0; g < EG; ++g) {
-                    const int tt = tg + g;
-                    gi[g] = 0; gv[g] = 0.0; gn[g] = 0; go[g] = 0;
-                    if (tt < K) {
-                        go[g] = etaoff[tt];
-                        gn[g] = etaoff[tt + 1] - go[g];
-                        if (lane < gn[g]) { gi[g] = eidx[go[g] + lane]; gv[g] = evals[go[g] + lane]; }
-                    }
-                }
-#pragma unroll
-                for (int g = 0; g < EG; ++g) {
-                    const int tt = tg + g;
-                    if (tt >= K) break;
-                    const int p = etap[tt];
-                    const double vp = ut[p];
-                    if (vp != 0.0) {
-                        // the pivot row p is replaced, the others accumulate (distinct rows)
-                        if (lane < gn[g]) {
-                            if (gi[g] == p) ut[p] = gv[g] * vp;
-                            else lds_add(&ut[gi[g]], gv[g] * vp);
+                    for (int g = 0; g < EG; ++g) {
+                        const int tt = tg + g;
+                        if (tt >= K) break;
+                        const int p = etap[tt];
+                        const double vp = ut[p];
+                        if (vp != 0.0) {
+                            // the pivot row p is replaced, the others accumulate (distinct rows)
+                            if (lane < gn[g]) {
+                                if (gi[g] == p) ut[p] = gv[g] * vp;
+                                else lds_add(&ut[gi[g]], gv[g] * vp);
+                            }
+                            for (int e = 64 + lane; e < gn[g]; e += 64) {
+                                const int i = eidx[go[g] + e];
+                                const double ev = evals[go[g] + e];
+                                if (i == p) ut[p] = ev * vp;
+                                else lds_add(&ut[i], ev * vp);
+                            }
+                            nops += gn[g];
                         }
-                        for (int e = 64 + lane; e < gn[g]; e += 64) {
-                            const int i = eidx[go[g] + e];
-                            const double ev = evals[go[g] + e];
-                            if (i == p) ut[p] = ev * vp;
-                            else lds_add(&ut[i], ev * vp);
-                        }
-                        nops += gn[g];
+                        h_wave_sync();
                     }
-                    h_wave_sync();
+                };
+                int ai[EG], an[EG], ao[EG], bi[EG], bn[EG], bo[EG];
+                double av[EG], bv[EG];
+                if (K <= 2 * EG) {
+                    for (int tg = 0; tg < K; tg += EG) {
+                        eta_group(tg, 1, ai, av, an, ao);
+                        apply(tg, ai, av, an, ao);
+                    }
+                } else {
+                    eta_group(0, 1, ai, av, an, ao);
+                    for (int tg = 0; tg < K;) {   // ping-pong: the next group in flight while one is applied
+                        eta_group(tg + EG, 1, bi, bv, bn, bo);
+                        apply(tg, ai, av, an, ao);
+                        tg += EG;
+                        if (tg >= K) break;
+                        eta_group(tg + EG, 1, ai, av, an, ao);
+                        apply(tg, bi, bv, bn, bo);
+                        tg += EG;
+                    }
                 }
             }
             const double arq = ut[r];

@@ -101,13 +101,10 @@ struct twosd_ctx {
     int CH = 0;                   // column slots per lane of the hypersparse kernel
     int *d_kslot = nullptr, *d_kix = nullptr;
     double *d_kv = nullptr, *d_d0 = nullptr;
-    int wr_width = 1;             // W row-ELL width (max row length)
-    int *d_wr_col = nullptr, *d_bcp = nullptr, *d_bci = nullptr;
-    double *d_wr_val = nullptr, *d_bcv = nullptr;
-    int *d_wr_ocol = nullptr;
+    int *d_bcp = nullptr, *d_bci = nullptr;
+    double *d_bcv = nullptr;
     int *d_wcp = nullptr, *d_wcc = nullptr;   // W by rows (CSR) for the segmented pricing scatter
     double *d_wcv = nullptr;
-    double *d_wr_oval = nullptr;
     int *d_brptr = nullptr, *d_brcol = nullptr;
     double *d_brval = nullptr;
     int *d_eidx = nullptr;

@@ -29,9 +29,6 @@ struct HyperParams {
     int retry;                                          // a pool start ending non-optimal is retried from pool[0]
     const int *colptr, *rowidx; const double *val;      // W CSC
     const double *q; const int8_t *btype;
-    int wr_width;                                       // W by rows as row-ELL (columns ascending, width
-    const int *wr_col; const double *wr_val;            //   min(max row length, 64), padding column -1);
-    const int *wr_ocol; const double *wr_oval;          //   long rows continue in an overflow CSR
     const int *wcp, *wcc; const double *wcv;            // W by rows as CSR (columns ascending)
     const int *bcp, *bci; const double *bcv;            // B^{-1} CSC (MP + 1 column pointers, rows ascending)
     const int *brptr, *brcol; const double *brval;      // B^{-1} CSR (MP rows)

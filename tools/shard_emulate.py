@@ -9,7 +9,9 @@ point-to-point links in parallel) and added -- it is the one number not measured
 
 Per-rank step = the rank's own phases + the exchange estimate; reported per x point and as the
 max over ranks, next to N = 1 (one context holding everything, the bench's single-GPU step).
-Usage (GPU box): python tools/shard_emulate.py [G] [scenarios] [steps] [pool] [training scenarios]
+Usage (GPU box): python tools/shard_emulate.py [G] [scenarios] [steps] [pool] [training scenarios] [warmup]
+(the bench protocol: `warmup` untimed steps cycling over the x points, then `steps` reported ones;
+every refresh trains from the current pool, so revisited x points get better pools, as in bench.py)
 """
 import json
 import os
@@ -40,6 +42,7 @@ def main():
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else 8
     POOL = int(sys.argv[4]) if len(sys.argv) > 4 else 4096
     TRAIN = int(sys.argv[5]) if len(sys.argv) > 5 else 4 * POOL
+    WARMUP = int(sys.argv[6]) if len(sys.argv) > 6 else 5
     seed = 20250219
     L1, NC, NV = 128, 160, 4096
     d = os.path.join(ROOT, "data", "smps", "storm")
@@ -155,7 +158,12 @@ def main():
         rk["phases"] = {"sel": tm[4] / 1e3, "lp": tm[0] / 1e3, "dedup": tm[1] / 1e3, "cut": (tc[2] + tc[3]) / 1e3}
         return 1e3 * (time.perf_counter() - t), piv
 
-    refresh(xs[-1])       # warmup: the pool at the last x point
+    refresh(xs[-1])       # the pool at the last x point
+    for i in range(WARMUP):   # untimed steps ending at the last x point (bench.py's warmup)
+        xx = xs[(i - WARMUP) % len(xs)]
+        refresh(xx)
+        for rk in ranks:
+            solve_cut(rk, xx)
     rows = []
     for i in range(steps):
         xx = xs[i % len(xs)]
@@ -173,7 +181,7 @@ def main():
         print(f"x{rows[-1][0]}: per-rank step max {rows[-1][1]:.2f} ms (mean {rows[-1][2]:.2f}), pivots {rows[-1][3]:.2f}, "
               f"pool {P}, pack {max(nbytes) / 1e6:.1f} MB, slowest rank {rows[-1][5]}", flush=True)
     step_ms = float(np.mean([r[1] for r in rows]))
-    print(json.dumps({"G": G, "scenarios": N, "pool": POOL, "train": TRAIN, "per_rank_step_ms": step_ms,
+    print(json.dumps({"G": G, "scenarios": N, "pool": POOL, "train": TRAIN, "warmup": WARMUP, "steps": steps, "per_rank_step_ms": step_ms,
                       "subproblems_per_s_projected": N / (step_ms * 1e-3),
                       "note": f"emulated on one GPU; xGMI all-gather estimated at {LINK_GBS} GB/s per link, "
                               f"{COLLECTIVE_MS} ms per collective ({REFRESH_COLLECTIVES} per refresh, "
