@@ -3,9 +3,9 @@
 // __shfl_xor lowers to ds_bpermute (an LDS-path round trip per 32-bit half); a double
 // reduction over 64 lanes then costs ~12 of them.  Here each 16-lane row is reduced with
 // DPP lane moves (quad_perm xor1, quad_perm xor2, row_half_mirror, row_mirror: every lane
-// of a row ends with the row result), then the four row results are combined in a fixed
-// order through v_readlane (lanes 0, 16, 32, 48).  The combine order is fixed, so the
-// result is bit-identical on every lane and every run.
+// of a row ends with the row result, the same bits on every lane), then the four row results
+// are combined in a fixed order by DPP row broadcasts into lane 63 and read from there.  The
+// combine order is fixed, so the result is bit-identical on every lane and every run.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -37,29 +37,6 @@ __device__ __forceinline__ double readlane_dbl(double v, int lane) {
 }
 
 // sum over the 64 lanes; every lane returns the same bits (uniform)
-__device__ __forceinline__ double wsum(double v) {
-    v += dpp_d<kDppXor1>(v);
-    v += dpp_d<kDppXor2>(v);
-    v += dpp_d<kDppHalfMirror>(v);
-    v += dpp_d<kDppMirror>(v);
-    return (readlane_dbl(v, 0) + readlane_dbl(v, 16)) + (readlane_dbl(v, 32) + readlane_dbl(v, 48));
-}
-
-__device__ __forceinline__ double wmin(double v) {
-    v = fmin(v, dpp_d<kDppXor1>(v));
-    v = fmin(v, dpp_d<kDppXor2>(v));
-    v = fmin(v, dpp_d<kDppHalfMirror>(v));
-    v = fmin(v, dpp_d<kDppMirror>(v));
-    return fmin(fmin(readlane_dbl(v, 0), readlane_dbl(v, 16)), fmin(readlane_dbl(v, 32), readlane_dbl(v, 48)));
-}
-
-__device__ __forceinline__ double wmax(double v) {
-    v = fmax(v, dpp_d<kDppXor1>(v));
-    v = fmax(v, dpp_d<kDppXor2>(v));
-    v = fmax(v, dpp_d<kDppHalfMirror>(v));
-    v = fmax(v, dpp_d<kDppMirror>(v));
-    return fmax(fmax(readlane_dbl(v, 0), readlane_dbl(v, 16)), fmax(readlane_dbl(v, 32), readlane_dbl(v, 48)));
-}
 
 // arg-reduction: the lane with the largest key (ties: smallest idx); returns the winning
 // idx (uniform) and the payload values of that lane.  Lanes without a candidate pass
@@ -116,10 +93,51 @@ __device__ __forceinline__ double dpp_bcast_d(double v) {
     const int hi = __builtin_amdgcn_update_dpp((int)(uint32_t)(u >> 32), (int)(uint32_t)(u >> 32), CTRL, ROWS, 0xF, false);
     return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
 }
+// the same with 0 outside the row mask (for sums)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_bcast0_d(double v) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, ROWS, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, ROWS, 0xF, false);
+    return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
 __device__ __forceinline__ int dpp_bcast_min_i(int v) {
     v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x142, 0xA, 0xF, false));
     return min(v, __builtin_amdgcn_update_dpp(v, v, 0x143, 0xC, 0xF, false));
 }
+// sum over the 64 lanes; every lane returns the same bits (uniform).  The row totals meet in
+// lane 63 as (r3 + r2) + (r1 + r0) -- the fixed order (r0 + r1) + (r2 + r3) up to commutation,
+// which is exact in IEEE arithmetic
+__device__ __forceinline__ double wsum(double v) {
+    v += dpp_d<kDppXor1>(v);
+    v += dpp_d<kDppXor2>(v);
+    v += dpp_d<kDppHalfMirror>(v);
+    v += dpp_d<kDppMirror>(v);
+    v += dpp_bcast0_d<0x142, 0xA>(v);   // rows 1 / 3: + the row 0 / row 2 total
+    v += dpp_bcast0_d<0x143, 0xC>(v);   // rows 2 / 3: + lane 31 (rows 0 + 1)
+    return readlane_dbl(v, 63);
+}
+
+__device__ __forceinline__ double wmin(double v) {
+    v = fmin(v, dpp_d<kDppXor1>(v));
+    v = fmin(v, dpp_d<kDppXor2>(v));
+    v = fmin(v, dpp_d<kDppHalfMirror>(v));
+    v = fmin(v, dpp_d<kDppMirror>(v));
+    v = fmin(v, dpp_bcast_d<0x142, 0xA>(v));
+    v = fmin(v, dpp_bcast_d<0x143, 0xC>(v));
+    return readlane_dbl(v, 63);
+}
+
+__device__ __forceinline__ double wmax(double v) {
+    v = fmax(v, dpp_d<kDppXor1>(v));
+    v = fmax(v, dpp_d<kDppXor2>(v));
+    v = fmax(v, dpp_d<kDppHalfMirror>(v));
+    v = fmax(v, dpp_d<kDppMirror>(v));
+    v = fmax(v, dpp_bcast_d<0x142, 0xA>(v));
+    v = fmax(v, dpp_bcast_d<0x143, 0xC>(v));
+    return readlane_dbl(v, 63);
+}
+
 // maximum over the 64 lanes (uniform)
 __device__ __forceinline__ double wmax_any(double v) {
     v = fmax(v, dpp_d<kDppXor1>(v));
