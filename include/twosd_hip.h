@@ -148,6 +148,13 @@ int twosd_refresh_train(twosd_ctx *ctx, int epi, const double *x, int first, int
 int twosd_refresh_train_ex(twosd_ctx *ctx, int epi, const double *x, int first, int count, int kcap, int *n_bases,
                            int *n_optimal, double *box_lo, double *box_hi);
 int twosd_refresh_cap_stats(twosd_ctx *ctx, int64_t *pivots_sum, int64_t *scenarios);
+/* Step 2 of the distributed refresh, identical on every rank (host code, no context): over the n
+ * bases all ranks list (twosd_refresh_train_bases, concatenated in rank order; rank_of[i] = the
+ * listing rank), a key listed by several ranks counts the sum of its counts and belongs to its
+ * first occurrence; the min(distinct, max_pool - 1) largest totals, ties by first occurrence, go
+ * to owner[] / rep[] (the owning rank and its first scenario), *npick of them. */
+int twosd_select_refresh_bases(const uint64_t *keys, const int64_t *counts, const int64_t *reps, const int32_t *rank_of,
+                               int n, int max_pool, int64_t *owner, int64_t *rep, int *npick);
 int twosd_refresh_train_bases(twosd_ctx *ctx, uint64_t *keys, int *counts, int *reps);
 int twosd_refresh_build_local(twosd_ctx *ctx, int n_own, const int *reps, int64_t *pack_bytes);
 int twosd_refresh_pack(twosd_ctx *ctx, void *d_dst);

@@ -2483,6 +2483,40 @@ extern "C" int twosd_refresh_cap_stats(twosd_ctx *c, int64_t *pivots_sum, int64_
     return TWOSD_OK;
 }
 
+// The global basis selection of a distributed refresh (host, no context): the bases the ranks
+// list (concatenated in rank order), a key seen by several ranks counting the sum of its counts
+// and owned by its first occurrence; the max_pool - 1 largest totals, ties by first occurrence --
+// the single-rank refresh's stable sort over all training scenarios.
+extern "C" int twosd_select_refresh_bases(const uint64_t *keys, const int64_t *counts, const int64_t *reps, const int32_t *rank_of,
+                                          int n, int max_pool, int64_t *owner, int64_t *rep, int *npick) {
+    if (n < 0 || !npick || (n > 0 && (!keys || !counts || !reps || !rank_of))) return fail(TWOSD_E_ARG, "select_refresh_bases: bad arguments");
+    *npick = 0;
+    if (n == 0 || max_pool <= 1) return TWOSD_OK;
+    if (!owner || !rep) return fail(TWOSD_E_ARG, "select_refresh_bases: NULL output");
+    std::vector<int> idx(n);
+    for (int i = 0; i < n; ++i) idx[i] = i;
+    std::sort(idx.begin(), idx.end(), [&](int a, int b) { return keys[a] != keys[b] ? keys[a] < keys[b] : a < b; });
+    struct G { int64_t tot; int first; };
+    std::vector<G> g;
+    g.reserve(n);
+    for (int a = 0; a < n;) {
+        int b = a;
+        int64_t t = 0;
+        while (b < n && keys[idx[b]] == keys[idx[a]]) t += counts[idx[b++]];
+        g.push_back({t, idx[a]});   // the lowest index of the key: its first occurrence
+        a = b;
+    }
+    const size_t k = std::min<size_t>(g.size(), (size_t)max_pool - 1);
+    std::partial_sort(g.begin(), g.begin() + k, g.end(),
+                      [](const G &a, const G &b) { return a.tot != b.tot ? a.tot > b.tot : a.first < b.first; });
+    for (size_t i = 0; i < k; ++i) {
+        owner[i] = rank_of[g[i].first];
+        rep[i] = reps[g[i].first];
+    }
+    *npick = (int)k;
+    return TWOSD_OK;
+}
+
 extern "C" int twosd_solve_batch(twosd_ctx *c, int epi, const double *x, int first, int count, double *obj,
                                  double *pi, double *y, int *status) {
     if (!c || !c->has_template) return fail(TWOSD_E_STATE, "solve_batch: no template");

@@ -191,6 +191,27 @@ def select_refresh_bases(keys, counts, reps, rank_of, max_pool):
     first occurrence.  The max_pool - 1 most frequent, ties by first occurrence in (rank,
     scenario) order -- the single-rank refresh's stable sort over all training scenarios.
     Returns (owner rank, owner's first scenario) of the picks, in pool order."""
+    import ctypes
+    from ._lib import check, load
+    keys = np.ascontiguousarray(keys, dtype=np.uint64)
+    n = int(keys.size)
+    if n == 0 or max_pool <= 1:
+        return np.zeros(0, dtype=np.int64), np.zeros(0, dtype=np.int64)
+    cnt = np.ascontiguousarray(counts, dtype=np.int64)
+    rp = np.ascontiguousarray(reps, dtype=np.int64)
+    rk = np.ascontiguousarray(rank_of, dtype=np.int32)
+    k = min(n, max_pool - 1)
+    owner = np.zeros(k, dtype=np.int64)
+    rep = np.zeros(k, dtype=np.int64)
+    npick = ctypes.c_int(0)
+    ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    check(load().twosd_select_refresh_bases(ptr(keys), ptr(cnt), ptr(rp), ptr(rk), n, int(max_pool), ptr(owner), ptr(rep),
+                                            ctypes.byref(npick)))
+    return owner[:npick.value], rep[:npick.value]
+
+
+def _select_refresh_bases_np(keys, counts, reps, rank_of, max_pool):
+    """numpy statement of select_refresh_bases (the tests check the native one against it)."""
     keys = np.asarray(keys, dtype=np.uint64)
     if keys.size == 0 or max_pool <= 1:
         return np.zeros(0, dtype=np.int64), np.zeros(0, dtype=np.int64)

@@ -131,3 +131,19 @@ def test_training_cap_is_global(stats, cap):
         mp.start_processes(_cap_worker, args=(2, port, stats, out), nprocs=2, join=True, start_method="spawn")
         res = dict(out)
     assert res[0] == res[1] == cap
+
+
+@pytest.mark.parametrize("max_pool", [1, 2, 5, 64, 5000])
+def test_native_selection_equals_numpy(max_pool):
+    """twosd_select_refresh_bases (host code of the library, no GPU) against the numpy statement:
+    random rank lists with repeated keys across ranks and tied totals."""
+    rng = np.random.default_rng(max_pool)
+    for G in (1, 3, 8):
+        keys = rng.integers(1, 60, size=700, dtype=np.int64).astype(np.uint64)
+        counts = rng.integers(1, 4, size=700)
+        reps = rng.integers(0, 10000, size=700)
+        rank_of = np.sort(rng.integers(0, G, size=700))
+        o1, r1 = sdist.select_refresh_bases(keys, counts, reps, rank_of, max_pool)
+        o2, r2 = sdist._select_refresh_bases_np(keys, counts, reps, rank_of, max_pool)
+        np.testing.assert_array_equal(o1, o2)
+        np.testing.assert_array_equal(r1, r2)
