@@ -25,7 +25,8 @@ from collections import defaultdict
 
 import numpy as np
 
-KERNELS = ["lp_hyper_kernel", "pool_refine_kernel", "pool_select_kernel", "cut_argmax2_kernel"]
+KERNELS = ["lp_hyper_kernel", "pool_refine_kernel", "pool_select_kernel", "cut_argmax2_kernel", "cut_fixup_kernel",
+           "pg_ftran_kernel", "pg_fill_kernel"]
 
 
 def short(name):
@@ -47,8 +48,19 @@ def load_pass(path):
     return disp
 
 
+def load_trace(path):
+    """dispatch id -> {name, ms} of a kernel-trace CSV (prof_reduce.py's .csv.gz or raw)"""
+    disp = {}
+    f = gzip.open(path, "rt", newline="") if path.endswith(".gz") else open(path, newline="")
+    for r in csv.DictReader(f):
+        disp[int(r["Dispatch_Id"])] = {"name": r["Kernel_Name"], "c": {},
+                                       "ms": (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6}
+    return disp
+
+
 def timed_steps(disp, K):
-    """per timed step: {kernel: the dispatch (largest FETCH/any counter) of that kernel in the step}"""
+    """per timed step: {kernel: the dispatch (largest FETCH/any counter; by duration in a trace) of
+    that kernel in the step}"""
     ids = sorted(disp)
     cuts = [i for i in ids if "cut_argmax2_kernel" in disp[i]["name"]]
     if len(cuts) < K + 1:
@@ -61,8 +73,8 @@ def timed_steps(disp, K):
                 k = short(disp[i]["name"])
                 if not k:
                     continue
-                val = sum(disp[i]["c"].values())
-                if k not in sel or val > sum(disp[sel[k]]["c"].values()):
+                val = sum(disp[i]["c"].values()) or disp[i]["ms"]
+                if k not in sel or val > (sum(disp[sel[k]]["c"].values()) or disp[sel[k]]["ms"]):
                     sel[k] = i
         steps.append({k: disp[i] for k, i in sel.items()})
     return steps
@@ -148,8 +160,51 @@ def main():
                         "counted by the kernel); eta stores are the only writes that grow with the pivots"}
     out["bench_lines"] = {t: {k: b.get(k) for k in ("value", "ms_per_step", "phases_ms_per_step", "lp_pivots_mean")}
                           for t, b in bench_lines.items()}
+    # timed-step kernel durations from the trace pass (no counters: undisturbed timing)
+    dur = defaultdict(list)
+    tr = glob.glob(os.path.join(src, "trace_trace.csv.gz")) + glob.glob(os.path.join(src, "trace", "**", "*kernel_trace.csv"), recursive=True)
+    if tr:
+        for st in timed_steps(load_trace(tr[0]), K):
+            for k, d in st.items():
+                dur[k].append(d["ms"])
+    out["trace_ms"] = {k: float(np.mean(v)) for k, v in dur.items()}
     with open(os.path.join(dst, "pmc_timed.json"), "w") as f:
         json.dump(out, f, indent=1)
+    # the summary bench.py reads (latest profiles/r*/pmc_summary.json): per kernel, the mean over
+    # the timed launches of the driver's protocol
+    summ = {"workload": "storm 1000000 scenarios, the driver's bench.py --gpus 1 --steps %d --warmup 5, 1 MI355X" % K,
+            "source": "rocprofv3 --kernel-trace --stats and separate --pmc passes over that command "
+                      "(tools/profile_r04.sh, reduced on the box by tools/prof_reduce.py); means over the timed steps' "
+                      "launches (tools/pmc_timed.py)",
+            "correction": "FETCH_SIZE/WRITE_SIZE are KiB; hbm_bytes = 1024*(2*FETCH_SIZE + WRITE_SIZE) (the guide's gfx950 "
+                          "correction for wide reads; an upper estimate for narrow accesses); hbm_bytes_raw = "
+                          "1024*(FETCH_SIZE + WRITE_SIZE)",
+            "scenarios": 1_000_000, "kernels": {}}
+    for k, ent in out["kernels"].items():
+        m = ent["mean"]
+        f_kib = m.get("FETCH_SIZE", 0.0) / 1024.0
+        w_kib = m.get("WRITE_SIZE", 0.0) / 1024.0
+        ms = out["trace_ms"].get(k)
+        e = {"duration_ms": ms, "FETCH_SIZE_KiB": f_kib, "WRITE_SIZE_KiB": w_kib,
+             "hbm_bytes_per_launch": 1024.0 * (2 * f_kib + w_kib), "hbm_bytes_per_launch_raw": 1024.0 * (f_kib + w_kib),
+             "scratch_bytes_per_lane": ent["meta"].get("scratch_bytes_per_lane")}
+        for cn in ("SQ_INSTS_VALU_MFMA_MOPS_F64", "SQ_INSTS_VALU_MFMA_F64", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES",
+                   "GRBM_GUI_ACTIVE", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
+                   "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA"):
+            if cn in m:
+                e[cn] = m[cn]
+        if ms and m.get("SQ_INSTS_VALU_MFMA_MOPS_F64"):
+            fl = 512.0 * m["SQ_INSTS_VALU_MFMA_MOPS_F64"]
+            e["mfma_f64_flops"] = fl
+            e["mfma_f64_tflops_counted"] = fl / (ms * 1e-3) / 1e12
+            e["mfma_util"] = e["mfma_f64_tflops_counted"] / 78.6
+            if m.get("GRBM_GUI_ACTIVE"):
+                e["mfma_busy_frac"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["GRBM_GUI_ACTIVE"] / 8.0 * 1024.0)
+        summ["kernels"][k] = e
+    if "lp_write_split" in out:
+        summ["lp_write_split"] = out["lp_write_split"]["fit"]
+    with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
+        json.dump(summ, f, indent=1)
     print(json.dumps({k: v["mean"] for k, v in out["kernels"].items()}, indent=1))
     if "lp_write_split" in out:
         print(json.dumps(out["lp_write_split"], indent=1))
