@@ -1269,13 +1269,14 @@ __global__ void pool_refine_merge_kernel(int N, int G, int ncand, const float *_
 }
 
 // chunks per tile: enough blocks to fill the GPU (~1024) when the batch alone does not, at least
-// kSelWaves bases / candidates per chunk
+// kSelWaves bases / candidates per chunk, at most 64 chunks (a rank's 2048 training scenarios at
+// N = 8 picking over a 4096-basis pool: 16 tiles x 64 chunks)
 static int sel_split(int N, int items) {
     if (getenv("TWOSD_SEL_NOSPLIT")) return 1;   // test hook: one chunk (the picks must not change)
     const int nb = (N + kSelTile - 1) / kSelTile;
     int g = (1024 + nb - 1) / nb;
     g = std::min(g, std::max(1, items / kSelWaves));
-    return std::max(1, std::min(g, 16));
+    return std::max(1, std::min(g, 64));
 }
 int pool_select_split(int N, int npool) { return sel_split(N, npool); }
 int pool_refine_split(int N, int ncand) { return sel_split(N, ncand); }
