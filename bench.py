@@ -258,11 +258,11 @@ def main():
     # a distributed refresh builds one pool for all ranks, so it is sized by the whole batch
     dist_refresh = world > 1 and args.refresh_dist == 1
     # pool size by the shard: 4096 per 1M scenarios on one rank, at least 512; the distributed
-    # refresh builds twice that (at least 1024): its training and composition are split over the
-    # ranks (profiles/r03/shard_emulate_pool*.txt: at N = 8, 1024-4096 bases all give a
-    # 31-35 ms per-rank step, 1024 the least)
+    # refresh builds four times that (at least 1024): its training and composition are split over
+    # the ranks (profiles/r04/n8/shard_emulate_pool*.txt: at N = 8 with the bench warmup, pools of
+    # 1024 / 1536 / 2048 / 3072 / 4096 bases give 18.7 / 18.3 / 18.4 / 20.3 / 22.1 ms per rank)
     if args.refresh_pool <= 0:
-        scope = 2 * n_local * E if dist_refresh else n_local * E
+        scope = 4 * n_local * E if dist_refresh else n_local * E
         args.refresh_pool = max(1024 if dist_refresh else 512, min(4096, int(4096 * scope / 1_000_000) // 256 * 256))
     if args.refresh_train <= 0:
         args.refresh_train = 4 * args.refresh_pool
