@@ -324,7 +324,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
         const int *brptr, *bcp;
         int K = 0, it = 0, status = TWOSD_LP_OPTIMAL;
         int eoff = 0;
-        long long nops = 0;
+        unsigned nops = 0;   // entries processed by this solve (< 2^32: at most kmax pivots of <= a few 10^4 each)
         // a pool start that ends non-optimal (numerics, iteration cap) is retried from the
         // primary basis, so the pool never changes which scenarios solve
         for (int attempt = 0; attempt < 2; ++attempt) {
@@ -350,7 +350,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 hb[t] = A->hb0[(size_t)pb * MP + 64 * t + ln];
                 wd[t] = 1.0f;
             }
-            nops += (long long)(__builtin_amdgcn_readlane(ksv, R) - eb[0]) * 64;
+            nops += (unsigned)(__builtin_amdgcn_readlane(ksv, R) - eb[0]) * 64u;
             // column u of every slot, in increasing u per row: the same fma order as a per-row walk
             for (int u = 0; u < w; ++u) {
                 double kvv[R];
@@ -976,7 +976,7 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
             CP.obj[s] = objv;
             CP.status[s] = status;
             CP.iters[s] = it;
-            if (CP.ops) CP.ops[s] = nops;
+            if (CP.ops) CP.ops[s] = (long long)nops;
             if (CP.etan) CP.etan[s] = eoff;   // the eta-arena entries this solve wrote (12 B each)
             if (CP.npool > 1) CP.pool_pick[s] = pb;   // 0 if the pool start was retried
         }

@@ -18,9 +18,10 @@ constexpr int kDppXor2 = 0x4E;        // quad_perm(2,3,0,1)
 constexpr int kDppHalfMirror = 0x141; // row_half_mirror
 constexpr int kDppMirror = 0x140;     // row_mirror
 
+// (the quad permutes and mirrors read a valid lane for every lane: no old value to preset)
 template <int CTRL>
 __device__ __forceinline__ int dpp_i(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
 }
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
