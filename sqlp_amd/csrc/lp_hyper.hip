@@ -1009,9 +1009,6 @@ constexpr int kSelWaves = 16;   // 16 waves share one staged scenario tile (late
 #define TWOSD_SEL_B 16           // records per batch of the selection streams (loads in flight)
 #endif
 constexpr int kSelB = TWOSD_SEL_B;
-#ifndef TWOSD_SEL_BRANCHFREE
-#define TWOSD_SEL_BRANCHFREE 0
-#endif
 // Two scenarios per lane: s0 + lane (.x) and s0 + 64 + lane (.y), 128 per block.  The staged
 // deltas are (x, y) pairs, so one ds_read_b64 (2 LDS cycles per wave, as a ds_read_b32) and one
 // v_pk_fma_f32 serve both.  The arithmetic per scenario is that of one scenario per lane (same
@@ -1053,20 +1050,6 @@ __device__ __forceinline__ sel_f2 h_stream2(const int2 *__restrict__ rec, int j0
                                             const sel_f2 *dvt2, int lane, Alive alive2) {
     sel_f2 inf = {cinf, cinf}, x = {0.0f, 0.0f};
     const int lane8 = 8 * lane;
-#if TWOSD_SEL_BRANCHFREE
-    // both paths computed, selected per record (row starts are a third to a half of the records):
-    // VALU instead of the uniform branch's SALU, the kernels' bottleneck
-    auto step = [&](int code, float v, sel_f2 dl) {
-        const bool rs = code < 0;
-        const sel_f2 vv = {v, v};
-        const sel_f2 fx = __builtin_elementwise_fma(vv, dl, x);
-        const sel_f2 vi = h_viol_f2(x, cw);
-        inf.x = rs ? inf.x + vi.x : inf.x;
-        inf.y = rs ? inf.y + vi.y : inf.y;
-        x.x = rs ? v : fx.x;
-        x.y = rs ? v : fx.y;
-    };
-#else
     auto step = [&](int code, float v, sel_f2 dl) {
         if (code < 0) {   // next row: close the previous one
             inf += h_viol_f2(x, cw);
@@ -1075,7 +1058,6 @@ __device__ __forceinline__ sel_f2 h_stream2(const int2 *__restrict__ rec, int j0
             x = __builtin_elementwise_fma((sel_f2){v, v}, dl, x);
         }
     };
-#endif
     int j = (__ballot(alive2(inf)) == 0) ? j1 : j0;
     for (; j + kSelB <= j1; j += kSelB) {   // batches of records: scalar loads and LDS reads in flight together
         int2 rc[kSelB];
