@@ -269,7 +269,7 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_refresh_sel); c->refresh_sel_cap = 0; c->box_epi = -1;
     dfree(c->d_eo_pb); dfree(c->d_eo_K); dfree(c->d_eo_off); dfree(c->d_eo_etap); dfree(c->d_eo_etaoff);
     dfree(c->d_eo_eidx); dfree(c->d_eo_evals); dfree(c->d_eo_used); c->eo_rows = c->eo_cap = 0; c->eo_kmax = 0;
-    dfree(c->d_pg_ival); dfree(c->d_pg_irow); dfree(c->d_pg_ioff); dfree(c->d_pg_amax); dfree(c->d_pg_d0p); dfree(c->d_pg_cnt); dfree(c->d_pg_tot);
+    dfree(c->d_pg_scrow); dfree(c->d_pg_scoff); dfree(c->d_pg_scval); dfree(c->d_pg_ival); dfree(c->d_pg_irow); dfree(c->d_pg_ioff); dfree(c->d_pg_amax); dfree(c->d_pg_d0p); dfree(c->d_pg_cnt); dfree(c->d_pg_tot);
     dfree(c->d_pg_valid); dfree(c->d_pg_head0); dfree(c->d_pg_map); dfree(c->d_pg_off); dfree(c->d_pg_pos);
     dfree(c->d_rt_pack); dfree(c->d_gs_heads); dfree(c->d_gs_cnt); dfree(c->d_gs_tot); dfree(c->d_gs_valid);
     dfree(c->d_gs_irow); dfree(c->d_gs_ioff); dfree(c->d_gs_ival);
@@ -853,28 +853,46 @@ static int pg_args(twosd_ctx *c, int nsrc, PgArgs &A) {
 static int pg_compute(twosd_ctx *c, int nsrc, PgArgs &A, int **h_tot, int **h_valid, long long *inz_out, bool dbg) {
     int rc;
     if ((rc = pg_args(c, nsrc, A))) return rc;
+    // the first pass keeps each source's nonzeros (up to sc_cap entries, sized from the last
+    // build's largest source; at most 1.5 GiB in all) for pg_gather_kernel: one FTRAN per
+    // column instead of two; a source past sc_cap runs the second FTRAN pass
+    const int m = c->L.m;
+    long long cap = c->pg_sc_cap > 0 ? c->pg_sc_cap : std::min<long long>((long long)m * m, 16384);
+    if (getenv("TWOSD_PG_NOSCRATCH")) cap = 0;   // A/B knob: two FTRAN passes
+    if (const char *e = getenv("TWOSD_PG_SCCAP")) cap = atoll(e);   // test hook: sources past it take pass 1
+    cap = std::min(cap, ((3LL << 29) / 12) / std::max(nsrc, 1));
+    if (cap > 0 && ((rc = dev_reserve(c, &c->d_pg_scrow, (size_t)nsrc * cap)) || (rc = dev_reserve(c, &c->d_pg_scval, (size_t)nsrc * cap)) ||
+                    (rc = dev_reserve(c, &c->d_pg_scoff, (size_t)nsrc * m))))
+        return rc;
+    A.sc_cap = cap; A.sc_row = c->d_pg_scrow; A.sc_val = c->d_pg_scval; A.sc_off = c->d_pg_scoff;
     HIPCHK(pg_launch_ftran(A, 0, nsrc, c->stream));
     int *h_nz = stage_buf<int>(c, 11, (size_t)nsrc);
     long long *h_ioff = stage_buf<long long>(c, 12, (size_t)nsrc);
     if (!h_nz || !h_ioff) return fail(TWOSD_E_DEVICE, "pool refresh: pinned staging allocation failed");
     HIPCHK(hipMemcpyAsync(h_nz, A.nztot, sizeof(int) * nsrc, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    long long inz = 0;
+    long long inz = 0, nzmax = 0;
+    int over = 0;
     for (int a = 0; a < nsrc; ++a) {
         h_ioff[a] = inz;
         inz += h_nz[a];
+        nzmax = std::max<long long>(nzmax, h_nz[a]);
+        over += h_nz[a] > cap;
     }
     if ((rc = dev_reserve(c, &c->d_pg_irow, (size_t)inz)) || (rc = dev_reserve(c, &c->d_pg_ival, (size_t)inz))) return rc;
     HIPCHK(hipMemcpyAsync(c->d_pg_ioff, h_ioff, sizeof(long long) * nsrc, hipMemcpyHostToDevice, c->stream));
     A.inter_off = c->d_pg_ioff; A.inter_row = c->d_pg_irow; A.inter_val = c->d_pg_ival;
-    HIPCHK(pg_launch_ftran(A, 1, nsrc, c->stream));
+    if (cap > 0) HIPCHK(pg_launch_gather(A, nsrc, c->stream));
+    if (over || cap == 0) HIPCHK(pg_launch_ftran(A, 1, nsrc, c->stream));
+    c->pg_sc_cap = std::max<long long>(1024, nzmax + nzmax / 2);   // the next build's scratch
     HIPCHK(pg_launch_count(A, nsrc, c->stream));
     int *ht = stage_buf<int>(c, 9, (size_t)5 * nsrc);
     if (!ht) return fail(TWOSD_E_DEVICE, "pool refresh: pinned staging allocation failed");
     HIPCHK(hipMemcpyAsync(ht, c->d_pg_tot, sizeof(int) * 4 * nsrc, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(ht + (size_t)4 * nsrc, c->d_pg_valid, sizeof(int) * nsrc, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    if (dbg) fprintf(stderr, "pg_compute: %d sources, %lld intermediate entries\n", nsrc, inz);
+    if (dbg) fprintf(stderr, "pg_compute: %d sources, %lld intermediate entries, largest %lld, %d past the scratch of %lld\n", nsrc, inz,
+                     nzmax, over, cap);
     *h_tot = ht;
     *h_valid = ht + (size_t)4 * nsrc;
     *inz_out = inz;

@@ -10,11 +10,15 @@
 // LDS, so no HBM round trip of a dense B^{-1}:
 //   pg_ftran_kernel<0>  per source: max |.| over B_pb^{-1} and the result (drop threshold
 //                       1e-14 max, as compose_binv) and per column the nonzero count;
-//   pg_ftran_kernel<1>  the same FTRAN again, the kept entries of each column written (rows
+//                       <0> also keeps each column's nonzeros (rows ascending) in a per-source
+//                       scratch of sc_cap entries;
+//   pg_gather_kernel    the kept entries of each column copied from that scratch (rows
 //                       ascending) into an intermediate CSC at host-prefixed offsets.  Kept:
 //                       rows some eta touched |v| > drop, other rows exactly B_pb^{-1}'s
 //                       entries -- compose_binv's rule, and its arithmetic: row r <- eta_r x_r,
 //                       row i <- fma(eta_i, x_r, row i), so the values are bit-identical;
+//   pg_ftran_kernel<1>  the same FTRAN again, writing the kept entries directly: only for the
+//                       sources whose nonzeros overflowed the scratch (round 3 ran it for all);
 //   pg_count_kernel     per source: row / element-row counts, pi0, the dual-feasibility and
 //                       4-probe residual checks of finish_composed, the per-basis totals;
 //   pg_fill_kernel      at host-prefixed offsets: CSC (compacted), CSR (columns ascending,
@@ -109,6 +113,9 @@ __global__ __launch_bounds__(kFtThreads) void pg_ftran_kernel(PgArgs A) {
         if (PASS == 0 && tid == 0) { A.amax[a] = -1.0; A.nztot[a] = 0; }
         return;
     }
+    if (PASS == 1 && A.sc_cap > 0 && A.nztot[a] <= A.sc_cap) return;   // pg_gather_kernel's source
+    __shared__ int sc_ctr;                                // PASS 0: scratch entries claimed
+    if (PASS == 0 && tid == 0) sc_ctr = 0;                // (visible after mark_touched's barriers)
     double *x = smem + (size_t)wv * m;                    // this wave's column, dense
     int *etap = reinterpret_cast<int *>(smem + (size_t)kFtWaves * m);
     int *etaoff = etap + A.kmax;
@@ -160,6 +167,27 @@ __global__ __launch_bounds__(kFtThreads) void pg_ftran_kernel(PgArgs A) {
             }
             if (lane == 0) nzc[c] = cnt;
             nzsum += cnt;
+            if (A.sc_cap > 0) {   // keep the nonzeros for the gather (a claim past sc_cap: none kept)
+                int off = 0;
+                if (lane == 0) off = atomicAdd(&sc_ctr, cnt);
+                off = __shfl(off, 0);
+                if ((long long)off + cnt <= A.sc_cap) {
+                    const size_t base = (size_t)a * A.sc_cap + off;
+                    int run = 0;
+                    for (int i0 = 0; i0 < m; i0 += 64) {
+                        const int i = i0 + lane;
+                        const double v = i < m ? x[i] : 0.0;
+                        const unsigned long long msk = __ballot(v != 0.0);
+                        if (v != 0.0) {
+                            const size_t at = base + run + __popcll(msk & lanemask_lt(lane));
+                            A.sc_row[at] = i;
+                            A.sc_val[at] = v;
+                        }
+                        run += __popcll(msk);
+                    }
+                }
+                if (lane == 0) A.sc_off[(size_t)a * m + c] = off;
+            }
         } else {
             const size_t base = (size_t)A.inter_off[a] + cstart[c];
             int run = 0;
@@ -196,6 +224,48 @@ __global__ __launch_bounds__(kFtThreads) void pg_ftran_kernel(PgArgs A) {
             A.amax[a] = v;
             A.nztot[a] = t;
         }
+    }
+}
+
+// ---- 1b. the kept entries from the first pass's scratch --------------------------------------
+// per column the entries of pg_ftran_kernel<1> (same rows, values and order: the scratch holds
+// the column's nonzeros rows ascending, v != 0, and the drop rule is applied here)
+__global__ __launch_bounds__(kFtThreads) void pg_gather_kernel(PgArgs A) {
+    extern __shared__ double smem[];
+    __shared__ int tmp[kFtThreads];
+    const int a = A.a0 + blockIdx.x, m = A.m, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (!(A.amax[a] >= 0.0) || A.nztot[a] > A.sc_cap) return;   // unusable, or pass 1's source
+    const Src S = src_of(A, a);
+    int *cstart = reinterpret_cast<int *>(smem);
+    unsigned char *touched = reinterpret_cast<unsigned char *>(cstart + m + 1);
+    mark_touched<kFtThreads>(A, S, touched);
+    const int *nzc = A.nzc + (size_t)a * m;
+    block_scan<kFtThreads>(nzc, cstart, m, tmp);
+    const double drop = 1e-14 * A.amax[a];
+    const int *srow = A.sc_row + (size_t)a * A.sc_cap;
+    const double *sval = A.sc_val + (size_t)a * A.sc_cap;
+    for (int c = wv; c < m; c += kFtWaves) {
+        const int n = nzc[c], off = A.sc_off[(size_t)a * m + c];
+        const size_t base = (size_t)A.inter_off[a] + cstart[c];
+        int run = 0;
+        for (int q0 = 0; q0 < n; q0 += 64) {
+            const int q = q0 + lane;
+            int i = 0;
+            double v = 0.0;
+            if (q < n) {
+                i = srow[off + q];
+                v = sval[off + q];
+            }
+            const bool kk = q < n && (touched[i] ? fabs(v) > drop : true);
+            const unsigned long long msk = __ballot(kk);
+            if (kk) {
+                const size_t at = base + run + __popcll(msk & lanemask_lt(lane));
+                A.inter_row[at] = i;
+                A.inter_val[at] = v;
+            }
+            run += __popcll(msk);
+        }
+        if (lane == 0) A.keptc[(size_t)a * m + c] = run;
     }
 }
 
@@ -448,6 +518,7 @@ __global__ __launch_bounds__(kPgThreads) void pg_fill_kernel(PgArgs A, PgFill F)
 static size_t ftran_lds(const PgArgs &A) {
     return sizeof(double) * kFtWaves * A.m + sizeof(int) * (2 * A.kmax + 1 + A.m + 1) + A.m + 16;
 }
+static size_t gather_lds(const PgArgs &A) { return sizeof(int) * (A.m + 1) + A.m + 16; }
 static size_t count_lds(const PgArgs &A) {
     return sizeof(double) * 3 * A.m + sizeof(int) * (3 * A.m + 1) + (A.n + A.m) + 16;
 }
@@ -471,6 +542,10 @@ static hipError_t launch_ftran(const PgArgs &A, int nb, hipStream_t s) {
 }
 hipError_t pg_launch_ftran(const PgArgs &A, int pass, int nb, hipStream_t s) {
     return pass == 0 ? launch_ftran<0>(A, nb, s) : launch_ftran<1>(A, nb, s);
+}
+hipError_t pg_launch_gather(const PgArgs &A, int nb, hipStream_t s) {
+    hipLaunchKernelGGL(pg_gather_kernel, dim3(nb), dim3(kFtThreads), gather_lds(A), s, A);
+    return hipGetLastError();
 }
 hipError_t pg_launch_count(const PgArgs &A, int nb, hipStream_t s) {
     hipLaunchKernelGGL(pg_count_kernel, dim3(nb), dim3(kPgThreads), count_lds(A), s, A);

@@ -168,6 +168,10 @@ struct twosd_ctx {
     long long *d_pg_ioff = nullptr;
     int *d_pg_cnt = nullptr, *d_pg_tot = nullptr, *d_pg_valid = nullptr, *d_pg_head0 = nullptr;
     int *d_pg_map = nullptr, *d_pg_off = nullptr, *d_pg_pos = nullptr;
+    // FTRAN results of the first pass kept for the gather (pool_gpu.hip): per source sc_cap entries
+    int *d_pg_scrow = nullptr, *d_pg_scoff = nullptr;
+    double *d_pg_scval = nullptr;
+    long long pg_sc_cap = 0;                       // entries per source of the last build (0: first build)
     // distributed refresh (twosd_refresh_*): this rank's training keys, its pack of built
     // sources, and the source table gathered from all ranks
     std::vector<unsigned long long> rt_keys;

@@ -99,6 +99,11 @@ struct PgArgs {
     int *rowcnt, *erowcnt;                               // nsrc x m
     int *tot;                                            // nsrc x 4: nnz, element entries, ELL rows, records
     int *valid;                                          // nsrc
+    // the first FTRAN pass keeps its nonzeros (rows ascending per column) in a scratch of sc_cap
+    // entries per source, columns at sc_off (claimed in completion order); a source whose nztot
+    // exceeds sc_cap is left to the second FTRAN pass (sc_cap = 0: every source)
+    long long sc_cap;
+    int *sc_row, *sc_off; double *sc_val;                // nsrc x sc_cap, nsrc x m, nsrc x sc_cap
 };
 struct PgFill {
     int P0, P;                                           // pool bases [P0, P0 + grid) of P
@@ -112,6 +117,7 @@ struct PgFill {
 };
 int pg_supported(int m, int n, int kmax);                // the LDS layouts fit
 hipError_t pg_launch_ftran(const PgArgs &A, int pass, int nb, hipStream_t s);
+hipError_t pg_launch_gather(const PgArgs &A, int nb, hipStream_t s);
 hipError_t pg_launch_count(const PgArgs &A, int nb, hipStream_t s);
 hipError_t pg_launch_fill(const PgArgs &A, const PgFill &F, int np, hipStream_t s);
 

@@ -230,3 +230,55 @@ def test_refresh_training_cap_too_low_is_solved_again():
     assert (st == 0).all()
     assert ctx.lp_stats()[0] / len(vals) < 20   # a pool at x2, not the primary basis alone
     ctx.set_refresh_kcap(0)
+
+
+@pytest.mark.parametrize("mode", ["scratch_small", "two_pass"])
+def test_pool_build_single_ftran_pass_identical(monkeypatch, capfd, mode):
+    """The pool build keeps the first FTRAN pass's nonzeros and gathers the kept entries from
+    them (pg_gather_kernel); sources past the scratch take the second FTRAN pass.  Against the
+    two-pass build (TWOSD_PG_NOSCRATCH) and a scratch so small that only some sources fit
+    (TWOSD_PG_SCCAP), the refreshed pool solves the same scenarios with bit-identical objectives
+    and the same pivots."""
+    from sqlp_amd import smps, twosd
+    inst = I.load("storm")
+    x_ev = I.x_ev("storm")
+    x2 = _sd_x()
+    vals = I.sample("storm", 3000, seed=41)
+    runs = []
+    cap_mid = None
+    for variant in ("default", mode):
+        monkeypatch.delenv("TWOSD_PG_NOSCRATCH", raising=False)
+        monkeypatch.delenv("TWOSD_PG_SCCAP", raising=False)
+        monkeypatch.setenv("TWOSD_DEBUG", "1")
+        if variant == "two_pass":
+            monkeypatch.setenv("TWOSD_PG_NOSCRATCH", "1")
+        elif variant == "scratch_small":     # the mean source: about half of them take pass 1
+            monkeypatch.setenv("TWOSD_PG_SCCAP", str(cap_mid))
+        ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+        ctx.compute_basis(x_ev, smps.mean_values(inst["sto"]))
+        tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+        twosd.add_scenarios(tr, I.sample("storm", 4096, seed=42))
+        ctx.pool_build(tr, x_ev, 0, 4096, 256)
+        ev = twosd.sdEpigraph(ctx, 1.0, 0.0)
+        twosd.add_scenarios(ev, vals)
+        P = ctx.pool_refresh(tr, x2, 0, 4096, 512)
+        P = ctx.pool_refresh(tr, x_ev, 0, 4096, 512)      # the second refresh composes from device-built bases
+        o, _, _, st = twosd.solve_batch(ev, x_ev, 0, len(vals), want_pi=False)
+        it, _ = ctx.last_lp_iters(len(vals))
+        runs.append((P, [ctx.pool_get(p) for p in range(P)], o, st, it))
+        builds = [ln.split() for ln in capfd.readouterr().err.splitlines() if ln.startswith("pg_compute:")]
+        assert len(builds) >= 2
+        # "pg_compute: S sources, Z intermediate entries, largest L, O past the scratch of C"
+        S, Z, O = int(builds[-1][1]), int(builds[-1][3]), int(builds[-1][8])
+        if variant == "default":
+            assert O == 0                    # the scratch (sized by the first build) held every source
+            cap_mid = Z // S
+        elif variant == "scratch_small":
+            assert 0 < O < S                 # some sources, not all, took the second FTRAN pass
+    (P_a, h_a, o_a, st_a, it_a), (P_b, h_b, o_b, st_b, it_b) = runs
+    assert P_a == P_b and P_a > 64
+    for a, b in zip(h_a, h_b):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(st_a, st_b)
+    np.testing.assert_array_equal(o_a, o_b)
+    np.testing.assert_array_equal(it_a, it_b)
