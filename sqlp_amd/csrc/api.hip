@@ -1567,7 +1567,25 @@ static int set_candidates(twosd_ctx *c, int level1, int ncand, int n, const int 
                 c->pool.size(), level1, diff, n, filled);
     }
     int rc;
-    if ((rc = upload_big(c, &c->d_cand, cand))) return rc;
+    int *h = stage_buf<int>(c, 15, cand.size());
+    if (!h) return fail(TWOSD_E_DEVICE, "pool candidates: pinned staging allocation failed");
+    std::copy(cand.begin(), cand.end(), h);
+    if ((rc = dev_reserve(c, &c->d_cand, cand.size()))) return rc;
+    HIPCHK(hipMemcpyAsync(c->d_cand, h, sizeof(int) * cand.size(), hipMemcpyHostToDevice, c->stream));
+    c->pool_l1 = level1;
+    c->pool_ncand = ncand;
+    c->cand_pending = false;
+    return TWOSD_OK;
+}
+
+// the lists are built by the next two-level selection (select_pool), on the host while its
+// level-1 pass runs on the device: same lists, the host time off the critical path
+static int defer_candidates(twosd_ctx *c, int level1, int ncand, std::vector<int> &&p1, std::vector<int> &&pf) {
+    c->cand_p1 = std::move(p1);
+    c->cand_pf = std::move(pf);
+    c->cand_pl1 = level1;
+    c->cand_pnc = ncand;
+    c->cand_pending = true;
     c->pool_l1 = level1;
     c->pool_ncand = ncand;
     return TWOSD_OK;
@@ -1595,7 +1613,7 @@ extern "C" int twosd_pool_set_candidates(twosd_ctx *c, int level1, int ncand, in
     for (int s = 0; s < n; ++s)
         if (p1[s] < 0 || p1[s] >= P || pf[s] < 0 || pf[s] >= P) return fail(TWOSD_E_ARG, "pool_set_candidates: pick outside the pool");
     HIPCHK(hipSetDevice(c->device));
-    return set_candidates(c, level1, ncand, n, p1, pf);
+    return defer_candidates(c, level1, ncand, std::vector<int>(p1, p1 + n), std::vector<int>(pf, pf + n));
 }
 
 extern "C" int twosd_pool_build_candidates(twosd_ctx *c, int epi, const double *x, int first, int count, int level1,
@@ -1612,7 +1630,7 @@ extern "C" int twosd_pool_build_candidates(twosd_ctx *c, int epi, const double *
     std::vector<int> p1(count), pf(count);
     int rc;
     if ((rc = candidate_picks(c, E, x, first, count, level1, p1.data(), pf.data()))) return rc;
-    return set_candidates(c, level1, ncand, count, p1.data(), pf.data());
+    return defer_candidates(c, level1, ncand, std::move(p1), std::move(pf));
 }
 
 extern "C" int twosd_last_pool_picks(twosd_ctx *c, int N, int *picks) {
@@ -2174,7 +2192,7 @@ int twosd::prepare_x(twosd_ctx *c, const double *x) {
 // pick.  npool_override > 0: flat over pool[0, npool_override) (candidate training).
 static int select_pool(twosd_ctx *c, const double *d_dv, int N, int *d_pick, int npool_override) {
     const int P = (int)c->pool.size();
-    const bool two = npool_override <= 0 && c->pool_l1 > 0 && c->pool_l1 < P && c->pool_ncand > 0 && c->d_cand;
+    const bool two = npool_override <= 0 && c->pool_l1 > 0 && c->pool_l1 < P && c->pool_ncand > 0 && (c->d_cand || c->cand_pending);
     const int np1 = npool_override > 0 ? npool_override : two ? c->pool_l1 : P;
     int rc;
     size_t tb = 0, tb2 = 0;
@@ -2207,6 +2225,9 @@ static int select_pool(twosd_ctx *c, const double *d_dv, int N, int *d_pick, int
     S.pkey = g1 > 1 ? c->d_sel_pkey : nullptr;
     S.ppick = g1 > 1 ? c->d_sel_ppick : nullptr;
     HIPCHK(launch_pool_select(S, c->stream));
+    if (two && c->cand_pending &&
+        (rc = set_candidates(c, c->cand_pl1, c->cand_pnc, (int)c->cand_p1.size(), c->cand_p1.data(), c->cand_pf.data())))
+        return rc;
     if (two) {
         HIPCHK(sort_by_pool(d_pick, c->d_order, N, np1, c->d_sort_tmp, &tb, c->stream));
         PoolRefineParams Q{};
@@ -2385,8 +2406,10 @@ int twosd::run_lp_ex(twosd_ctx *c, const double *x, const double *d_dv, int N, c
 
 // batch statistics on the device (integer sums: exact, order independent): [0] pivots,
 // [1] executed FMAs, [2] max pivots, [3] non-optimal scenarios
-__global__ void lp_stats_kernel(int N, const int *__restrict__ its, const long long *__restrict__ ops,
-                                const int *__restrict__ st, const int *__restrict__ etan, unsigned long long *out) {
+__global__ void __launch_bounds__(256) lp_stats_kernel(int N, const int *__restrict__ its, const long long *__restrict__ ops,
+                                                      const int *__restrict__ st, const int *__restrict__ etan,
+                                                      unsigned long long *out) {
+    __shared__ unsigned long long red[4][5];
     unsigned long long a = 0, b = 0, d = 0, e = 0;
     unsigned long long mx = 0;
     for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < N; s += gridDim.x * blockDim.x) {
@@ -2404,7 +2427,16 @@ __global__ void lp_stats_kernel(int N, const int *__restrict__ its, const long l
         const unsigned long long m2 = __shfl_down(mx, o);
         mx = m2 > mx ? m2 : mx;
     }
+    // one set of atomics per block (per wave they serialised on five addresses: ~0.25 ms at 1M)
+    const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
+        red[w][0] = a; red[w][1] = b; red[w][2] = mx; red[w][3] = d; red[w][4] = e;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int v = 1; v < (int)(blockDim.x >> 6); ++v) {
+            a += red[v][0]; b += red[v][1]; mx = red[v][2] > mx ? red[v][2] : mx; d += red[v][3]; e += red[v][4];
+        }
         atomicAdd(&out[0], a);
         atomicAdd(&out[1], b);
         atomicMax(&out[2], mx);
@@ -2453,7 +2485,7 @@ static int copy_lp_outputs(twosd_ctx *c, int N, double *obj, double *pi, double 
         if (rc) return rc;
     }
     HIPCHK(hipMemsetAsync(c->d_lpstats, 0, 5 * sizeof(unsigned long long), c->stream));
-    hipLaunchKernelGGL(lp_stats_kernel, dim3((unsigned)std::min(1024, (N + 255) / 256)), dim3(256), 0, c->stream, N,
+    hipLaunchKernelGGL(lp_stats_kernel, dim3((unsigned)std::min(256, (N + 255) / 256)), dim3(256), 0, c->stream, N,
                        c->d_iters, c->d_ops, c->d_status, c->d_etan, c->d_lpstats);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(lp_obj_kernel, dim3(kObjBlocks), dim3(256), 0, c->stream, N, c->d_obj, d_w, c->d_objpart);

@@ -28,39 +28,41 @@ namespace twosd {
 // has-NaN flag.  The sequential sum is a dependent chain per vector, so each lane walks
 // its own vector; the block's 256 vectors are staged through LDS 16 columns at a time
 // (coalesced 128-byte row segments in, conflict-free stride-17 reads out).
-constexpr int kKeyCols = 16;
-__global__ void __launch_bounds__(256) dvs_key_kernel(int count, int m, const double *__restrict__ pis,
-                                                      uint64_t *__restrict__ hash, uint64_t *__restrict__ fp,
-                                                      int *__restrict__ nanflag) {
-    __shared__ double tile[256 * (kKeyCols + 1)];
-    const int c0 = blockIdx.x * 256;
-    const int c = c0 + threadIdx.x;
-    double acc = 0.0;               // sequential sum in index order (dual_set.jl:47-50)
+// one wavefront per vector: the lanes load the row coalesced and fold the order-independent
+// parts (fingerprint sum, NaN flag); |pi_i| goes through LDS and lane 0 adds it in index order
+// (the reference's sequential sum, dual_set.jl:47-50, so the same bits).  Round 3 used one
+// thread per vector: a push of ~4k vectors occupied 16 CUs for ~0.26 ms.
+constexpr int kKeyWaves = 4;
+__global__ void __launch_bounds__(64 * kKeyWaves) dvs_key_kernel(int count, int m, const double *__restrict__ pis,
+                                                               uint64_t *__restrict__ hash, uint64_t *__restrict__ fp,
+                                                               int *__restrict__ nanflag) {
+    extern __shared__ double kabs[];   // kKeyWaves x m
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * kKeyWaves + w;
+    if (c >= count) return;            // whole wavefronts; no block barrier below
+    double *a = kabs + (size_t)w * m;
+    const double *p = pis + (size_t)c * m;
     uint64_t f = 0;
     int hasnan = 0;
-    for (int i0 = 0; i0 < m; i0 += kKeyCols) {
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < kKeyCols; ++u) {
-            // element u*256 + t of the chunk: vector (u*256+t)/16, column (u*256+t)%16
-            const int q = u * 256 + threadIdx.x, vr = q / kKeyCols, col = q % kKeyCols;
-            const int cv = c0 + vr, i = i0 + col;
-            tile[vr * (kKeyCols + 1) + col] = (cv < count && i < m) ? pis[(size_t)cv * m + i] : 0.0;
-        }
-        __syncthreads();
-        const int lim = min(kKeyCols, m - i0);
-        for (int col = 0; col < lim; ++col) {
-            const double v = tile[threadIdx.x * (kKeyCols + 1) + col];
-            hasnan |= isnan(v);
-            f += mix64(comp_bits(v) ^ (0xD6E8FEB86659FD93ull * (uint64_t)(i0 + col + 1)));
-            acc += fabs(v);
-        }
+    for (int i = lane; i < m; i += 64) {
+        const double v = p[i];
+        hasnan |= isnan(v);
+        f += mix64(comp_bits(v) ^ (0xD6E8FEB86659FD93ull * (uint64_t)(i + 1)));
+        a[i] = fabs(v);
     }
-    if (c >= count) return;
-    const uint64_t h = (uint64_t)__double_as_longlong(round16(acc));
-    hash[c] = h;
-    fp[c] = mix64(f ^ h);
-    nanflag[c] = hasnan;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) f += __shfl_xor(f, o);
+    hasnan = __any(hasnan);
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // this wave's LDS writes done (lgkmcnt 0)
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+        double acc = 0.0;
+        for (int i = 0; i < m; ++i) acc += a[i];
+        const uint64_t h = (uint64_t)__double_as_longlong(round16(acc));
+        hash[c] = h;
+        fp[c] = mix64(f ^ h);
+        nanflag[c] = hasnan;
+    }
 }
 
 // full key equality of candidate row a (hash ha) and row b (hash hb); one wavefront
@@ -318,8 +320,8 @@ int dvs_push_device(twosd_ctx *c, int count, const double *d_pis, int *d_out_ind
         HIPCHK(hipMemcpyAsync(w->cfp, d_fp, sizeof(uint64_t) * count, hipMemcpyDeviceToDevice, c->stream));
         HIPCHK(hipMemcpyAsync(w->nanflag, d_nan, sizeof(int) * count, hipMemcpyDeviceToDevice, c->stream));
     } else {
-        hipLaunchKernelGGL(dvs_key_kernel, dim3((count + 255) / 256), dim3(256), 0, c->stream, count, m, d_pis, w->chash,
-                           w->cfp, w->nanflag);
+        hipLaunchKernelGGL(dvs_key_kernel, dim3((count + kKeyWaves - 1) / kKeyWaves), dim3(64 * kKeyWaves),
+                           sizeof(double) * kKeyWaves * m, c->stream, count, m, d_pis, w->chash, w->cfp, w->nanflag);
     }
     hipLaunchKernelGGL(dvs_lookup_kernel, dim3(nb), dim3(256), 0, c->stream, count, m, d_pis, w->chash, w->cfp,
                        w->nanflag, D.V, D.hash, D.fp, D.table, D.tcap - 1, w->out);

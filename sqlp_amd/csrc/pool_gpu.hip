@@ -237,15 +237,16 @@ __global__ __launch_bounds__(kFtThreads) void pg_gather_kernel(PgArgs A) {
     if (!(A.amax[a] >= 0.0) || A.nztot[a] > A.sc_cap) return;   // unusable, or pass 1's source
     const Src S = src_of(A, a);
     int *cstart = reinterpret_cast<int *>(smem);
-    unsigned char *touched = reinterpret_cast<unsigned char *>(cstart + m + 1);
+    int *soff = cstart + m + 1;                           // scratch offsets, staged once
+    unsigned char *touched = reinterpret_cast<unsigned char *>(soff + m);
+    for (int c = tid; c < m; c += kFtThreads) soff[c] = A.sc_off[(size_t)a * m + c];
     mark_touched<kFtThreads>(A, S, touched);
-    const int *nzc = A.nzc + (size_t)a * m;
-    block_scan<kFtThreads>(nzc, cstart, m, tmp);
+    block_scan<kFtThreads>(A.nzc + (size_t)a * m, cstart, m, tmp);
     const double drop = 1e-14 * A.amax[a];
     const int *srow = A.sc_row + (size_t)a * A.sc_cap;
     const double *sval = A.sc_val + (size_t)a * A.sc_cap;
     for (int c = wv; c < m; c += kFtWaves) {
-        const int n = nzc[c], off = A.sc_off[(size_t)a * m + c];
+        const int n = cstart[c + 1] - cstart[c], off = soff[c];
         const size_t base = (size_t)A.inter_off[a] + cstart[c];
         int run = 0;
         for (int q0 = 0; q0 < n; q0 += 64) {
@@ -518,7 +519,7 @@ __global__ __launch_bounds__(kPgThreads) void pg_fill_kernel(PgArgs A, PgFill F)
 static size_t ftran_lds(const PgArgs &A) {
     return sizeof(double) * kFtWaves * A.m + sizeof(int) * (2 * A.kmax + 1 + A.m + 1) + A.m + 16;
 }
-static size_t gather_lds(const PgArgs &A) { return sizeof(int) * (A.m + 1) + A.m + 16; }
+static size_t gather_lds(const PgArgs &A) { return sizeof(int) * (2 * A.m + 1) + A.m + 16; }
 static size_t count_lds(const PgArgs &A) {
     return sizeof(double) * 3 * A.m + sizeof(int) * (3 * A.m + 1) + (A.n + A.m) + 16;
 }

@@ -81,6 +81,11 @@ struct twosd_ctx {
     // level 2 over the candidate bases of the level-1 pick (d_cand: pool_l1 x pool_ncand)
     int pool_l1 = 0, pool_ncand = 0;
     int *d_cand = nullptr;
+    // candidate lists of the last refresh, built on the host by the next two-level selection while
+    // its level-1 pass runs (select_pool); pool_l1 / pool_ncand already describe them
+    std::vector<int> cand_p1, cand_pf;
+    int cand_pl1 = 0, cand_pnc = 0;
+    bool cand_pending = false;
     int *d_cpick = nullptr;       // candidate picks of the training scenarios (grow-only)
     float *d_sel_key = nullptr;
     float *d_sel_pkey = nullptr;          // chunked selection partials (split x N)
