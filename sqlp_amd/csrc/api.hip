@@ -1954,7 +1954,19 @@ __global__ void pool_xbase_kernel(int P, int MP, const int *__restrict__ brptr, 
     const size_t p = t / MP, i = t - p * MP;
     const int *rp = brptr + p * (MP + 1);
     double s = 0.0;
-    for (int q = rp[i]; q < rp[i + 1]; ++q) s = fma(brval[q], b[brcol[q]], s);
+    int q = rp[i];
+    const int q1 = rp[i + 1];
+    // four entries' loads in flight together; the fmas stay in column order (same bits)
+    for (; q + 4 <= q1; q += 4) {
+        const int c0 = brcol[q], c1 = brcol[q + 1], c2 = brcol[q + 2], c3 = brcol[q + 3];
+        const double v0 = brval[q], v1 = brval[q + 1], v2 = brval[q + 2], v3 = brval[q + 3];
+        const double b0 = b[c0], b1 = b[c1], b2 = b[c2], b3 = b[c3];
+        s = fma(v0, b0, s);
+        s = fma(v1, b1, s);
+        s = fma(v2, b2, s);
+        s = fma(v3, b3, s);
+    }
+    for (; q < q1; ++q) s = fma(brval[q], b[brcol[q]], s);
     xbase[t] = s;
 }
 
