@@ -102,7 +102,9 @@ int twosd_pool_build(twosd_ctx *ctx, int epi, const double *x, int first, int co
  * that a flat selection over the whole pool picks most often for the training scenarios
  * [first, first+count) of epi at x sharing the level-1 pick.  Cuts the selection cost of a
  * large pool to about that of its first level1 bases.  level1 = 0: flat selection;
- * ncand <= 1024.  Reset by any change of the pool. */
+ * ncand <= 1024.  Reset by any change of the pool.  The lists themselves are counted on the
+ * host by the next two-level selection while its level-1 pass runs (twosd_pool_set_candidates
+ * likewise): an allocation failure of their upload is reported by that solve. */
 int twosd_pool_build_candidates(twosd_ctx *ctx, int epi, const double *x, int first, int count, int level1,
                                 int ncand);
 /* Rebuild the pool at x: solve the training scenarios [first, first+count) of epi at x from
