@@ -171,8 +171,11 @@ constexpr int kLdsRow2 = 32;             // doubles per k-row of a chunk
 // two k-rows a half-wave reads together (g = 0, 1 / 2, 3) fall on disjoint banks
 __device__ __forceinline__ int lds2(int kk, int vv) { return kk * kLdsRow2 + (vv ^ ((kk & 1) << 4)); }
 
+#ifndef TWOSD_CUT_LB3
+#define TWOSD_CUT_LB3 1                  // 3 blocks per CU for KB <= 22 (168 VGPRs; ssn: 62 -> 76 % of the roofline)
+#endif
 template <int KB>
-__global__ void __launch_bounds__(256, 2) cut_argmax2_kernel(CutParams P) {
+__global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_argmax2_kernel(CutParams P) {
     __shared__ double Bs[2][4 * KB * kLdsRow2];     // double-buffered chunk (k-major)
     __shared__ double bs[2][kVT2];
     extern __shared__ unsigned long long hl[];      // nv entries when P.hist_lds
