@@ -147,3 +147,24 @@ def test_empty_vertex_set_raises():
     twosd.add_scenarios(epi, I.sample("lands", 4, 1))
     with pytest.raises(TwoSDError):            # UndefRefError in build_sasa_cut (epigraph.jl:140)
         twosd.build_sasa_cut(epi, I.x_ev("lands"), twosd.sdDualVertexSet(ctx))
+
+
+def test_cut_ssn_full_rounds_three_blocks_per_cu():
+    """ssn's 22 k-blocks run the cut kernel at 3 blocks per CU; at 120k scenarios (938 tiles) the
+    persistent grid runs whole-tile rounds and then the vertex-split tail.  Against the C oracle:
+    the same argmax (tolerance rule), alpha and beta to 1e-8."""
+    from oracle import cpu
+    from sqlp_amd import twosd
+    ctx, x, V = _setup("ssn", nv_src=768)
+    N = 120_000
+    vals = I.sample("ssn", N, seed=29)
+    w = np.random.default_rng(7).uniform(0.5, 1.5, size=N)
+    epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(epi, vals, w)
+    cut, mv, ma = twosd._build_cut(epi, x, 1e-12, want_argmax=True)
+    sp = I.load("ssn")["osp2"]
+    a, b, omv, oma = cpu.build_cut(sp.r, sp.T, x, V.matrix(), ctx.rows, vals - sp.r[ctx.rows], w, tie_rel=1e-12, nthreads=8)
+    assert (ma == oma).mean() > 0.999
+    np.testing.assert_allclose(mv, omv, rtol=1e-10, atol=1e-9)
+    assert cut.alpha == pytest.approx(a, rel=1e-8, abs=1e-8)
+    np.testing.assert_allclose(cut.beta, b, rtol=1e-8, atol=1e-8 * (1 + np.abs(b).max()))
