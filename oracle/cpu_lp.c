@@ -432,7 +432,15 @@ int oracle_lp_solve_batch(void *p, int N, int k, const int *rows, const double *
  * argmax_procedure + build_sasa_cut in reference loop order for RHS-only scenarios.
  *   base_rhs = r (m), T (m x n1 row-major), x (n1), V (nv x m row-major),
  *   scenario s: dr = DR[s,:] on rows[]; weights w[s].
- * Scores are computed as the reference does: dot(pi, r - T x) + dot(pi, dvec).
+ * Scores are computed as the reference does: dot(pi, r - T x) + dot(pi, dvec)
+ * (subprob.jl:147-155), each dot sequential in row order with every product and sum rounded
+ * on its own (built with -ffp-contract=off): base[i] = r[i] - T[i][0] x[0] - ...;
+ * vb[v] = sum_i pi[i] base[i]; t = sum over the random rows in ascending order of
+ * pi[row] dvec[row] (the zero rows of the dense dvec add exactly nothing).  This is the
+ * arithmetic every tie decision of the build is pinned to (the GPU re-decides rows with
+ * several vertices within its error band in exactly this order).  The reference's own
+ * OpenBLAS ddot sums in a CPU-dependent blocked order, so its picks at rounding-level ties
+ * cannot be pinned by any restatement.
  * tie_rel == 0: strict '>' (first max); > 0: lowest index within tie_rel*(1+|max|).
  */
 void oracle_build_cut(int m, int n1, int nv, int N, int k, const int *rows, const double *r, const double *T,
@@ -442,6 +450,13 @@ void oracle_build_cut(int m, int n1, int nv, int N, int k, const int *rows, cons
     for (int i = 0; i < m; ++i) { double s = r[i]; for (int j = 0; j < n1; ++j) s -= T[(size_t)i * n1 + j] * x[j]; base[i] = s; }
     double *vb = (double *)malloc(sizeof(double) * (nv ? nv : 1));
     for (int v = 0; v < nv; ++v) { double s = 0; for (int i = 0; i < m; ++i) s += V[(size_t)v * m + i] * base[i]; vb[v] = s; }
+    /* elements by ascending row (element order within a row): insertion sort, k is small */
+    int *ord = (int *)malloc(sizeof(int) * (k ? k : 1));
+    for (int j = 0; j < k; ++j) {
+        int q = j;
+        while (q > 0 && rows[ord[q - 1]] > rows[j]) { ord[q] = ord[q - 1]; --q; }
+        ord[q] = j;
+    }
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #endif
@@ -454,7 +469,7 @@ void oracle_build_cut(int m, int n1, int nv, int N, int k, const int *rows, cons
             double M = -INFINITY; int arg = -1;
             for (int v = 0; v < nv; ++v) {
                 const double *pv = V + (size_t)v * m; double t = 0;
-                for (int j = 0; j < k; ++j) t += pv[rows[j]] * d[j];
+                for (int q = 0; q < k; ++q) { const int j = ord[q]; t += pv[rows[j]] * d[j]; }
                 sc[v] = vb[v] + t;
                 if (sc[v] > M) { M = sc[v]; arg = v; }
             }
@@ -479,7 +494,7 @@ void oracle_build_cut(int m, int n1, int nv, int N, int k, const int *rows, cons
         for (int j = 0; j < n1; ++j) { double c = 0; for (int i = 0; i < m; ++i) c += T[(size_t)i * n1 + j] * pv[i]; beta[j] += -p * c; }
     }
     *alpha = a;
-    free(g); free(base); free(vb);
+    free(g); free(base); free(vb); free(ord);
 }
 
 /* ================= warm-start pool (CPU counterpart of the GPU basis pool) ================= */

@@ -136,18 +136,45 @@ def tie_tolerance(M: float, rel: float) -> float:
     return rel * (1.0 + abs(M))
 
 
+def _seq_base(coef: Coefficients, x):
+    """r - T x as oracle_build_cut forms it: r[i], then minus T[i, j] x[j] for j = 0, 1, ...,
+    each product and difference rounded on its own."""
+    prod = coef.transfer * x[None, :]
+    base = np.array(coef.rhs, dtype=np.float64)
+    for j in range(prod.shape[1]):
+        base = base - prod[:, j]
+    return base
+
+
+def _seq_rowdot(A, b):
+    """sum_i A[v, i] b[i] for every row v, in index order (np.cumsum adds sequentially; the
+    products are rounded first: no contraction)."""
+    if A.shape[1] == 0:
+        return np.zeros(A.shape[0])
+    return np.cumsum(A * b[None, :], axis=1)[:, -1]
+
+
 def argmax_procedure(coef: Coefficients, deltas, x, V, tie_rel: float = 0.0):
     """subprob.jl:141-169 (MIN_SENSE).  tie_rel == 0 is the reference rule exactly (strict
     '>' so the first maximum in insertion order wins).  tie_rel > 0 is the build's
     documented near-tie rule: the lowest vertex index whose score is within
-    tie_rel*(1+|max|) of the maximum."""
+    tie_rel*(1+|max|) of the maximum.
+    Scores s = dot(pi, r - T x) + dot(pi, dvec) (:147-155) with both dots sequential in row order
+    and no contraction -- oracle_build_cut's arithmetic, which the GPU's decisions are pinned to
+    (dvec's zero rows are dropped: adding an exact 0 changes nothing).  The reference's OpenBLAS
+    ddot adds in a CPU-dependent blocked order, so at rounding-level ties its pick is not
+    reproducible by any restatement."""
     x = np.asarray(x, dtype=np.float64)
-    base = coef.rhs - coef.transfer @ x
+    base = _seq_base(coef, x)
     Vl = list(V)
     vals, args = [], []
+    Vm = np.array(Vl, dtype=np.float64).reshape(len(Vl), -1)
+    vb = _seq_rowdot(Vm, base)
     for dr, dT in deltas:
         dvec = dr - dT @ x
-        scores = [float(np.dot(p, base) + np.dot(p, dvec)) for p in Vl]
+        nz = np.flatnonzero(dvec)
+        t = _seq_rowdot(Vm[:, nz], dvec[nz]) if len(nz) else np.zeros(len(Vl))
+        scores = [float(s) for s in (vb + t)]
         if tie_rel == 0.0:
             best, arg = -math.inf, -1
             for i, s in enumerate(scores):

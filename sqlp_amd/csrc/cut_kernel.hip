@@ -7,6 +7,19 @@
 //                = base[v]          +  (DR_w . PK_v)           (an N x |V| x k GEMM)
 //     a(w)  = lowest v within tie_rel*(1+|max|) of max_v score[w,v]   (tie_rel=0: the
 //             reference's strict '>' first maximum)
+// The DECISION is made on scores evaluated in the restatement's arithmetic order
+// (oracle/cpu_lp.c oracle_build_cut; subprob.jl:147-158 with the dots sequential, no
+// contraction): base[v] = sum_i pi_v[i] * bvec[i] in index order, then
+// score = base[v] + (sum_e pi_v[row_e] * (coef_e dv[w,e]) in element order).  The MFMA pass
+// computes every score to within a bound `band` of that value (both share base[v]; the
+// k-term dot differs by at most 2 gamma_{k+4} sum|terms|), so a row whose band around the
+// MFMA maximum holds ONE vertex is decided; a row with several (real ties: degenerate
+// scenarios whose optimal duals are all in V) is re-decided by cut_fixup_kernel, which
+// evaluates the logged in-band candidates in the restatement's order -- the same pick as the
+// C port, bit for bit, at any tie.
+//   candidate log: while a lane scans its vertices it appends every vertex whose MFMA score
+//   reaches the running band [M - tol(M) - band, ...]; the band's floor only rises with M, so
+//   the log is a superset of the final band (a jump past the band restarts it).
 //     p_w   = weight_w / total_weight
 //     alpha = g.r + sum_{e RHS} S_e,   beta = -T' g - sum_{e T} S_e e_{col_e}
 // with g = sum_v h_v pi_v,  h_v = sum_{w: a(w)=v} p_w,  S_e = sum_w p_w PK[a(w),e] dv[w,e].
@@ -14,7 +27,8 @@
 //
 // Kernels:
 //   cut_pk_kernel      PK (|V| x k4 row-major) and PKT (k4 x vcap) gathers of new vertices
-//   cut_vbase_kernel   base[v] = pi_v . (r - T x)                (8|V|(m+1) bytes)
+//   cut_vbase_kernel   base[v] = pi_v . (r - T x) in index order (8|V|(m+1) bytes) and the
+//                      decision band (max_v |base[v]| + sum_e |PK[v,e] coef_e| dmax_e)
 //   cut_pktc_kernel    PKTc = coef(x) * PKT plus the base row: the chunk source of the argmax
 //   cut_argmax2_kernel MFMA score tiles (v_mfma_f64_16x16x4f64: 32 vertices x 32 scenarios
 //                      per wave and chunk), vertex chunks DMA'd into LDS, running max/argmax
@@ -22,8 +36,8 @@
 //                      fixed-point atomics (exact and order independent -> identical on any
 //                      rank count); the last round's tiles split by vertex range
 //   cut_tail_merge_kernel  per-range results of the split tiles merged in vertex order
-//   cut_fixup_kernel   scenarios whose running argmax slid within the tolerance band are
-//                      re-decided by the exact two-pass rule (sequential fp64)
+//   cut_fixup_kernel   scenarios with several vertices in the decision band: their logged
+//                      candidates re-scored in the restatement's order and decided by its rule
 //   cut_reduce_kernel  deterministic fixed-order sum of the partial slots
 //   cut_g_kernel(s)    g = sum_v h_v pi_v (two-level, fixed order)
 #include <hip/hip_runtime.h>
@@ -52,19 +66,26 @@ struct CutParams {
     const double *PKT;     // k4 x vcap
     const double *PKTc;    // 4 KB x vcap32: coef_e(x) * PKT, zero padded (cut_argmax2_kernel's LDS-DMA source)
     int vcap32;            // row stride of PKTc (a multiple of 32 >= nv)
-    const double *base;    // nv
-    int *arg; double *val; int *flag;   // N
+    const double *base;    // nv: pi_v . bvec in index order (the restatement's base dot)
+    const int *eord;       // k: elements by ascending row (the restated score's order)
+    const unsigned long long *band_bits;   // max_v (|base[v]| + sum_e |PK[v,e] coef_e| dmax_e), as bits
+    double band_scale;     // band = band_scale * that maximum (4 gamma_{k+4}: twice the 2 gamma bound)
+    int *arg; double *val; int *flag;   // N; flag != 0: re-decide (main rows: 4-bit log counts per lane group)
+    int *cand;             // candidate logs of the whole tiles: [(s * 4 + g) * kCandC + i]
+    int *tcand;            // of the tail ranges: [(((s - t0) * tail_S + range) * 4 + g) * kCandC + i]
     unsigned long long *hist;           // nv (fixed point)
     unsigned long long *hist_part;      // gridDim.x x nv block histograms (hist_lds mode)
     double *partial;       // slots x (k + 1): [sum p*val, S_0..S_{k-1}]
     // work units of cut_argmax2_kernel: units [0, full_units) are whole scenario tiles; the
     // tiles past them (the last, partial round of the persistent grid) are cut into tail_S
-    // vertex ranges each, and such a unit leaves its per-scenario (M, SV, I, F) in tp_* at
+    // vertex ranges each, and such a unit leaves its per-scenario (M, I, log counts) in tp_* at
     // [(s - 128 full_units) tail_S + range] for cut_tail_merge_kernel
     int full_units, tail_S;
-    double *tp_m, *tp_sv;
+    double *tp_m;
     int *tp_i, *tp_f;
 };
+
+constexpr int kCandC = 8;          // logged candidates per (scenario, lane group); count kCandC + 1 = overflow
 
 __global__ void cut_pk_kernel(int from, int to, int m, int k, int k4, int vcap, const int *__restrict__ rows,
                               const double *__restrict__ V, double *__restrict__ PK, double *__restrict__ PKT) {
@@ -92,47 +113,84 @@ __global__ void cut_pktc_kernel(int nv, int k, int rows, int vcap, int vcap32, c
     }
 }
 
-__global__ void __launch_bounds__(256) cut_vbase_kernel(int nv, int m, const double *__restrict__ V,
-                                                        const double *__restrict__ bvec, double *__restrict__ base) {
-    const int lane = threadIdx.x & 63;
-    const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int nw = (gridDim.x * blockDim.x) >> 6;
-    for (int v = gw; v < nv; v += nw) {
-        const double *p = V + (size_t)v * m;
+// base[v] = sum_i V[v][i] * bvec[i] in index order with every product and sum rounded on its
+// own (oracle_build_cut's vb[v]), one wavefront per vertex: the lanes form the products of a
+// 512-entry slice in LDS, lane 0 adds them in order.  The wave also folds the vertex's term of
+// the decision band: |base[v]| + sum_e |PK[v,e] coef_e| dmax_e (any order: a bound).
+constexpr int kVbSlice = 512;
+__global__ void __launch_bounds__(256) cut_vbase_kernel(int nv, int m, int k, int k4, const double *__restrict__ V,
+                                                        const double *__restrict__ bvec, const double *__restrict__ PK,
+                                                        const double *__restrict__ coef, const unsigned long long *__restrict__ dmax,
+                                                        double *__restrict__ base, unsigned long long *__restrict__ band_bits) {
+#pragma clang fp contract(off)
+    __shared__ double prod[4][kVbSlice];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int v0 = blockIdx.x * 4; v0 < nv; v0 += gridDim.x * 4) {   // block-uniform trip count
+        const int v = v0 + wid;
+        const bool act = v < nv;
+        const double *p = V + (size_t)(act ? v : 0) * m;
         double s = 0.0;
-        for (int i = lane; i < m; i += 64) s = fma(p[i], bvec[i], s);
+        for (int i0 = 0; i0 < m; i0 += kVbSlice) {
+            const int n = min(kVbSlice, m - i0);
+            if (act)
+                for (int i = lane; i < n; i += 64) prod[wid][i] = p[i0 + i] * bvec[i0 + i];
+            __syncthreads();
+            if (act && lane == 0) {
+#pragma unroll 8
+                for (int i = 0; i < n; ++i) s = s + prod[wid][i];
+            }
+            __syncthreads();
+        }
+        if (!act) continue;
+        double a = 0.0;
+        for (int e = lane; e < k; e += 64)
+            a += fabs(PK[(size_t)v * k4 + e] * coef[e]) * __longlong_as_double((long long)dmax[e]);
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-        if (lane == 0) base[v] = s;
+        for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+        if (lane == 0) {
+            base[v] = s;
+            const double t = fabs(s) + a;
+            atomicMax(band_bits, (unsigned long long)__double_as_longlong(isfinite(t) ? t : INFINITY));
+        }
     }
 }
 
-__device__ __forceinline__ double tolf(double M, double rel) { return rel * (1.0 + fabs(M)); }
-
-// Running (max, argmax) of one scenario row over the vertices one lane sees, in increasing
-// vertex order: M = max so far, I = lowest vertex within tolf(M) of M, SV = its score,
-// F = the exact rule cannot be decided from this state (left to cut_fixup_kernel).
-struct RowBest { double M, SV; int I, F; };
-
-__device__ __forceinline__ void row_update(RowBest &b, double s, int v, double rel) {
-    if (s == -INFINITY) return;
-    if (b.M == -INFINITY || s > b.M + tolf(b.M, rel)) {
-        // a new max beyond the old band; if the old candidate still lies within the new
-        // band the lowest-index rule would keep it -> flag (rare: scores 1e-12 apart)
-        if (b.M != -INFINITY && b.SV >= s - tolf(s, rel)) b.F = 1;
-        b.M = s; b.I = v; b.SV = s;
-    } else if (s > b.M) {
-        // max slides up inside the band: the candidate must stay within the new band
-        if (!(b.SV >= s - tolf(s, rel))) b.F = 1;
-        b.M = s;
-    }
-    // s within the band but not above M: a later (higher) index never wins
+// dmax[e] = max |dv[s][e]| over scenarios [from, to) folded into the epigraph's running maximum
+// (non-negative doubles order as their bit patterns)
+__global__ void __launch_bounds__(256) cut_dmax_kernel(int from, int to, int k, const double *__restrict__ dv,
+                                                       unsigned long long *__restrict__ dmax) {
+    if ((int)threadIdx.x >= k) return;
+    const int e = threadIdx.x;
+    double mx = 0.0;
+    for (int s = from + blockIdx.x; s < to; s += gridDim.x) mx = fmax(mx, fabs(dv[(size_t)s * k + e]));   // NaN ignored: its scores never win
+    atomicMax(&dmax[e], (unsigned long long)__double_as_longlong(mx));
 }
 
-// the same update behind its only trigger: every action needs s > M (M = -inf takes any
-// finite s), so the common case is one compare
-__device__ __forceinline__ void row_update_fast(RowBest &b, double s, int v, double rel) {
-    if (__builtin_expect(s > b.M, 0)) row_update(b, s, v, rel);
+// floor of the decision band around a running maximum M: a vertex below it cannot be the
+// restatement's pick (monotone in M for tie_rel < 1)
+__device__ __forceinline__ double band_floor(double M, double rel, double band) { return M - (rel * (1.0 + fabs(M)) + band); }
+
+// Running state of one scenario row over the vertices one lane sees, in increasing vertex
+// order: M = max so far, thr = band_floor(M), I = the first vertex scoring M, n = entries in
+// this lane's candidate log (kCandC + 1: overflowed).
+struct RowEx { double M, thr; int I, n; };
+
+// s >= thr: s enters the band of the running max (or raises it)
+__device__ __forceinline__ void row_log(RowEx &b, double s, int v, double rel, double band, int *log) {
+    if (s == -INFINITY) return;                  // padding vertices (-inf base row) never enter
+    const double tn = band_floor(s, rel, band);
+    if (tn > b.M) {                              // every earlier entry is below the band for good
+        log[0] = v;
+        b.n = 1;
+    } else {
+        if (b.n < kCandC) log[b.n] = v;
+        b.n = min(b.n + 1, kCandC + 1);
+    }
+    if (s > b.M) { b.M = s; b.I = v; b.thr = tn; }
+}
+
+__device__ __forceinline__ void row_fast(RowEx &b, double s, int v, double rel, double band, int *log) {
+    if (__builtin_expect(s >= b.thr, 0)) row_log(b, s, v, rel, band, log);
 }
 
 // ---- v2: the score tile transposed -- MFMA A operand = the staged vertex chunk, B operand =
@@ -149,20 +207,6 @@ __device__ __forceinline__ void row_update_fast(RowBest &b, double s, int v, dou
 #ifndef TWOSD_CUT_SB
 #define TWOSD_CUT_SB 1                   // scheduling barrier between the groups
 #endif
-#ifndef TWOSD_CUT_FASTRU
-#define TWOSD_CUT_FASTRU 1               // row updates behind the s > M test
-#endif
-#if TWOSD_CUT_FASTRU
-#define RU2 row_update_fast
-#else
-#define RU2 row_update
-#endif
-#ifndef TWOSD_CUT_BASEK
-#define TWOSD_CUT_BASEK 1                // vertex base as an extra k-row of the chunk (no VALU add)
-#endif
-#ifndef TWOSD_CUT_PF
-#define TWOSD_CUT_PF 0                   // read the next group's fragments before this group's MFMAs
-#endif
 constexpr int kVT2 = 32;                 // vertices per LDS chunk (two 16-vertex MFMA tiles)
 constexpr int kCutTile2 = 128;           // scenarios per block tile (4 waves x 2 x 16)
 constexpr int kLdsRow2 = 32;             // doubles per k-row of a chunk
@@ -171,13 +215,37 @@ constexpr int kLdsRow2 = 32;             // doubles per k-row of a chunk
 // two k-rows a half-wave reads together (g = 0, 1 / 2, 3) fall on disjoint banks
 __device__ __forceinline__ int lds2(int kk, int vv) { return kk * kLdsRow2 + (vv ^ ((kk & 1) << 4)); }
 
+// Combine the 4 lanes (g) of a scenario column: the row maximum M, and for each lane the number
+// of its logged entries that can lie in the band of M (0 when the lane's own max is below the
+// band floor).  tot == 1: the row is decided, its pick the first vertex of the one lane that
+// reaches the band; otherwise the row is re-decided from the logs, whose lengths `pack` holds
+// (4 bits per lane group; kCandC + 1 = overflowed).  Every lane of the column ends with the result.
+__device__ __forceinline__ void combine_ex(RowEx &rb, double rel, double band, int g, int &pack, int &tot) {
+    double M = rb.M;
+    M = fmax(M, __shfl_xor(M, 16));
+    M = fmax(M, __shfl_xor(M, 32));
+    const double thr = band_floor(M, rel, band);
+    const int n = (rb.M != -INFINITY && rb.M >= thr) ? rb.n : 0;
+    int pk = n << (4 * g);
+    tot = n;
+    int it = n ? rb.I : 0x7fffffff;
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) {
+        tot += __shfl_xor(tot, o);
+        pk |= __shfl_xor(pk, o);
+        it = min(it, __shfl_xor(it, o));
+    }
+    rb.M = M;
+    rb.I = (M == -INFINITY || it == 0x7fffffff) ? -1 : it;
+    pack = pk;
+}
+
 #ifndef TWOSD_CUT_LB3
 #define TWOSD_CUT_LB3 1                  // 3 blocks per CU for KB <= 22 (168 VGPRs; ssn: 62 -> 76 % of the roofline)
 #endif
 template <int KB>
 __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_argmax2_kernel(CutParams P) {
     __shared__ double Bs[2][4 * KB * kLdsRow2];     // double-buffered chunk (k-major)
-    __shared__ double bs[2][kVT2];
     extern __shared__ unsigned long long hl[];      // nv entries when P.hist_lds
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar staging loop
@@ -187,6 +255,8 @@ __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_
     const int ntiles = (P.N + kCutTile2 - 1) / kCutTile2;
     const int nchunks = (P.nv + kVT2 - 1) / kVT2;
     const int nunits = P.full_units + (ntiles - P.full_units) * P.tail_S;
+    const double band = P.band_scale * __longlong_as_double((long long)*P.band_bits);
+    const double rel = P.tie_rel;
     double pv_sum = 0.0;
     double Sacc[2] = {0.0, 0.0};   // lane (g, j): e = 4 kb + g for kb = j, j + 16
 
@@ -207,17 +277,20 @@ __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_
             const int sa = s0 + j, sb = s0 + 16 + j;
             a0[kb] = (sa < P.N && e < P.k) ? P.dv[(size_t)sa * P.k + e] : 0.0;
             a1[kb] = (sb < P.N && e < P.k) ? P.dv[(size_t)sb * P.k + e] : 0.0;
-            if (TWOSD_CUT_BASEK && e == P.k) a0[kb] = a1[kb] = 1.0;   // x the base row of the chunk
+            if (e == P.k) a0[kb] = a1[kb] = 1.0;   // x the base row of the chunk
         }
-        RowBest rb0, rb1;   // scenario s0 + j / s0 + 16 + j over this lane's vertices v0 + g + 4r (+16)
-        rb0.M = -INFINITY; rb0.SV = -INFINITY; rb0.I = -1; rb0.F = 0;
+        RowEx rb0, rb1;   // scenario s0 + j / s0 + 16 + j over this lane's vertices v0 + g + 4r (+16)
+        rb0.M = -INFINITY; rb0.thr = -INFINITY; rb0.I = -1; rb0.n = 0;
         rb1 = rb0;
+        // this lane's candidate logs of the two scenarios (rows padded to whole tiles)
+        int *log0 = tail ? P.tcand + ((((size_t)(s0 + j - P.full_units * kCutTile2)) * P.tail_S + range) * 4 + g) * kCandC
+                         : P.cand + (((size_t)(s0 + j)) * 4 + g) * kCandC;
+        const size_t lstep = (size_t)16 * (tail ? P.tail_S : 1) * 4 * kCandC;   // scenario + 16
 
         // chunk staging by LDS-DMA (global_load_lds_dwordx4, no VGPR round trip): instruction i
         // of the chunk writes k-rows 4i .. 4i+3 (1 KiB, lane-linear), lane L the 16 bytes of
         // row 4i + L/16 at LDS position 2 (L % 16); the source vertex pair is that position with
         // the row's half swap (lds2) applied, so the image is exactly lds2's layout
-        double preb = -INFINITY;
         auto stage = [&](int buf, int v0) {
             for (int i = wid; i < KB; i += 4) {
                 const int kk = 4 * i + (lane >> 4);
@@ -225,10 +298,8 @@ __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_
                 __builtin_amdgcn_global_load_lds((const void *)(P.PKTc + (size_t)kk * P.vcap32 + v0 + vv),
                                                  (__attribute__((address_space(3))) void *)&Bs[buf][i * 4 * kLdsRow2], 16, 0, 0);
             }
-            if (!TWOSD_CUT_BASEK && threadIdx.x < kVT2) preb = v0 + (int)threadIdx.x < P.nv ? P.base[v0 + threadIdx.x] : -INFINITY;
         };
         stage(0, c_lo * kVT2);
-        if (!TWOSD_CUT_BASEK && threadIdx.x < kVT2) bs[0][threadIdx.x] = preb;
         __syncthreads();            // chunk c_lo landed (the barrier drains the DMA)
         for (int ch = c_lo; ch < c_hi; ++ch) {
             const int buf = (ch - c_lo) & 1;
@@ -240,42 +311,6 @@ __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_
             // fragments are read in groups of KG k-blocks ahead of their MFMAs; the scheduling
             // barrier keeps the compiler from hoisting every read of the chunk (register spills)
             constexpr int KG = TWOSD_CUT_KG;
-            if constexpr (TWOSD_CUT_PF) {
-                // software-pipelined: group k0 + KG is read while group k0 is multiplied
-                double x0[KG], x1[KG];
-#pragma unroll
-                for (int u = 0; u < KG; ++u) {
-                    x0[u] = Bs[buf][lds2(4 * u + g, j)];
-                    x1[u] = Bs[buf][lds2(4 * u + g, 16 + j)];
-                }
-#pragma unroll
-                for (int k0 = 0; k0 < KB; k0 += KG) {
-                    double y0[KG], y1[KG];
-#pragma unroll
-                    for (int u = 0; u < KG; ++u) {
-                        if (k0 + KG + u < KB) {
-                            y0[u] = Bs[buf][lds2(4 * (k0 + KG + u) + g, j)];
-                            y1[u] = Bs[buf][lds2(4 * (k0 + KG + u) + g, 16 + j)];
-                        }
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int u = 0; u < KG; ++u) {
-                        if (k0 + u < KB) {
-                            c00 = __builtin_amdgcn_mfma_f64_16x16x4f64(x0[u], a0[k0 + u], c00, 0, 0, 0);
-                            c01 = __builtin_amdgcn_mfma_f64_16x16x4f64(x0[u], a1[k0 + u], c01, 0, 0, 0);
-                            c10 = __builtin_amdgcn_mfma_f64_16x16x4f64(x1[u], a0[k0 + u], c10, 0, 0, 0);
-                            c11 = __builtin_amdgcn_mfma_f64_16x16x4f64(x1[u], a1[k0 + u], c11, 0, 0, 0);
-                        }
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int u = 0; u < KG; ++u) {
-                        x0[u] = y0[u];
-                        x1[u] = y1[u];
-                    }
-                }
-            } else {
 #pragma unroll
             for (int k0 = 0; k0 < KB; k0 += KG) {
                 double x0[KG], x1[KG];
@@ -297,85 +332,48 @@ __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_
                 }
                 if (TWOSD_CUT_SB) __builtin_amdgcn_sched_barrier(0);
             }
-            }
             // C/D: register r of a tile is vertex row g + 4r, scenario column j; this lane's
-            // vertices in increasing order: v0 + g + 4r, then v0 + 16 + g + 4r
-            if constexpr (TWOSD_CUT_BASEK) {   // the scores include the base (-inf past nv)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    RU2(rb0, c00[r], v0 + g + 4 * r, P.tie_rel);
-                    RU2(rb1, c01[r], v0 + g + 4 * r, P.tie_rel);
-                }
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    RU2(rb0, c10[r], v0 + 16 + g + 4 * r, P.tie_rel);
-                    RU2(rb1, c11[r], v0 + 16 + g + 4 * r, P.tie_rel);
-                }
-            } else {
+            // vertices in increasing order: v0 + g + 4r, then v0 + 16 + g + 4r.  The scores
+            // include the base (-inf past nv).
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int va = v0 + g + 4 * r;
-                const double ba = va < P.nv ? bs[buf][g + 4 * r] : -INFINITY;
-                RU2(rb0, ba + c00[r], va, P.tie_rel);
-                RU2(rb1, ba + c01[r], va, P.tie_rel);
+                row_fast(rb0, c00[r], v0 + g + 4 * r, rel, band, log0);
+                row_fast(rb1, c01[r], v0 + g + 4 * r, rel, band, log0 + lstep);
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int vb = v0 + 16 + g + 4 * r;
-                const double bb = vb < P.nv ? bs[buf][16 + g + 4 * r] : -INFINITY;
-                RU2(rb0, bb + c10[r], vb, P.tie_rel);
-                RU2(rb1, bb + c11[r], vb, P.tie_rel);
+                row_fast(rb0, c10[r], v0 + 16 + g + 4 * r, rel, band, log0);
+                row_fast(rb1, c11[r], v0 + 16 + g + 4 * r, rel, band, log0 + lstep);
             }
-            }
-            if (!TWOSD_CUT_BASEK && ch + 1 < c_hi && threadIdx.x < kVT2) bs[buf ^ 1][threadIdx.x] = preb;
             __syncthreads();
         }
-        // combine the 4 lanes (g) of each scenario column: max M, band threshold, lowest candidate
-        // inside the band; a lane whose max reaches the band but whose candidate does not (or
-        // that flagged) -> exact fixup.  Every lane of the column ends with the result.
-        auto combine = [&](RowBest &rb) {
-            double M = rb.M;
-            M = fmax(M, __shfl_xor(M, 16));
-            M = fmax(M, __shfl_xor(M, 32));
-            const double thr = M - tolf(M, P.tie_rel);
-            const bool reach = rb.M != -INFINITY && rb.M >= thr;
-            int it = (reach && rb.SV >= thr) ? rb.I : 0x7fffffff;
-            double st = rb.SV;
-            int fl = reach && (rb.F || !(rb.SV >= thr));
-#pragma unroll
-            for (int o = 16; o <= 32; o <<= 1) {
-                const int i2 = __shfl_xor(it, o);
-                const double s2 = __shfl_xor(st, o);
-                fl |= __shfl_xor(fl, o);
-                if (i2 < it) { it = i2; st = s2; }
-            }
-            rb.I = (M == -INFINITY || it == 0x7fffffff) ? -1 : it;
-            rb.SV = st;
-            rb.F = fl;
-            rb.M = M;
-        };
-        combine(rb0);
-        combine(rb1);
+        int pk0, pk1, nt0, nt1;
+        combine_ex(rb0, rel, band, g, pk0, nt0);
+        combine_ex(rb1, rel, band, g, pk1, nt1);
         const int sa = s0 + j, sb = s0 + 16 + j;
         if (tail) {   // this vertex range's result; cut_tail_merge_kernel decides and sums
             if (g == 0) {
                 const int t0 = P.full_units * kCutTile2;
+                // the log lengths of the range's band: the merge decides with the band of the row's
+                // maximum over all ranges (a range below it contributes nothing)
                 if (sa < P.N) {
                     const size_t o = (size_t)(sa - t0) * P.tail_S + range;
-                    P.tp_m[o] = rb0.M; P.tp_sv[o] = rb0.SV; P.tp_i[o] = rb0.I; P.tp_f[o] = rb0.F;
+                    P.tp_m[o] = rb0.M; P.tp_i[o] = rb0.I; P.tp_f[o] = pk0;
                 }
                 if (sb < P.N) {
                     const size_t o = (size_t)(sb - t0) * P.tail_S + range;
-                    P.tp_m[o] = rb1.M; P.tp_sv[o] = rb1.SV; P.tp_i[o] = rb1.I; P.tp_f[o] = rb1.F;
+                    P.tp_m[o] = rb1.M; P.tp_i[o] = rb1.I; P.tp_f[o] = pk1;
                 }
             }
             continue;
         }
+        if (nt0 < 2) pk0 = 0;   // decided
+        if (nt1 < 2) pk1 = 0;
         if (g == 0) {
-            if (sa < P.N) { P.arg[sa] = rb0.I; P.val[sa] = rb0.SV; P.flag[sa] = rb0.F; }
-            if (sb < P.N) { P.arg[sb] = rb1.I; P.val[sb] = rb1.SV; P.flag[sb] = rb1.F; }
+            if (sa < P.N) { P.arg[sa] = rb0.I; P.val[sa] = rb0.M; P.flag[sa] = pk0; }
+            if (sb < P.N) { P.arg[sb] = rb1.I; P.val[sb] = rb1.M; P.flag[sb] = pk1; }
         }
-        const bool ok0 = sa < P.N && !rb0.F && rb0.I >= 0, ok1 = sb < P.N && !rb1.F && rb1.I >= 0;
+        const bool ok0 = sa < P.N && !pk0 && rb0.I >= 0, ok1 = sb < P.N && !pk1 && rb1.I >= 0;
         const double p0 = ok0 ? P.w[sa] * P.inv_total : 0.0, p1 = ok1 ? P.w[sb] * P.inv_total : 0.0;
         // sum p * val and the vertex histogram, scenarios in order (lane 0 reads them from lanes 0-15)
 #pragma unroll
@@ -385,7 +383,7 @@ __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_
                 const int ok = __shfl(t == 0 ? (int)ok0 : (int)ok1, jj);
                 const int ai = __shfl(t == 0 ? rb0.I : rb1.I, jj);
                 const double pp = __shfl(t == 0 ? p0 : p1, jj);
-                const double vl = __shfl(t == 0 ? rb0.SV : rb1.SV, jj);
+                const double vl = __shfl(t == 0 ? rb0.M : rb1.M, jj);
                 if (lane == 0 && ok) {
                     pv_sum = fma(pp, vl, pv_sum);
                     const unsigned long long hq = (unsigned long long)__double2ull_rn(pp * kFix);
@@ -440,46 +438,46 @@ __global__ void __launch_bounds__(256) cut_hist_reduce_kernel(int nb, int nv, co
     hist[v] += s;
 }
 
-// Tail scenarios: merge the per-range results in vertex order -- the same rule as `combine`
-// over the 4 lanes of a column: M = max, band threshold, lowest candidate inside the band,
-// flag when a range reaches the band but its candidate does not -- then, for a decided
-// scenario, its p * val, histogram weight and S_e terms (as cut_fixup_kernel).  One wavefront
-// per scenario, lane r = range r.
+// Tail scenarios: merge the per-range results -- the same rule as combine_ex over the ranges:
+// M = max, a range contributes its log lengths when its maximum reaches the band of M; one
+// entry in all: decided (the pick is that range's first maximum), then the scenario's p * val,
+// histogram weight and S_e terms (as cut_fixup_kernel); several: flag for the fixup (val = M).
+// One wavefront per scenario, lane r = range r.
+__device__ __forceinline__ int nib_sum(int pk) { return (pk & 15) + ((pk >> 4) & 15) + ((pk >> 8) & 15) + ((pk >> 12) & 15); }
+
 __global__ void __launch_bounds__(256) cut_tail_merge_kernel(CutParams P, int slot0) {
     const int lane = threadIdx.x & 63;
     const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int nw = (gridDim.x * blockDim.x) >> 6;
     const int t0 = P.full_units * kCutTile2, S = P.tail_S;
+    const double band = P.band_scale * __longlong_as_double((long long)*P.band_bits);
     double pv_sum = 0.0, Sacc[2] = {0.0, 0.0};
     for (int ts = gw; ts < P.N - t0; ts += nw) {
         const int s = t0 + ts;
-        double m = -INFINITY, sv = -INFINITY;
-        int ii = -1, ff = 0;
+        double m = -INFINITY;
+        int ii = -1, pk = 0;
         if (lane < S) {
             const size_t o = (size_t)ts * S + lane;
-            m = P.tp_m[o]; sv = P.tp_sv[o]; ii = P.tp_i[o]; ff = P.tp_f[o];
+            m = P.tp_m[o]; ii = P.tp_i[o]; pk = P.tp_f[o];
         }
         double M = m;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) M = fmax(M, __shfl_xor(M, o));
-        const double thr = M - tolf(M, P.tie_rel);
-        const bool reach = m != -INFINITY && m >= thr;
-        int it = (reach && ii >= 0 && sv >= thr) ? ii : 0x7fffffff;
-        double st = sv;
-        int fl = reach && (ff || ii < 0 || !(sv >= thr));
+        const double thr = band_floor(M, P.tie_rel, band);
+        const int n = (m != -INFINITY && m >= thr) ? nib_sum(pk) : 0;
+        int tot = n, it = n ? ii : 0x7fffffff;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
-            const int i2 = __shfl_xor(it, o);
-            const double s2 = __shfl_xor(st, o);
-            fl |= __shfl_xor(fl, o);
-            if (i2 < it) { it = i2; st = s2; }
+            tot += __shfl_xor(tot, o);
+            it = min(it, __shfl_xor(it, o));
         }
         const int I = (M == -INFINITY || it == 0x7fffffff) ? -1 : it;
-        if (lane == 0) { P.arg[s] = I; P.val[s] = st; P.flag[s] = fl; }
+        const int fl = tot >= 2;
+        if (lane == 0) { P.arg[s] = I; P.val[s] = M; P.flag[s] = fl; }
         if (fl || I < 0) continue;
         const double p = P.w[s] * P.inv_total;
         if (lane == 0) {
-            pv_sum = fma(p, st, pv_sum);
+            pv_sum = fma(p, M, pv_sum);
             atomicAdd(&P.hist[I], (unsigned long long)__double2ull_rn(p * kFix));
         }
 #pragma unroll
@@ -497,42 +495,122 @@ __global__ void __launch_bounds__(256) cut_tail_merge_kernel(CutParams P, int sl
     }
 }
 
-// exact two-pass rule for flagged scenarios; one wavefront per scenario
+// score[s, v] in the restatement's order (oracle_build_cut, twosd_ref.argmax_procedure):
+// t = sum over the random rows in ascending order of pi_v[row_e] (coef_e dv[s,e]) -- the dense
+// dot(pi, dvec) of subprob.jl:155 with its zero rows dropped (adding 0 is exact) -- every
+// operation rounded on its own, then base[v] + t
+__device__ __forceinline__ double restated_score(const CutParams &P, int v, int s) {
+#pragma clang fp contract(off)
+    const double *pk = P.PK + (size_t)v * P.k4;
+    const double *d = P.dv + (size_t)s * P.k;
+    double t = 0.0;
+#pragma unroll 4
+    for (int q = 0; q < P.k; ++q) {
+        const int e = P.eord[q];
+        t = t + pk[e] * (P.coef[e] * d[e]);
+    }
+    return P.base[v] + t;
+}
+
+// Re-decide the flagged scenarios in the restatement's arithmetic: the logged candidates of the
+// lane groups (and tail ranges) that reach the band hold every vertex that can be the pick; an
+// overflowed log falls back to all vertices.  tie_rel = 0: the first strict maximum (highest
+// score, lowest index among equal scores); > 0: the lowest index within tie_rel (1 + |M|) of
+// the maximum M (oracle_build_cut's rule).  One wavefront per scenario.
 __global__ void __launch_bounds__(256) cut_fixup_kernel(CutParams P, int slot0) {
+#pragma clang fp contract(off)
     const int lane = threadIdx.x & 63;
     const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int nw = (gridDim.x * blockDim.x) >> 6;
+    const int t0 = P.full_units * kCutTile2, S = P.tail_S;
+    const double band = P.band_scale * __longlong_as_double((long long)*P.band_bits);
     double pv_sum = 0.0, Sacc[2] = {0.0, 0.0};
-    // the flags are read 64 at a time (one coalesced load per wave step: flagged scenarios are
-    // rare, and a flag per dependent load made the scan of 1M flags 0.35 ms); the flagged ones of
-    // a step in ascending order
-    for (int s0 = gw * 64; s0 < P.N; s0 += nw * 64) {
-    uint64_t todo = __ballot(s0 + lane < P.N && P.flag[s0 + lane] != 0);
+    // the flags are read 64 at a time (one coalesced load per wave step); the flagged ones of a
+    // step in ascending order
+    for (int sb0 = gw * 64; sb0 < P.N; sb0 += nw * 64) {
+    uint64_t todo = __ballot(sb0 + lane < P.N && P.flag[sb0 + lane] != 0);
     while (todo) {
-        const int s = s0 + (int)__builtin_ctzll(todo);
+        const int s = sb0 + (int)__builtin_ctzll(todo);
         todo &= todo - 1;
-        // pass 1: max over v (lanes stride vertices)
-        double mx = -INFINITY;
-        for (int v = lane; v < P.nv; v += 64) {
-            double sc = P.base[v];
-            for (int e = 0; e < P.k; ++e) sc = fma(P.PK[(size_t)v * P.k4 + e], P.dv[(size_t)s * P.k + e] * P.coef[e], sc);
-            mx = fmax(mx, sc);
+        const bool trow = s >= t0;
+        const int ts = s - t0;
+        const int flag = P.flag[s];
+        const double thr = trow ? band_floor(P.val[s], P.tie_rel, band) : 0.0;
+        const int nslots = (trow ? S : 1) * 4 * kCandC;
+        // the candidate of slot q (-1: empty), *ovf set on an overflowed log
+        auto cand_of = [&](int q, bool &ovf) -> int {
+            const int r = q / (4 * kCandC), g = (q / kCandC) & 3, i = q % kCandC;
+            int pk = flag;
+            const int *base;
+            if (trow) {
+                const size_t o = (size_t)ts * S + r;
+                const double mr = P.tp_m[o];
+                pk = (mr != -INFINITY && mr >= thr) ? P.tp_f[o] : 0;
+                base = P.tcand + (o * 4 + g) * kCandC;
+            } else {
+                base = P.cand + ((size_t)s * 4 + g) * kCandC;
+            }
+            const int c = (pk >> (4 * g)) & 15;
+            if (c > kCandC) { ovf = true; return -1; }
+            return i < c ? base[i] : -1;
+        };
+        // pass 0: per lane the highest restated score, lowest vertex among equal ones
+        bool ovf = false;
+        double bm = -INFINITY;
+        int bi = 0x7fffffff;
+        for (int q = lane; q < nslots; q += 64) {
+            const int v = cand_of(q, ovf);
+            if (v < 0) continue;
+            const double sc = restated_score(P, v, s);
+            if (sc > bm || (sc == bm && v < bi)) { bm = sc; bi = v; }
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
-        const double tl = tolf(mx, P.tie_rel);
-        int best = 0x7fffffff;
-        double bv = -INFINITY;
-        for (int v = lane; v < P.nv; v += 64) {
-            double sc = P.base[v];
-            for (int e = 0; e < P.k; ++e) sc = fma(P.PK[(size_t)v * P.k4 + e], P.dv[(size_t)s * P.k + e] * P.coef[e], sc);
-            if (sc >= mx - tl && v < best) { best = v; bv = sc; }
+        const bool full = __ballot(ovf) != 0;
+        if (full) {   // a log overflowed: every vertex (lanes take them in increasing order)
+            bm = -INFINITY; bi = 0x7fffffff;
+            for (int v = lane; v < P.nv; v += 64) {
+                const double sc = restated_score(P, v, s);
+                if (sc > bm) { bm = sc; bi = v; }
+            }
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
-            const int b2 = __shfl_xor(best, o);
-            const double v2 = __shfl_xor(bv, o);
-            if (b2 < best) { best = b2; bv = v2; }
+            const double m2 = __shfl_xor(bm, o);
+            const int i2 = __shfl_xor(bi, o);
+            if (m2 > bm || (m2 == bm && i2 < bi)) { bm = m2; bi = i2; }
+        }
+        int best = bi;
+        double bv = bm;
+        if (P.tie_rel > 0.0 && best != 0x7fffffff) {
+            // pass 1: the lowest vertex within the tolerance of the maximum (same candidates)
+            const double tol = P.tie_rel * (1.0 + fabs(bm));
+            const double lim = bm - tol;
+            int lo = 0x7fffffff;
+            double lv = -INFINITY;
+            if (full) {
+                for (int v = lane; v < best; v += 64) {
+                    const double sc = restated_score(P, v, s);
+                    if (sc >= lim && v < lo) { lo = v; lv = sc; }
+                }
+            } else {
+                bool dummy = false;
+                for (int q = lane; q < nslots; q += 64) {
+                    const int v = cand_of(q, dummy);
+                    if (v < 0 || v >= best) continue;
+                    const double sc = restated_score(P, v, s);
+                    if (sc >= lim && v < lo) { lo = v; lv = sc; }
+                }
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const int i2 = __shfl_xor(lo, o);
+                const double v2 = __shfl_xor(lv, o);
+                if (i2 < lo) { lo = i2; lv = v2; }
+            }
+            if (lo < best) { best = lo; bv = lv; }
+        }
+        if (best == 0x7fffffff) {   // no finite score: no pick (as the argmax pass leaves it)
+            if (lane == 0) { P.arg[s] = -1; P.val[s] = -INFINITY; }
+            continue;
         }
         const double p = P.w[s] * P.inv_total;
         if (lane == 0) {
@@ -616,6 +694,7 @@ struct CutWs {
     int pk_count = 0, pk_vcap = 0, pk_k4 = 0;
     size_t pk_cap = 0;
     int *rows = nullptr;
+    int *eord = nullptr;    // elements by ascending row: the order of the restated score's dot
     double *coef = nullptr, *bvec = nullptr, *base = nullptr, *partial = nullptr, *sums = nullptr;
     double *gpart = nullptr, *g = nullptr;
     int *arg = nullptr, *flag = nullptr;
@@ -623,9 +702,15 @@ struct CutWs {
     unsigned long long *hist = nullptr, *hist_part = nullptr;
     size_t hpart_cap = 0;
     double *part2 = nullptr;
-    double *tp_m = nullptr, *tp_sv = nullptr;
+    double *tp_m = nullptr;
     int *tp_i = nullptr, *tp_f = nullptr;
     size_t tp_cap = 0;
+    int *cand = nullptr, *tcand = nullptr;    // candidate logs (whole tiles / tail ranges)
+    size_t cand_cap = 0, tcand_cap = 0;
+    unsigned long long *band_bits = nullptr;
+    // per epigraph: max |dv[., e]| over its scenarios (bits), the rows folded in so far
+    std::vector<unsigned long long *> dmax;
+    std::vector<int> dmax_rows, dmax_k;
     size_t base_cap = 0, part_cap = 0, n_cap = 0, hist_cap = 0, gpart_cap = 0, sums_cap = 0, part2_cap = 0;
     int m = 0, vec_m = 0;
     std::vector<double> h_coef, h_bvec;   // pinned-lifetime host staging for async uploads
@@ -639,10 +724,12 @@ static CutWs *cws(twosd_ctx *c) {
 void cut_free(twosd_ctx *c) {
     if (!c->cut_ws) return;
     CutWs *w = (CutWs *)c->cut_ws;
-    hipFree(w->PK); hipFree(w->PKT); hipFree(w->PKTc); hipFree(w->rows); hipFree(w->coef); hipFree(w->bvec); hipFree(w->base);
+    hipFree(w->PK); hipFree(w->PKT); hipFree(w->PKTc); hipFree(w->rows); hipFree(w->eord); hipFree(w->coef); hipFree(w->bvec); hipFree(w->base);
     hipFree(w->partial); hipFree(w->sums); hipFree(w->gpart); hipFree(w->g); hipFree(w->arg); hipFree(w->flag);
     hipFree(w->val); hipFree(w->hist); hipFree(w->part2); hipFree(w->hist_part);
-    hipFree(w->tp_m); hipFree(w->tp_sv); hipFree(w->tp_i); hipFree(w->tp_f);
+    hipFree(w->tp_m); hipFree(w->tp_i); hipFree(w->tp_f);
+    hipFree(w->cand); hipFree(w->tcand); hipFree(w->band_bits);
+    for (auto *p : w->dmax) hipFree(p);
     delete w;
     c->cut_ws = nullptr;
 }
@@ -652,7 +739,7 @@ void cut_invalidate_pk(twosd_ctx *c) {
     CutWs *w = (CutWs *)c->cut_ws;
     w->pk_count = 0;
     if (w->rows) hipFree(w->rows);
-    w->rows = nullptr;   // forces re-upload of the element rows
+    w->rows = nullptr;   // forces re-upload of the element rows (and their order)
 }
 
 #define HIPCHK(expr)                                                                               \
@@ -731,8 +818,14 @@ static int update_pk(twosd_ctx *c) {
     const int nv = c->dvs.size, k = c->k, k4 = (std::max(k, 1) + 3) & ~3, m = c->L.m;
     int rc;
     if (!w->rows || w->pk_k4 != k4 || w->m != m) {
-        if ((rc = realloc_dev(&w->rows, std::max(k, 1)))) return rc;
+        if ((rc = realloc_dev(&w->rows, std::max(k, 1))) || (rc = realloc_dev(&w->eord, std::max(k, 1)))) return rc;
         if (k) HIPCHK(hipMemcpy(w->rows, c->pos_row.data(), sizeof(int) * k, hipMemcpyHostToDevice));
+        // the restated score's element order: ascending row (the dense dot over the m rows), element
+        // order within a row
+        std::vector<int> ord(k);
+        for (int e = 0; e < k; ++e) ord[e] = e;
+        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return c->pos_row[a] < c->pos_row[b]; });
+        if (k) HIPCHK(hipMemcpy(w->eord, ord.data(), sizeof(int) * k, hipMemcpyHostToDevice));
         w->pk_count = 0;
         w->pk_k4 = k4;
         w->m = m;
@@ -762,20 +855,21 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     const EpiDevice &E = c->epis[epi];
     const int N = E.count, k = c->k, m = c->L.m, nv = c->dvs.size, n1 = c->n1;
     const int k4 = (std::max(k, 1) + 3) & ~3;
-    // v2 with the base row: k + 1 rows of the chunk
-    const bool base_row = TWOSD_CUT_BASEK;
-    const int KB = kb_for(base_row ? ((k + 1 + 3) & ~3) : k4);
+    // the chunk's k-rows: k element rows plus the vertex base row
+    const int KB = kb_for((k + 1 + 3) & ~3);
     if (KB < 0) return fail(TWOSD_E_UNSUPPORTED, "k = %d random elements exceeds the cut kernel envelope (127)", k);
     int rc;
     if ((rc = update_pk(c))) return rc;
-    // host: bvec = r - T x, coef
+    // host: bvec = r - T x as the restatement forms it (oracle_build_cut: r[i], then minus each
+    // T[i][j] x[j] in column order, no contraction), coef
     std::vector<double> &bvec = w->h_bvec, &coef = w->h_coef;
     bvec.assign(m, 0.0);
     coef.assign(k4, 0.0);
     for (int i = 0; i < m; ++i) {
-        double s = 0.0;
-        for (int jj = 0; jj < n1; ++jj) s += c->T[(size_t)i * n1 + jj] * x[jj];
-        bvec[i] = c->r[i] - s;
+#pragma clang fp contract(off)
+        double s = c->r[i];
+        for (int jj = 0; jj < n1; ++jj) s = s - c->T[(size_t)i * n1 + jj] * x[jj];
+        bvec[i] = s;
     }
     for (int e = 0; e < k; ++e) coef[e] = c->pos_col[e] < 0 ? 1.0 : -x[c->pos_col[e]];
     if (!w->coef || !w->bvec || !w->g || w->vec_m != m) {
@@ -817,23 +911,56 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     }
     const int nunits = full + (ntiles - full) * S;
     const int nblocks = std::max(1, std::min(nunits, B));
-    const int fix_blocks = std::max(1, std::min((N + 3) / 4, c->num_cus));
+    // the fixup takes 64 scenarios per wave step: enough waves that every SIMD holds several
+    static const int fix_per_cu = getenv("TWOSD_FIX_BPC") ? std::max(1, atoi(getenv("TWOSD_FIX_BPC"))) : 4;
+    const int fix_blocks = std::max(1, std::min((N + 255) / 256, fix_per_cu * c->num_cus));
     const int ntail = S > 1 ? N - full * kCutTile2 : 0;
     const int merge_blocks = ntail > 0 ? std::max(1, std::min((ntail + 3) / 4, c->num_cus)) : 0;
     const size_t slots = (size_t)nblocks * 4 + (size_t)fix_blocks * 4 + (size_t)merge_blocks * 4;
     if ((size_t)ntail * S > w->tp_cap) {
-        if ((rc = realloc_dev(&w->tp_m, (size_t)ntail * S)) || (rc = realloc_dev(&w->tp_sv, (size_t)ntail * S)) ||
-            (rc = realloc_dev(&w->tp_i, (size_t)ntail * S)) || (rc = realloc_dev(&w->tp_f, (size_t)ntail * S)))
+        if ((rc = realloc_dev(&w->tp_m, (size_t)ntail * S)) || (rc = realloc_dev(&w->tp_i, (size_t)ntail * S)) ||
+            (rc = realloc_dev(&w->tp_f, (size_t)ntail * S)))
             return rc;
         w->tp_cap = (size_t)ntail * S;
+    }
+    // candidate logs: rows padded to whole tiles (the padding scenarios of a tile log too)
+    const size_t cand_need = (size_t)full * kCutTile2 * 4 * kCandC;
+    const size_t tcand_need = (size_t)(ntiles - full) * kCutTile2 * S * 4 * kCandC;
+    if (cand_need > w->cand_cap) {
+        if ((rc = realloc_dev(&w->cand, cand_need))) return rc;
+        w->cand_cap = cand_need;
+    }
+    if (tcand_need > w->tcand_cap) {
+        if ((rc = realloc_dev(&w->tcand, tcand_need))) return rc;
+        w->tcand_cap = tcand_need;
+    }
+    if (!w->band_bits && (rc = realloc_dev(&w->band_bits, 1))) return rc;
+    // the epigraph's max |dv| per element, folded in for the rows added since the last cut
+    if ((int)w->dmax.size() <= epi) {
+        w->dmax.resize(epi + 1, nullptr);
+        w->dmax_rows.resize(epi + 1, 0);
+        w->dmax_k.resize(epi + 1, -1);
+    }
+    if (w->dmax_k[epi] != k) {
+        if ((rc = realloc_dev(&w->dmax[epi], std::max(k, 1)))) return rc;
+        HIPCHK(hipMemsetAsync(w->dmax[epi], 0, sizeof(unsigned long long) * std::max(k, 1), c->stream));
+        w->dmax_k[epi] = k;
+        w->dmax_rows[epi] = 0;
+    }
+    if (w->dmax_rows[epi] < N && k > 0) {
+        const int rows = N - w->dmax_rows[epi];
+        hipLaunchKernelGGL(cut_dmax_kernel, dim3(std::max(1, std::min(rows, 2048))), dim3(256), 0, c->stream, w->dmax_rows[epi], N, k,
+                           E.d_dv, w->dmax[epi]);
+        w->dmax_rows[epi] = N;
     }
     if (slots * (k + 1) > w->part_cap) {
         if ((rc = realloc_dev(&w->partial, slots * (k + 1)))) return rc;
         w->part_cap = slots * (k + 1);
     }
     HIPCHK(hipMemsetAsync(d_hist, 0, sizeof(unsigned long long) * std::max(nv, 1), c->stream));
-    hipLaunchKernelGGL(cut_vbase_kernel, dim3(std::max(1, std::min((nv + 3) / 4, 4096))), dim3(256), 0, c->stream, nv, m,
-                       c->dvs.V, w->bvec, w->base);
+    HIPCHK(hipMemsetAsync(w->band_bits, 0, sizeof(unsigned long long), c->stream));
+    hipLaunchKernelGGL(cut_vbase_kernel, dim3(std::max(1, std::min((nv + 3) / 4, 4096))), dim3(256), 0, c->stream, nv, m, k, k4,
+                       c->dvs.V, w->bvec, w->PK, w->coef, w->dmax[epi], w->base, w->band_bits);
     CutParams P{};
     P.N = N; P.k = k; P.k4 = k4; P.nv = nv; P.vcap = w->pk_vcap; P.m = m;
     static const int hist_lds_max = getenv("TWOSD_HIST_LDS") ? atoi(getenv("TWOSD_HIST_LDS")) : kHistLds;
@@ -844,6 +971,15 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     }
     P.hist_part = w->hist_part;
     P.tie_rel = tie_rel; P.inv_total = 1.0 / total_weight;
+    // band: the MFMA score and the restated one both add base[v] to a (k + 1)-term dot and differ
+    // by at most 2 gamma_{k+4} (|base[v]| + sum_e |PK coef dv|) (one more rounding per T element
+    // term, coef folded on the other side); twice that for safety
+    {
+        const double u = ldexp(1.0, -53), nk = (double)(k + 4);
+        P.band_scale = 2.0 * 2.0 * (nk * u / (1.0 - nk * u));
+    }
+    P.band_bits = w->band_bits;
+    P.cand = w->cand; P.tcand = w->tcand; P.eord = w->eord;
     P.dv = E.d_dv; P.w = E.d_w; P.coef = w->coef; P.PK = w->PK; P.PKT = w->PKT; P.base = w->base;
     {
         const int vcap32 = (nv + 31) & ~31, rows = 4 * KB;
@@ -853,13 +989,13 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
         }
         const size_t tot = (size_t)rows * vcap32;
         hipLaunchKernelGGL(cut_pktc_kernel, dim3((unsigned)std::min<size_t>(4096, (tot + 255) / 256)), dim3(256), 0, c->stream, nv, k,
-                           rows, w->pk_vcap, vcap32, w->PKT, w->coef, base_row ? w->base : nullptr, w->PKTc);
+                           rows, w->pk_vcap, vcap32, w->PKT, w->coef, w->base, w->PKTc);
         P.PKTc = w->PKTc;
         P.vcap32 = vcap32;
     }
     P.arg = w->arg; P.val = w->val; P.flag = w->flag; P.hist = d_hist; P.partial = w->partial;
     P.full_units = full; P.tail_S = S;
-    P.tp_m = w->tp_m; P.tp_sv = w->tp_sv; P.tp_i = w->tp_i; P.tp_f = w->tp_f;
+    P.tp_m = w->tp_m; P.tp_i = w->tp_i; P.tp_f = w->tp_f;
     launch_argmax(KB, P, nblocks, c->stream);
     if (P.hist_lds)
         hipLaunchKernelGGL(cut_hist_reduce_kernel, dim3((nv + 255) / 256), dim3(256), 0, c->stream, nblocks, nv, w->hist_part,

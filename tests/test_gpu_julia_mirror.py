@@ -141,9 +141,8 @@ def test_julia_mirror_sd_iteration_replay(name, E, iters, tie_rel):
                 assert got.weight_mark == wm
                 val = float(np.sum(w / w.sum() * mv))
                 assert got.alpha + got.beta @ x == pytest.approx(val, rel=1e-9, abs=1e-9)
-                if tie_rel == 0.0 and _near_tie(coef, o_deltas[e], x, Vm):
-                    ties += 1
-                    a, b = got.alpha, got.beta.copy()                # either tied vertex is the rule's pick
+                if _near_tie(coef, o_deltas[e], x, Vm):
+                    ties += 1                                        # decided in the restatement's arithmetic
                 assert got.alpha == pytest.approx(a, rel=1e-8, abs=1e-8)
                 np.testing.assert_allclose(got.beta, b, rtol=1e-8, atol=1e-8 * (1 + np.abs(b).max()))
                 if x is xc:
