@@ -150,6 +150,12 @@ int twosd_refresh_train(twosd_ctx *ctx, int epi, const double *x, int first, int
 int twosd_refresh_train_ex(twosd_ctx *ctx, int epi, const double *x, int first, int count, int kcap, int *n_bases,
                            int *n_optimal, double *box_lo, double *box_hi);
 int twosd_refresh_cap_stats(twosd_ctx *ctx, int64_t *pivots_sum, int64_t *scenarios);
+/* The training pivot cap twosd_pool_refresh would use for a last large batch of `scenarios`
+ * solves with `pivots_sum` pivots in all, under this context's setting (and TWOSD_TRAIN_KCAP):
+ * > 0 the setting, < 0 none (0), auto max(32, ceil(3 sum / n)).  The distributed refresh calls it
+ * with the all-reduced sums, so every rank and the single-rank refresh apply one rule.  Host code
+ * only; ctx may be NULL (setting 0). */
+int twosd_training_cap(twosd_ctx *ctx, int64_t pivots_sum, int64_t scenarios, int *cap);
 /* Step 2 of the distributed refresh, identical on every rank (host code, no context): over the n
  * bases all ranks list (twosd_refresh_train_bases, concatenated in rank order; rank_of[i] = the
  * listing rank), a key listed by several ranks counts the sum of its counts and belongs to its

@@ -137,9 +137,31 @@ static T *stage_buf(twosd_ctx *c, int slot, size_t n) {
     return static_cast<T *>(c->stage[slot]);
 }
 
-// head of pool basis p (materialised from c->pool_hb for a device-built basis on first use: a
-// refresh of 4096 bases would otherwise spend ~2 ms building host heads nobody reads)
-static const std::vector<int> &head_of(twosd_ctx *c, int p) {
+// the two-level candidate lists (device, or staged for the next selection) refer to pool
+// indices: every change of the pool drops them
+static void reset_candidates(twosd_ctx *c) {
+    c->pool_l1 = c->pool_ncand = 0;
+    c->cand_pending = false;
+    std::vector<int>().swap(c->cand_p1);
+    std::vector<int>().swap(c->cand_pf);
+}
+
+// the pool no longer matches the device arrays (a failed build or head read-back): keep only
+// the primary basis (a host basis) and refuse solves until a basis is installed again
+static int drop_pool(twosd_ctx *c, int code) {
+    if (c->pool.size() > 1) c->pool.resize(1);
+    c->has_basis = false;
+    c->prep_valid = false;
+    c->k_valid = false;
+    c->pool_hb_valid = false;
+    reset_candidates(c);
+    return code;
+}
+
+// head of pool basis p into *h (materialised from c->pool_hb for a device-built basis on first
+// use: a refresh of 4096 bases would otherwise spend ~2 ms building host heads nobody reads).
+// A failed device read-back drops the pool (drop_pool) and returns TWOSD_E_DEVICE.
+static int head_of(twosd_ctx *c, int p, const std::vector<int> **h) {
     PoolBasis &B = c->pool[p];
     if (B.hb_row >= 0 && !c->pool_hb_valid) {
         // the heads of a device-built pool are fetched on the first host use, not by the refresh
@@ -149,24 +171,29 @@ static const std::vector<int> &head_of(twosd_ctx *c, int p) {
             if (c->pool_hb) hipHostFree(c->pool_hb);
             c->pool_hb = nullptr;
             c->pool_hb_cap = 0;
-            if (hipHostMalloc((void **)&c->pool_hb, sizeof(int) * need * 5 / 4) == hipSuccess) c->pool_hb_cap = need * 5 / 4;
+            if (hipHostMalloc((void **)&c->pool_hb, sizeof(int) * need * 5 / 4) != hipSuccess)
+                return drop_pool(c, fail(TWOSD_E_DEVICE, "pool heads: pinned allocation of %zu ints failed", need));
+            c->pool_hb_cap = need * 5 / 4;
         }
-        if (c->pool_hb && hipMemcpyAsync(c->pool_hb, c->d_hb0, sizeof(int) * need, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
-            hipStreamSynchronize(c->stream) == hipSuccess)
-            c->pool_hb_valid = true;
+        hipError_t e = hipMemcpyAsync(c->pool_hb, c->d_hb0, sizeof(int) * need, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) return drop_pool(c, fail(TWOSD_E_DEVICE, "pool heads: read-back failed: %s", hipGetErrorString(e)));
+        c->pool_hb_valid = true;
     }
-    if (B.hb_row >= 0 && c->pool_hb_valid) {
+    if (B.hb_row >= 0) {
         const int m = c->L.m;
         const int *r = c->pool_hb + (size_t)B.hb_row * c->MP;
         B.head.resize(m);
         for (int i = 0; i < m; ++i) B.head[i] = r[i] >> 2;
         B.hb_row = -1;
     }
-    if (B.hb_row >= 0) B.head.assign(c->L.m, -1);   // the device read failed: no valid head (never a short vector)
-    return B.head;
+    if (h) *h = &B.head;
+    return TWOSD_OK;
 }
-static void materialize_heads(twosd_ctx *c) {
-    for (int p = 0; p < (int)c->pool.size(); ++p) head_of(c, p);
+static int materialize_heads(twosd_ctx *c) {
+    for (int p = 0; p < (int)c->pool.size(); ++p)
+        if (int rc = head_of(c, p, nullptr)) return rc;
+    return TWOSD_OK;
 }
 
 // f(i) for i in [0, n) on up to 16 host threads (per-basis pool preparation: independent work)
@@ -479,7 +506,7 @@ static void pi0_from_rows(const twosd_ctx *c, PoolBasis &B) {
 // host CSR rows and pi0 of the bases a device refresh built (dev_only), read back from the
 // pool arrays: upload_pool, prepare_elements and the host compose work on the host forms
 static int ensure_host_pool(twosd_ctx *c) {
-    materialize_heads(c);
+    if (int rc = materialize_heads(c)) return rc;
     const int P = (int)c->pool.size(), MP = c->MP, m = c->L.m;
     int last = -1;
     for (int p = 0; p < P; ++p)
@@ -590,7 +617,7 @@ static int upload_pool(twosd_ctx *c) {
     }
     c->prep_valid = false;
     c->k_valid = false;
-    c->pool_l1 = c->pool_ncand = 0;   // candidate lists refer to pool indices: rebuild after a change
+    reset_candidates(c);   // candidate lists refer to pool indices: rebuild after a change
     return TWOSD_OK;
 }
 
@@ -618,7 +645,7 @@ static bool same_basis(const std::vector<int> &a, const std::vector<int> &b) {
 
 // append a basis to the pool; returns 1 if added, 0 if already present, < 0 on error
 static int pool_add(twosd_ctx *c, const std::vector<int> &head, bool upload_now) {
-    materialize_heads(c);
+    if (int rc = materialize_heads(c)) return rc;
     for (const PoolBasis &B : c->pool)
         if (same_basis(B.head, head)) return 0;
     PoolBasis pb;
@@ -677,8 +704,9 @@ extern "C" int twosd_pool_size(twosd_ctx *c, int *size) {
 extern "C" int twosd_pool_get(twosd_ctx *c, int p, int *head) {
     if (c && !c->has_basis) return fail(TWOSD_E_STATE, "pool_get: no basis");
     if (!c || !head || p < 0 || p >= (int)c->pool.size()) return fail(TWOSD_E_ARG, "pool_get: basis %d of %zu", p, c ? c->pool.size() : 0);
-    const std::vector<int> &h = head_of(c, p);
-    std::copy(h.begin(), h.end(), head);
+    const std::vector<int> *h = nullptr;
+    if (int rc = head_of(c, p, &h)) return rc;
+    std::copy(h->begin(), h->end(), head);
     return TWOSD_OK;
 }
 
@@ -732,7 +760,7 @@ extern "C" int twosd_pool_build(twosd_ctx *c, int epi, const double *x, int firs
         HIPCHK(hipMemcpy(heads.data(), c->d_head_out, sizeof(int) * heads.size(), hipMemcpyDeviceToHost));
         HIPCHK(hipMemcpy(st.data(), c->d_status, sizeof(int) * nh, hipMemcpyDeviceToHost));
         std::map<std::vector<int>, std::pair<int, int>> freq;   // sorted head -> (count, first scenario)
-        materialize_heads(c);
+        if ((rc = materialize_heads(c))) return rc;
         for (const PoolBasis &B : c->pool) {
             std::vector<int> key(B.head);
             std::sort(key.begin(), key.end());
@@ -926,16 +954,9 @@ static int pg_assemble(twosd_ctx *c, PgArgs &A, const int *h_tot, const int *h_v
     // contents) and then overwritten: a failure past this point leaves c->pool describing
     // arrays that no longer hold it.  The context then drops its basis, so every later solve
     // fails cleanly (TWOSD_E_STATE) until twosd_compute_basis / twosd_set_basis installs one.
-    auto broken = [c](int code) {
-        // the device-built bases read their heads lazily from pool_hb, which the failing path may
-        // have reallocated or overwritten: keep only the primary (a host basis)
-        if (c->pool.size() > 1) c->pool.resize(1);
-        c->has_basis = false;
-        c->prep_valid = false;
-        c->k_valid = false;
-        c->pool_l1 = c->pool_ncand = 0;
-        return code;
-    };
+    // the device-built bases read their heads lazily from pool_hb, which the failing path may
+    // have reallocated or overwritten: keep only the primary (a host basis)
+    auto broken = [c](int code) { return drop_pool(c, code); };
     if (const char *inj = getenv("TWOSD_INJECT_FAIL"); inj && !strcmp(inj, "refresh_fill"))   // test hook
         return broken(fail(TWOSD_E_DEVICE, "pool refresh: injected failure after the pool-array reservation"));
     HIPCHK(hipMemcpyAsync(c->d_pg_map, map.data(), sizeof(int) * P, hipMemcpyHostToDevice, c->stream));
@@ -975,7 +996,7 @@ static int pg_assemble(twosd_ctx *c, PgArgs &A, const int *h_tot, const int *h_v
     c->b0_nnz = h_tot[0];
     c->prep_valid = false;
     c->k_valid = true;
-    c->pool_l1 = c->pool_ncand = 0;
+    reset_candidates(c);
     if (dbg) {
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         fprintf(stderr, "pg_assemble: P=%d fill + heads %.2f ms, host pool %.2f ms\n", P, ms(t0, t1),
@@ -1006,12 +1027,19 @@ static int refresh_build_device(twosd_ctx *c, const std::vector<int> &sel) {
 // batch, at least 32 (storm: 32-33; ssn, ~33 pivots a solve: ~100); none before any batch.
 // Storm 1M, 4096-basis pool (profiles/r03/train_kcap_1M.txt): cap 32 vs none -- refresh
 // 18.3 vs 25.6 ms, and the next solve 86.6 vs 108.5 ms (fewer pivots from the capped pool).
-static int train_kcap(const twosd_ctx *c) {
-    if (const char *e = getenv("TWOSD_TRAIN_KCAP")) return atoi(e);   // A/B knob
-    if (c->train_kcap > 0) return c->train_kcap;
-    if (c->train_kcap < 0 || c->piv_mean_ref <= 0.0) return 0;
-    return std::max(32, (int)std::ceil(3.0 * c->piv_mean_ref));
+// The one statement of the rule (twosd_training_cap exposes it to the distributed refresh, which
+// applies it to the all-reduced pivot sum and size of every rank): setting = TWOSD_TRAIN_KCAP if
+// set, else the context's (twosd_set_refresh_kcap); > 0 that cap, < 0 none, 0 auto =
+// max(32, ceil(3 sum / n)) in integers, none before any large batch.
+static int training_cap_rule(const twosd_ctx *c, int64_t sum, int64_t n) {
+    const char *e = getenv("TWOSD_TRAIN_KCAP");   // A/B knob
+    const int setting = e ? atoi(e) : (c ? c->train_kcap : 0);
+    if (setting > 0) return setting;
+    if (setting < 0 || n <= 0 || sum <= 0) return 0;
+    const int64_t q = (3 * sum + n - 1) / n;
+    return (int)std::max<int64_t>(32, std::min<int64_t>(q, INT32_MAX));
 }
+static int train_kcap(const twosd_ctx *c) { return training_cap_rule(c, c->piv_ref_sum, c->piv_ref_n); }
 
 // The training solves of a refresh (basis keys, eta files, final heads) under the pivot cap.  The
 // auto cap follows the last batch's pivots at the previous x; when x moved far from the pool's x
@@ -1601,7 +1629,7 @@ extern "C" int twosd_pool_candidate_picks(twosd_ctx *c, int epi, const double *x
         c->CH <= 0)
         return fail(TWOSD_E_ARG, "pool_candidate_picks: bad arguments");
     HIPCHK(hipSetDevice(c->device));
-    c->pool_l1 = c->pool_ncand = 0;   // the flat pick runs over the whole pool
+    reset_candidates(c);   // the flat pick runs over the whole pool
     return candidate_picks(c, E, x, first, count, level1, p1, pf);
 }
 
@@ -1624,7 +1652,7 @@ extern "C" int twosd_pool_build_candidates(twosd_ctx *c, int epi, const double *
     const int P = (int)c->pool.size();
     if (first < 0 || count < 1 || first + count > E.count || level1 < 0 || ncand < 0 || ncand > 1024 || (c->n1 > 0 && !x))
         return fail(TWOSD_E_ARG, "pool_build_candidates: bad arguments");
-    c->pool_l1 = c->pool_ncand = 0;
+    reset_candidates(c);
     if (level1 == 0 || ncand == 0 || level1 >= P || P < 2 || c->CH <= 0) return TWOSD_OK;   // flat selection
     HIPCHK(hipSetDevice(c->device));
     std::vector<int> p1(count), pf(count);
@@ -2535,6 +2563,13 @@ extern "C" int twosd_last_objective(twosd_ctx *c, double *weighted_sum, double *
     if (!c) return fail(TWOSD_E_ARG, "last_objective: NULL");
     if (weighted_sum) *weighted_sum = c->last_obj_wsum;
     if (weight_sum) *weight_sum = c->last_obj_w;
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_training_cap(twosd_ctx *c, int64_t pivots_sum, int64_t scenarios, int *cap) {
+    if (!cap) return fail(TWOSD_E_ARG, "training_cap: NULL");   // ctx NULL: setting 0 (host code only)
+    if (pivots_sum < 0 || scenarios < 0) return fail(TWOSD_E_ARG, "training_cap: negative pivot sum / size");
+    *cap = training_cap_rule(c, pivots_sum, scenarios);
     return TWOSD_OK;
 }
 

@@ -10,8 +10,9 @@ hot path shards naturally by scenario:
     all-reduced over RCCL (backend "nccl") -- a few KB per cut.
   * vertex-set growth (push_sharded): every rank dedups its new duals locally, then the
     locally-new rows are all-gathered and pushed in (rank, local index) order, so every rank
-    holds the same ordered set (the order decides argmax ties); check_vertex_sets_agree
-    compares size + fingerprint across ranks before every cut all-reduce.
+    holds the same ordered set (the order decides argmax ties); every cut all-reduce checks
+    size + fingerprint across ranks inside its own fp64 sums (CutExchange.build_cut: no extra
+    collective, all ranks raise alike before the histogram all-reduce).
 The collectives are plain torch.distributed calls on tensors, so the same code runs on
 CPU tensors with gloo (tests) and on HIP tensors with RCCL (bench).
 """
@@ -43,15 +44,15 @@ def allreduce_cut_partials(hist: torch.Tensor, sums: torch.Tensor):
 
 
 def allgather_rows_ordered(rows: torch.Tensor) -> torch.Tensor:
-    """Concatenate every rank's (n_r x m) rows in rank order (variable n_r)."""
+    """Concatenate every rank's (n_r x m) rows in rank order (variable n_r): one fixed all-gather
+    of the counts (one host synchronisation), then the rows padded to the longest."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return rows
     G = dist.get_world_size()
-    n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=rows.device)
-    counts = [torch.zeros_like(n) for _ in range(G)]
-    dist.all_gather(counts, n)
-    counts = [int(c.item()) for c in counts]
+    counts = [int(c) for c in _gather_fixed(np.array([rows.shape[0]], dtype=np.int64), rows.device)[:, 0]]
     mx = max(counts)
+    if mx == 0:
+        return rows[:0]
     pad = torch.zeros((mx, rows.shape[1]), dtype=rows.dtype, device=rows.device)
     pad[: rows.shape[0]] = rows
     bufs = [torch.zeros_like(pad) for _ in range(G)]
@@ -115,20 +116,39 @@ class CutExchange:
         library zero-fills and writes the buffers on its stream, synchronously), all-reduce,
         identical finalize on every rank.  Returns (alpha, beta), or (alpha, beta, sums of
         `extra`) when extra (a few fp64 per rank, e.g. the incumbent objective's sum_s w_s obj_s
-        and sum_s w_s) is given: those travel in the same all-reduce as the cut's fp64 sums."""
-        if verify:
-            check_vertex_sets_agree(self.ctx)
+        and sum_s w_s) is given: those travel in the same all-reduce as the cut's fp64 sums.
+        verify: the vertex sets must agree (the histogram adds by vertex index).  The check rides
+        in the fp64 all-reduce, which runs before the histogram's: each rank adds v and v^2 for
+        v = |V| and the four 16-bit pieces of its set fingerprint; the sets agree iff every sum
+        equals G v and G v^2 (equality in Cauchy-Schwarz), which every rank then sees alike --
+        all raise, or none, and no collective of a different length is entered."""
+        G = world()[1]
         n_extra = 0 if extra is None else len(extra)
-        hist, sums, n_f64 = self._buffers(n_extra)
+        chk = _vertex_check_row(self.ctx) if (verify and G > 1) else None
+        n_chk = 0 if chk is None else 2 * len(chk)
+        hist, sums, n_f64 = self._buffers(n_extra + n_chk)
         self.ctx.cut_partial(epi, x, tie_rel, total_weight, hist.data_ptr(), sums.data_ptr())
+        tail = []
         if n_extra:
-            sums[n_f64:] = torch.tensor(np.asarray(extra, dtype=np.float64), device=sums.device)
-        allreduce_cut_partials(hist, sums)
+            tail.append(np.asarray(extra, dtype=np.float64))
+        if n_chk:
+            tail.append(np.concatenate([chk, chk * chk]))
+        if tail:
+            sums[n_f64:] = torch.tensor(np.concatenate(tail), device=sums.device)
+        if G > 1:
+            dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+            if n_chk:
+                got = sums[n_f64 + n_extra:].cpu().numpy()
+                want = G * np.concatenate([chk, chk * chk])
+                if not np.array_equal(got, want):
+                    raise RuntimeError(f"vertex sets differ across ranks: this rank (size, fingerprint pieces) = "
+                                       f"{chk.astype(np.int64).tolist()}, sums over {G} ranks = {got[:len(chk)].tolist()}")
+            dist.all_reduce(hist, op=dist.ReduceOp.SUM)
         self._sync()         # the collective runs on torch / RCCL streams, finalize on the library's
         cut = self.ctx.cut_finalize(x, hist.data_ptr(), sums.data_ptr())
         if extra is None:
             return cut
-        return cut[0], cut[1], sums[n_f64:].cpu().numpy()
+        return cut[0], cut[1], sums[n_f64:n_f64 + n_extra].cpu().numpy()
 
 
 def build_cut_sharded(ctx, epi, x, total_weight, tie_rel, device, verify=True, extra=None):
@@ -138,6 +158,15 @@ def build_cut_sharded(ctx, epi, x, total_weight, tie_rel, device, verify=True, e
     if ex is None:
         ex = ctx._cut_exchange = CutExchange(ctx, device)
     return ex.build_cut(epi, x, total_weight, tie_rel, verify=verify, extra=extra)
+
+
+def _vertex_check_row(ctx) -> np.ndarray:
+    """(|V|, the fingerprint's four 16-bit pieces) as fp64: integers whose squares and sums over
+    any rank count stay exact."""
+    from .twosd import sdDualVertexSet
+    V = sdDualVertexSet(ctx)
+    fp = int(V.fingerprint()) & ((1 << 64) - 1)
+    return np.array([len(V)] + [(fp >> (16 * i)) & 0xFFFF for i in range(4)], dtype=np.float64)
 
 
 def check_vertex_sets_agree(ctx):
@@ -306,18 +335,10 @@ def refresh_training_cap(ctx, device=None) -> int:
     setting, else twosd_pool_refresh's auto rule -- 3 x the mean pivots of the last batch of
     >= 4096 scenarios, at least 32 -- over every rank's last batch (one all-reduce of two int64),
     so all ranks train under the same cap whatever their own batches were.  0: none."""
-    import math
-    import os
-    env = os.environ.get("TWOSD_TRAIN_KCAP")
-    setting = int(env) if env else getattr(ctx, "refresh_kcap", 0)
-    if setting > 0:
-        return setting
-    if setting < 0:
-        return 0
     ps, pn = ctx.refresh_cap_stats()
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         ps, pn = (int(v) for v in _allreduce_i64([ps, pn], device))
-    return max(32, math.ceil(3.0 * ps / pn)) if pn > 0 else 0
+    return ctx.training_cap(ps, pn)        # the native rule (setting, env, auto) on the global sums
 
 
 def refresh_sharded(ctx, train_epi, x, first, count, max_pool, level1=0, ncand=0, device=None):

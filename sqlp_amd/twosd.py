@@ -204,6 +204,13 @@ class SDContext:
         check(self.lib.twosd_refresh_cap_stats(self.h, C.byref(s), C.byref(n)))
         return s.value, n.value
 
+    def training_cap(self, pivots_sum, scenarios) -> int:
+        """The refresh's training pivot cap for a last large batch of `scenarios` solves with
+        `pivots_sum` pivots (twosd_training_cap: the native rule, this context's setting)."""
+        cap = C.c_int()
+        check(self.lib.twosd_training_cap(self.h, int(pivots_sum), int(scenarios), C.byref(cap)))
+        return cap.value
+
     def last_objective(self):
         """(sum_s w_s obj_s, sum_s w_s) of the last solve_batch / solve_push / solve_values batch
         (twosd_last_objective): the incumbent objective at x is their quotient."""

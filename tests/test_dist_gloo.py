@@ -137,3 +137,80 @@ def test_ordered_vertex_merge_equals_sequential_push():
             merged.push(v)
     assert len(merged) == len(seq)
     assert all(np.array_equal(a, b) for a, b in zip(merged.data, seq.data))
+
+
+class _FakeCutCtx:
+    """Stand-in for SDContext's cut partial / finalize (the oracle's semantics, no GPU): writes
+    this rank's partials into the exchange's buffers through their data pointers, as the
+    library does, and finalizes from them."""
+
+    def __init__(self, lo, hi):
+        self.lo, self.hi = lo, hi
+        self.prob = _problem()
+
+    def cut_partial_len(self):
+        m, n1, k, rows, cols, r, T, V, dv, w, x = self.prob
+        return V.shape[0], k + 1
+
+    def cut_partial(self, epi, x, tie_rel, total_weight, hist_ptr, sums_ptr):
+        import ctypes as C
+        h, s = _partial(self.lo, self.hi, total_weight)
+        np.ctypeslib.as_array((C.c_int64 * h.size).from_address(hist_ptr))[:] = h
+        np.ctypeslib.as_array((C.c_double * s.size).from_address(sums_ptr))[:] = s
+
+    def cut_finalize(self, x, hist_ptr, sums_ptr):
+        import ctypes as C
+        m, n1, k, rows, cols, r, T, V, dv, w, xx = self.prob
+        h = np.ctypeslib.as_array((C.c_int64 * V.shape[0]).from_address(hist_ptr)).copy()
+        s = np.ctypeslib.as_array((C.c_double * (k + 1)).from_address(sums_ptr)).copy()
+        return sdist.finalize_from_partials(h, s, V, r, T, cols)
+
+
+def _extra_worker(rank, world, port, mismatch, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m, n1, k, rows, cols, r, T, V, dv, w, x = _problem()
+        lo, hi = sdist.shard_range(dv.shape[0], rank, world)
+        ex = sdist.CutExchange(_FakeCutCtx(lo, hi), torch.device("cpu"))
+        a1, b1 = ex.build_cut(0, x, w.sum(), 0.0, verify=False)
+        extra = [1.5 * (rank + 1), 0.25 * rank]
+        a2, b2, es = ex.build_cut(0, x, w.sum(), 0.0, verify=False, extra=extra)
+        # the vertex-set check riding in the fp64 all-reduce (size + fingerprint pieces)
+        row = np.array([9.0, 11.0, 2.0, 65535.0, 7.0])
+        if mismatch and rank == 1:
+            row[3] -= 1.0
+        sdist._vertex_check_row = lambda ctx: row.copy()
+        try:
+            a3, b3, es3 = ex.build_cut(0, x, w.sum(), 0.0, verify=True, extra=extra)
+            chk = "passed"
+        except RuntimeError:
+            a3, b3, es3, chk = None, None, None, "raised"
+        out[rank] = (a1, b1, a2, b2, es, a3, b3, es3, chk)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mismatch", [False, True])
+def test_cut_exchange_extra_and_vertex_check(mismatch):
+    """CutExchange.build_cut with extra fp64 values (bench: the incumbent objective's sum w obj and
+    sum w) in the cut's all-reduce: alpha / beta bit-identical to the call without extra, the
+    extra slots the ranks' totals; the vertex-set check in the same all-reduce passes when the
+    sets agree and raises on every rank when they do not."""
+    port = _free_port()
+    with mp.get_context("spawn").Manager() as mgr:
+        out = mgr.dict()
+        mp.start_processes(_extra_worker, args=(2, port, mismatch, out), nprocs=2, join=True, start_method="spawn")
+        res = dict(out)
+    m, n1, k, rows, cols, r, T, V, dv, w, x = _problem()
+    want_extra = np.array([1.5 + 3.0, 0.25])
+    for rnk in (0, 1):
+        a1, b1, a2, b2, es, a3, b3, es3, chk = res[rnk]
+        assert a1 == a2 and np.array_equal(b1, b2)
+        np.testing.assert_array_equal(es, want_extra)
+        if mismatch:
+            assert chk == "raised"
+        else:
+            assert chk == "passed" and a3 == a1 and np.array_equal(b3, b1)
+            np.testing.assert_array_equal(es3, want_extra)
+    assert res[0][0] == res[1][0]

@@ -107,6 +107,14 @@ class _CapStats:
     def refresh_cap_stats(self):
         return self.stats
 
+    def training_cap(self, ps, pn):
+        """The native rule (twosd_training_cap, host code) with no context: setting 0 = auto."""
+        import ctypes as C
+        from sqlp_amd import _lib
+        cap = C.c_int()
+        assert _lib.load().twosd_training_cap(None, int(ps), int(pn), C.byref(cap)) == 0
+        return cap.value
+
 
 def _cap_worker(rank, world, port, stats, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))

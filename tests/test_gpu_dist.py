@@ -281,3 +281,62 @@ def test_refresh_sharded_capped_equals_single_rank():
         np.testing.assert_array_equal(o["picks"], picks)
         assert o["piv"] == piv
     print(f"capped refresh_sharded: cap {cap}, pool {size}")
+
+
+def test_refresh_sharded_g1_auto_cap_equals_pool_refresh(monkeypatch):
+    """One rank, the auto training cap (no setting, no TWOSD_TRAIN_KCAP): refresh_sharded derives
+    the cap through the native rule (twosd_training_cap) from the same last-batch statistics
+    twosd_pool_refresh reads, so both build the same pool (the Python copy of the rule
+    differed at an exact-integer 3 x mean and for TWOSD_TRAIN_KCAP=0)."""
+    import math
+    from sqlp_amd import dist as sdist
+    from sqlp_amd import twosd
+    monkeypatch.delenv("TWOSD_TRAIN_KCAP", raising=False)
+    x = _refresh_x()
+    states, caps = [], []
+    for sharded in (True, False):
+        ctx = _storm_ctx()
+        warm = twosd.sdEpigraph(ctx, 1.0, 0.0)
+        twosd.add_sampled_scenarios(warm, 6144, 777)
+        twosd.solve_batch(warm, I.x_ev("storm"), 0, 6144, want_pi=False)
+        ps, pn = ctx.refresh_cap_stats()
+        assert pn == 6144
+        cap = ctx.training_cap(ps, pn)
+        assert cap == max(32, math.ceil(3 * ps / pn))
+        assert ctx.training_cap(ps, 0) == 0                 # no large batch yet: no cap
+        tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+        twosd.add_sampled_scenarios(tr, R_TRAIN, 4242)
+        if sharded:
+            import torch
+            size, ms = sdist.refresh_sharded(ctx, tr, x, 0, R_TRAIN, R_POOL, 128, 160, torch.device("cuda", 0))
+            caps.append(ms["kcap"])
+        else:
+            size = ctx.pool_refresh(tr, x, 0, R_TRAIN, R_POOL)
+            ctx.pool_build_candidates(tr, x, 0, R_TRAIN, 128, 160)
+            caps.append(cap)
+        states.append((size,) + _pool_state(ctx, x))
+    assert caps[0] == caps[1]
+    (s0, h0, o0, st0, p0, v0), (s1, h1, o1, st1, p1, v1) = states
+    assert s0 == s1
+    np.testing.assert_array_equal(h0, h1)
+    np.testing.assert_array_equal(o0, o1)
+    np.testing.assert_array_equal(p0, p1)
+    assert v0 == v1
+
+
+def test_training_cap_setting_and_env(monkeypatch):
+    """twosd_training_cap: an explicit setting wins, a negative one means no cap, and
+    TWOSD_TRAIN_KCAP is read as a setting (0 = auto) on the native side for every caller."""
+    ctx = _storm_ctx()
+    monkeypatch.delenv("TWOSD_TRAIN_KCAP", raising=False)
+    assert ctx.training_cap(3 * 11 * 1000, 1000) == 33          # exact integer 3 x mean: no round-up
+    assert ctx.training_cap(100, 1000) == 32                    # floor 32
+    ctx.set_refresh_kcap(40)
+    assert ctx.training_cap(100, 1000) == 40
+    ctx.set_refresh_kcap(-1)
+    assert ctx.training_cap(100000, 1000) == 0
+    ctx.set_refresh_kcap(0)
+    monkeypatch.setenv("TWOSD_TRAIN_KCAP", "0")
+    assert ctx.training_cap(50000, 1000) == 150
+    monkeypatch.setenv("TWOSD_TRAIN_KCAP", "77")
+    assert ctx.training_cap(50000, 1000) == 77
