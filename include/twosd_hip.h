@@ -268,6 +268,14 @@ int twosd_build_cut(twosd_ctx *ctx, int epi, const double *x, double tie_rel,
                     double *max_val, int *max_arg);
 
 /*
+ * Counters of the last twosd_build_cut / twosd_cut_partial (diagnostics, synchronous read):
+ * out[0] scenarios re-decided in the restatement's arithmetic (several vertices within the
+ * MFMA scores' error band of the maximum), out[1] candidate vertices scored for them, out[2]
+ * scenarios re-scanned over every vertex (a candidate log overflowed).
+ */
+int twosd_cut_stats(twosd_ctx *ctx, int64_t *out);
+
+/*
  * Multi-GPU split of twosd_build_cut: each rank computes partial sums over its own
  * scenarios into a caller-provided DEVICE buffer (layout in twosd_cut_partial_len),
  * the caller all-reduces it (sum; e.g. torch.distributed / RCCL), then finalize.

@@ -72,6 +72,7 @@ struct CutParams {
     double band_scale;     // band = band_scale * that maximum (4 gamma_{k+4}: twice the 2 gamma bound)
     int *arg; double *val; int *flag;   // N; flag != 0: re-decide (main rows: 4-bit log counts per lane group)
     int *cand;             // candidate logs of the whole tiles: [(s * 4 + g) * kCandC + i]
+    unsigned long long *fstats;   // fixup counters: re-decided scenarios, candidates scored, full re-scans
     int *tcand;            // of the tail ranges: [(((s - t0) * tail_S + range) * 4 + g) * kCandC + i]
     unsigned long long *hist;           // nv (fixed point)
     unsigned long long *hist_part;      // gridDim.x x nv block histograms (hist_lds mode)
@@ -513,18 +514,37 @@ __device__ __forceinline__ double restated_score(const CutParams &P, int v, int 
 }
 
 // Re-decide the flagged scenarios in the restatement's arithmetic: the logged candidates of the
-// lane groups (and tail ranges) that reach the band hold every vertex that can be the pick; an
-// overflowed log falls back to all vertices.  tie_rel = 0: the first strict maximum (highest
-// score, lowest index among equal scores); > 0: the lowest index within tie_rel (1 + |M|) of
-// the maximum M (oracle_build_cut's rule).  One wavefront per scenario.
+// lane groups (and tail ranges) that reach the band hold every vertex that can be the pick.
+// tie_rel = 0: the first strict maximum (highest score, lowest index among equal scores); > 0:
+// the lowest index within tie_rel (1 + |M|) of the maximum M (oracle_build_cut's rule).
+// One wavefront per scenario.  The candidates are compacted into an LDS list (at most 64); the
+// products pi_v[row_e] (coef_e dv[s,e]) of kFixB candidates at a time are formed by the whole
+// wave (lanes over the elements, in the restated order) into LDS, then lane c adds candidate c's
+// products in order -- the sequential dependent chain runs once per batch, not once per load.
+// A log that overflowed (or more than 64 candidates) falls back to every vertex, one lane per
+// vertex with the restated_score loop.
+constexpr int kFixB = 8;             // candidates per product batch
+constexpr int kFixLd = 129;          // doubles per product row (k <= 128; odd stride: conflict-free)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 __global__ void __launch_bounds__(256) cut_fixup_kernel(CutParams P, int slot0) {
 #pragma clang fp contract(off)
-    const int lane = threadIdx.x & 63;
+    __shared__ double prod[4][kFixB][kFixLd];
+    __shared__ int clv[4][64];
+    __shared__ double cls[4][64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int nw = (gridDim.x * blockDim.x) >> 6;
     const int t0 = P.full_units * kCutTile2, S = P.tail_S;
     const double band = P.band_scale * __longlong_as_double((long long)*P.band_bits);
+    // this lane's elements in the restated order: q = lane, lane + 64
+    const int e0 = lane < P.k ? P.eord[lane] : -1, e1 = lane + 64 < P.k ? P.eord[lane + 64] : -1;
+    const double c0 = e0 >= 0 ? P.coef[e0] : 0.0, c1 = e1 >= 0 ? P.coef[e1] : 0.0;
     double pv_sum = 0.0, Sacc[2] = {0.0, 0.0};
+    unsigned long long st_rows = 0, st_cands = 0, st_full = 0;
     // the flags are read 64 at a time (one coalesced load per wave step); the flagged ones of a
     // step in ascending order
     for (int sb0 = gw * 64; sb0 < P.N; sb0 += nw * 64) {
@@ -537,77 +557,108 @@ __global__ void __launch_bounds__(256) cut_fixup_kernel(CutParams P, int slot0) 
         const int flag = P.flag[s];
         const double thr = trow ? band_floor(P.val[s], P.tie_rel, band) : 0.0;
         const int nslots = (trow ? S : 1) * 4 * kCandC;
-        // the candidate of slot q (-1: empty), *ovf set on an overflowed log
-        auto cand_of = [&](int q, bool &ovf) -> int {
-            const int r = q / (4 * kCandC), g = (q / kCandC) & 3, i = q % kCandC;
-            int pk = flag;
-            const int *base;
-            if (trow) {
-                const size_t o = (size_t)ts * S + r;
-                const double mr = P.tp_m[o];
-                pk = (mr != -INFINITY && mr >= thr) ? P.tp_f[o] : 0;
-                base = P.tcand + (o * 4 + g) * kCandC;
-            } else {
-                base = P.cand + ((size_t)s * 4 + g) * kCandC;
+        // 1. compact the candidates into clv (slot order; overflow: > 64 or an overflowed log)
+        int nc = 0;
+        bool full = false;
+        for (int q0 = 0; q0 < nslots && !full; q0 += 64) {
+            const int q = q0 + lane;
+            int v = -1;
+            bool ovf = false;
+            if (q < nslots) {
+                const int r = q / (4 * kCandC), g = (q / kCandC) & 3, i = q % kCandC;
+                int pk = flag;
+                const int *lb;
+                if (trow) {
+                    const size_t o = (size_t)ts * S + r;
+                    const double mr = P.tp_m[o];
+                    pk = (mr != -INFINITY && mr >= thr) ? P.tp_f[o] : 0;
+                    lb = P.tcand + (o * 4 + g) * kCandC;
+                } else {
+                    lb = P.cand + ((size_t)s * 4 + g) * kCandC;
+                }
+                const int c = (pk >> (4 * g)) & 15;
+                ovf = c > kCandC;
+                if (!ovf && i < c) v = lb[i];
             }
-            const int c = (pk >> (4 * g)) & 15;
-            if (c > kCandC) { ovf = true; return -1; }
-            return i < c ? base[i] : -1;
-        };
-        // pass 0: per lane the highest restated score, lowest vertex among equal ones
-        bool ovf = false;
-        double bm = -INFINITY;
-        int bi = 0x7fffffff;
-        for (int q = lane; q < nslots; q += 64) {
-            const int v = cand_of(q, ovf);
-            if (v < 0) continue;
-            const double sc = restated_score(P, v, s);
-            if (sc > bm || (sc == bm && v < bi)) { bm = sc; bi = v; }
+            const uint64_t has = __ballot(v >= 0);
+            full = __ballot(ovf) != 0 || nc + __popcll(has) > 64;
+            if (!full && v >= 0) clv[wid][nc + __popcll(has & ((1ull << lane) - 1))] = v;
+            nc += __popcll(has);
         }
-        const bool full = __ballot(ovf) != 0;
-        if (full) {   // a log overflowed: every vertex (lanes take them in increasing order)
-            bm = -INFINITY; bi = 0x7fffffff;
+        wave_lds_sync();
+        int best = 0x7fffffff;
+        double bv = -INFINITY;
+        if (!full) {
+            st_cands += nc;
+            // 2. restated scores of the candidates, kFixB at a time
+            const double *dr = P.dv + (size_t)s * P.k;
+            const double d0 = e0 >= 0 ? c0 * dr[e0] : 0.0, d1 = e1 >= 0 ? c1 * dr[e1] : 0.0;
+            for (int b0 = 0; b0 < nc; b0 += kFixB) {
+                const int nb = min(kFixB, nc - b0);
+                for (int c = 0; c < nb; ++c) {
+                    const double *pk = P.PK + (size_t)clv[wid][b0 + c] * P.k4;
+                    if (e0 >= 0) prod[wid][c][lane] = pk[e0] * d0;
+                    if (e1 >= 0) prod[wid][c][lane + 64] = pk[e1] * d1;
+                }
+                wave_lds_sync();
+                if (lane < nb) {
+                    double t = 0.0;
+#pragma unroll 8
+                    for (int q = 0; q < P.k; ++q) t = t + prod[wid][lane][q];
+                    cls[wid][b0 + lane] = P.base[clv[wid][b0 + lane]] + t;
+                }
+                wave_lds_sync();
+            }
+            // 3. the rule over the list (lane c holds candidate c)
+            const int v = lane < nc ? clv[wid][lane] : 0x7fffffff;
+            const double sc = lane < nc ? cls[wid][lane] : -INFINITY;
+            double M = sc;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) M = fmax(M, __shfl_xor(M, o));
+            if (M != -INFINITY) {   // NaN / -inf scores never win (no lane with a finite maximum: no pick)
+                const double lim = P.tie_rel > 0.0 ? M - P.tie_rel * (1.0 + fabs(M)) : M;
+                int it = (lane < nc && sc >= lim) ? v : 0x7fffffff;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) it = min(it, __shfl_xor(it, o));
+                best = it;
+                const int src = __builtin_ctzll(__ballot(lane < nc && v == it));
+                bv = __shfl(sc, src);
+            }
+        } else {
+            ++st_full;
+            // every vertex, lanes in increasing vertex order: pass 0 the first strict maximum
+            double bm = -INFINITY;
+            int bi = 0x7fffffff;
             for (int v = lane; v < P.nv; v += 64) {
                 const double sc = restated_score(P, v, s);
                 if (sc > bm) { bm = sc; bi = v; }
             }
-        }
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const double m2 = __shfl_xor(bm, o);
-            const int i2 = __shfl_xor(bi, o);
-            if (m2 > bm || (m2 == bm && i2 < bi)) { bm = m2; bi = i2; }
-        }
-        int best = bi;
-        double bv = bm;
-        if (P.tie_rel > 0.0 && best != 0x7fffffff) {
-            // pass 1: the lowest vertex within the tolerance of the maximum (same candidates)
-            const double tol = P.tie_rel * (1.0 + fabs(bm));
-            const double lim = bm - tol;
-            int lo = 0x7fffffff;
-            double lv = -INFINITY;
-            if (full) {
+            for (int o = 32; o > 0; o >>= 1) {
+                const double m2 = __shfl_xor(bm, o);
+                const int i2 = __shfl_xor(bi, o);
+                if (m2 > bm || (m2 == bm && i2 < bi)) { bm = m2; bi = i2; }
+            }
+            best = bi;
+            bv = bm;
+            if (P.tie_rel > 0.0 && best != 0x7fffffff) {   // pass 1: the lowest vertex within the tolerance
+                const double lim = bm - P.tie_rel * (1.0 + fabs(bm));
+                int lo = 0x7fffffff;
+                double lv = -INFINITY;
                 for (int v = lane; v < best; v += 64) {
                     const double sc = restated_score(P, v, s);
                     if (sc >= lim && v < lo) { lo = v; lv = sc; }
                 }
-            } else {
-                bool dummy = false;
-                for (int q = lane; q < nslots; q += 64) {
-                    const int v = cand_of(q, dummy);
-                    if (v < 0 || v >= best) continue;
-                    const double sc = restated_score(P, v, s);
-                    if (sc >= lim && v < lo) { lo = v; lv = sc; }
-                }
-            }
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                const int i2 = __shfl_xor(lo, o);
-                const double v2 = __shfl_xor(lv, o);
-                if (i2 < lo) { lo = i2; lv = v2; }
+                for (int o = 32; o > 0; o >>= 1) {
+                    const int i2 = __shfl_xor(lo, o);
+                    const double v2 = __shfl_xor(lv, o);
+                    if (i2 < lo) { lo = i2; lv = v2; }
+                }
+                if (lo < best) { best = lo; bv = lv; }
             }
-            if (lo < best) { best = lo; bv = lv; }
         }
+        ++st_rows;
         if (best == 0x7fffffff) {   // no finite score: no pick (as the argmax pass leaves it)
             if (lane == 0) { P.arg[s] = -1; P.val[s] = -INFINITY; }
             continue;
@@ -632,6 +683,11 @@ __global__ void __launch_bounds__(256) cut_fixup_kernel(CutParams P, int slot0) 
     for (int t = 0; t < 2; ++t) {
         const int e = lane + 64 * t;
         if (e < P.k) out[1 + e] = Sacc[t];
+    }
+    if (P.fstats && lane == 0 && st_rows) {
+        atomicAdd(&P.fstats[0], st_rows);
+        atomicAdd(&P.fstats[1], st_cands);
+        atomicAdd(&P.fstats[2], st_full);
     }
 }
 
@@ -706,6 +762,7 @@ struct CutWs {
     int *tp_i = nullptr, *tp_f = nullptr;
     size_t tp_cap = 0;
     int *cand = nullptr, *tcand = nullptr;    // candidate logs (whole tiles / tail ranges)
+    unsigned long long *fstats = nullptr;     // fixup counters of the last cut (3)
     size_t cand_cap = 0, tcand_cap = 0;
     unsigned long long *band_bits = nullptr;
     // per epigraph: max |dv[., e]| over its scenarios (bits), the rows folded in so far
@@ -728,7 +785,7 @@ void cut_free(twosd_ctx *c) {
     hipFree(w->partial); hipFree(w->sums); hipFree(w->gpart); hipFree(w->g); hipFree(w->arg); hipFree(w->flag);
     hipFree(w->val); hipFree(w->hist); hipFree(w->part2); hipFree(w->hist_part);
     hipFree(w->tp_m); hipFree(w->tp_i); hipFree(w->tp_f);
-    hipFree(w->cand); hipFree(w->tcand); hipFree(w->band_bits);
+    hipFree(w->cand); hipFree(w->tcand); hipFree(w->band_bits); hipFree(w->fstats);
     for (auto *p : w->dmax) hipFree(p);
     delete w;
     c->cut_ws = nullptr;
@@ -935,6 +992,8 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
         w->tcand_cap = tcand_need;
     }
     if (!w->band_bits && (rc = realloc_dev(&w->band_bits, 1))) return rc;
+    if (!w->fstats && (rc = realloc_dev(&w->fstats, 4))) return rc;
+    HIPCHK(hipMemsetAsync(w->fstats, 0, sizeof(unsigned long long) * 4, c->stream));
     // the epigraph's max |dv| per element, folded in for the rows added since the last cut
     if ((int)w->dmax.size() <= epi) {
         w->dmax.resize(epi + 1, nullptr);
@@ -979,7 +1038,7 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
         P.band_scale = 2.0 * 2.0 * (nk * u / (1.0 - nk * u));
     }
     P.band_bits = w->band_bits;
-    P.cand = w->cand; P.tcand = w->tcand; P.eord = w->eord;
+    P.cand = w->cand; P.tcand = w->tcand; P.eord = w->eord; P.fstats = w->fstats;
     P.dv = E.d_dv; P.w = E.d_w; P.coef = w->coef; P.PK = w->PK; P.PKT = w->PKT; P.base = w->base;
     {
         const int vcap32 = (nv + 31) & ~31, rows = 4 * KB;
@@ -1100,6 +1159,19 @@ extern "C" int twosd_build_cut(twosd_ctx *c, int epi, const double *x, double ti
     if (weight_mark) *weight_mark = E.total_weight;
     if (max_val) HIPCHK(hipMemcpy(max_val, w->val, sizeof(double) * E.count, hipMemcpyDeviceToHost));
     if (max_arg) HIPCHK(hipMemcpy(max_arg, w->arg, sizeof(int) * E.count, hipMemcpyDeviceToHost));
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_cut_stats(twosd_ctx *c, int64_t *out) {
+    if (!c || !out) return fail(TWOSD_E_ARG, "cut_stats: NULL");
+    for (int i = 0; i < 3; ++i) out[i] = 0;
+    CutWs *w = c->cut_ws ? (CutWs *)c->cut_ws : nullptr;
+    if (!w || !w->fstats) return TWOSD_OK;
+    unsigned long long h[4] = {0, 0, 0, 0};
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpy(h, w->fstats, sizeof(h), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 3; ++i) out[i] = (int64_t)h[i];
     return TWOSD_OK;
 }
 

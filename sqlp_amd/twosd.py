@@ -204,6 +204,13 @@ class SDContext:
         check(self.lib.twosd_refresh_cap_stats(self.h, C.byref(s), C.byref(n)))
         return s.value, n.value
 
+    def cut_stats(self):
+        """(scenarios re-decided in the restatement's arithmetic, candidates scored, full
+        re-scans) of the last cut (twosd_cut_stats)."""
+        out = np.zeros(3, dtype=np.int64)
+        check(self.lib.twosd_cut_stats(self.h, ptr(out)))
+        return tuple(int(v) for v in out)
+
     def training_cap(self, pivots_sum, scenarios) -> int:
         """The refresh's training pivot cap for a last large batch of `scenarios` solves with
         `pivots_sum` pivots (twosd_training_cap: the native rule, this context's setting)."""

@@ -231,16 +231,18 @@ def test_cut_many_exact_ties_overflow_the_logs():
     top = int(np.bincount(oma0).argmax())
     copies = np.repeat(Vm0[top][None, :], 41, axis=0)
     copies[1:, i0] += np.arange(1, 41, dtype=np.float64)
-    V = twosd.sdDualVertexSet(ctx)
+    V = twosd.sdDualVertexSet(ctx)          # the context's one set (V0): rebuilt with the copies first
+    V.clear()
     V.push_batch(np.vstack([copies, Vm0]))
-    assert len(V) == 41 + len(Vm0)
+    assert len(V) == 40 + len(Vm0)                      # copies[0] is Vm0[top] itself
     epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
     twosd.add_scenarios(epi, vals)
     Vm = V.matrix()
     for tie_rel in (0.0, 1e-12):
         cut, mv, ma = twosd._build_cut(epi, x, tie_rel, want_argmax=True)
         a, b, omv, oma = cpu.build_cut(sp.r, sp.T, x, Vm, ctx.rows, vals - sp.r[ctx.rows], np.ones(N), tie_rel=tie_rel)
-        assert (oma == 0).sum() >= (oma0 == top).sum()     # the copies' first one wins
+        assert (oma == 0).sum() >= (oma0 == top).sum(), (np.bincount(oma)[:45].tolist(), int((oma0 == top).sum()),
+                                                         bool(np.array_equal(Vm[0], Vm0[top])), float(np.abs(Vm[1:41, i0] - Vm0[top, i0]).max()))
         assert (ma == oma).all(), (tie_rel, int((ma != oma).sum()))
         assert cut.alpha == pytest.approx(a, rel=1e-8, abs=1e-8)
         np.testing.assert_allclose(cut.beta, b, rtol=1e-8, atol=1e-8 * (1 + np.abs(b).max()))
