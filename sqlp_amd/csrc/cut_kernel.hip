@@ -26,7 +26,8 @@
 // (Same value as the reference's per-scenario loop, re-associated.)
 //
 // Kernels:
-//   cut_pk_kernel      PK (|V| x k4 row-major) and PKT (k4 x vcap) gathers of new vertices
+//   cut_pk_kernel      PK (|V| x k4 row-major), PKT (k4 x vcap) and PKO (PK's columns in the
+//                      restated element order) gathers of new vertices
 //   cut_vbase_kernel   base[v] = pi_v . (r - T x) in index order (8|V|(m+1) bytes) and the
 //                      decision band (max_v |base[v]| + sum_e |PK[v,e] coef_e| dmax_e)
 //   cut_pktc_kernel    PKTc = coef(x) * PKT plus the base row: the chunk source of the argmax
@@ -38,6 +39,7 @@
 //   cut_tail_merge_kernel  per-range results of the split tiles merged in vertex order
 //   cut_fixup_kernel   scenarios with several vertices in the decision band: their logged
 //                      candidates re-scored in the restatement's order and decided by its rule
+//   cut_rescan_kernel  the few whose candidate log overflowed: every vertex re-scored
 //   cut_reduce_kernel  deterministic fixed-order sum of the partial slots
 //   cut_g_kernel(s)    g = sum_v h_v pi_v (two-level, fixed order)
 #include <hip/hip_runtime.h>
@@ -64,6 +66,7 @@ struct CutParams {
     const double *coef;    // k4 (zero padded)
     const double *PK;      // nv x k4
     const double *PKT;     // k4 x vcap
+    const double *PKO;     // nv x k4: PK with its columns in the restated order (PKO[v][q] = PK[v][eord[q]])
     const double *PKTc;    // 4 KB x vcap32: coef_e(x) * PKT, zero padded (cut_argmax2_kernel's LDS-DMA source)
     int vcap32;            // row stride of PKTc (a multiple of 32 >= nv)
     const double *base;    // nv: pi_v . bvec in index order (the restatement's base dot)
@@ -86,10 +89,13 @@ struct CutParams {
     int *tp_i, *tp_f;
 };
 
-constexpr int kCandC = 8;          // logged candidates per (scenario, lane group); count kCandC + 1 = overflow
+constexpr int kCandC = 16;         // logged candidates per (scenario, lane group); count kCandC + 1 = overflow
+constexpr int kCandBits = 5;       // bits of one lane group's count in a packed flag (4 groups: 20 bits)
+static_assert(4 * kCandC == 64, "one 64-lane step of the fixup's enumeration covers one scenario's log slots");
 
 __global__ void cut_pk_kernel(int from, int to, int m, int k, int k4, int vcap, const int *__restrict__ rows,
-                              const double *__restrict__ V, double *__restrict__ PK, double *__restrict__ PKT) {
+                              const int *__restrict__ eord, const double *__restrict__ V, double *__restrict__ PK,
+                              double *__restrict__ PKT, double *__restrict__ PKO) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     const int total = (to - from) * k4;
     if (idx >= total) return;
@@ -97,6 +103,7 @@ __global__ void cut_pk_kernel(int from, int to, int m, int k, int k4, int vcap, 
     const double x = e < k ? V[(size_t)v * m + rows[e]] : 0.0;
     PK[(size_t)v * k4 + e] = x;
     PKT[(size_t)e * vcap + v] = x;
+    PKO[(size_t)v * k4 + e] = e < k ? V[(size_t)v * m + rows[eord[e]]] : 0.0;   // column q = e in the restated order
 }
 
 // PKTc[kk][v] = coef_kk * PKT[kk][v] over rows [0, rows) x columns [0, vcap32), zero outside
@@ -220,14 +227,14 @@ __device__ __forceinline__ int lds2(int kk, int vv) { return kk * kLdsRow2 + (vv
 // of its logged entries that can lie in the band of M (0 when the lane's own max is below the
 // band floor).  tot == 1: the row is decided, its pick the first vertex of the one lane that
 // reaches the band; otherwise the row is re-decided from the logs, whose lengths `pack` holds
-// (4 bits per lane group; kCandC + 1 = overflowed).  Every lane of the column ends with the result.
+// (kCandBits per lane group; kCandC + 1 = overflowed).  Every lane of the column ends with the result.
 __device__ __forceinline__ void combine_ex(RowEx &rb, double rel, double band, int g, int &pack, int &tot) {
     double M = rb.M;
     M = fmax(M, __shfl_xor(M, 16));
     M = fmax(M, __shfl_xor(M, 32));
     const double thr = band_floor(M, rel, band);
     const int n = (rb.M != -INFINITY && rb.M >= thr) ? rb.n : 0;
-    int pk = n << (4 * g);
+    int pk = n << (kCandBits * g);
     tot = n;
     int it = n ? rb.I : 0x7fffffff;
 #pragma unroll
@@ -444,7 +451,9 @@ __global__ void __launch_bounds__(256) cut_hist_reduce_kernel(int nb, int nv, co
 // entry in all: decided (the pick is that range's first maximum), then the scenario's p * val,
 // histogram weight and S_e terms (as cut_fixup_kernel); several: flag for the fixup (val = M).
 // One wavefront per scenario, lane r = range r.
-__device__ __forceinline__ int nib_sum(int pk) { return (pk & 15) + ((pk >> 4) & 15) + ((pk >> 8) & 15) + ((pk >> 12) & 15); }
+__device__ __forceinline__ int nib_sum(int pk) {
+    return (pk & 31) + ((pk >> kCandBits) & 31) + ((pk >> (2 * kCandBits)) & 31) + ((pk >> (3 * kCandBits)) & 31);
+}
 
 __global__ void __launch_bounds__(256) cut_tail_merge_kernel(CutParams P, int slot0) {
     const int lane = threadIdx.x & 63;
@@ -502,13 +511,13 @@ __global__ void __launch_bounds__(256) cut_tail_merge_kernel(CutParams P, int sl
 // operation rounded on its own, then base[v] + t
 __device__ __forceinline__ double restated_score(const CutParams &P, int v, int s) {
 #pragma clang fp contract(off)
-    const double *pk = P.PK + (size_t)v * P.k4;
+    const double *po = P.PKO + (size_t)v * P.k4;
     const double *d = P.dv + (size_t)s * P.k;
     double t = 0.0;
 #pragma unroll 4
     for (int q = 0; q < P.k; ++q) {
         const int e = P.eord[q];
-        t = t + pk[e] * (P.coef[e] * d[e]);
+        t = t + po[q] * (P.coef[e] * d[e]);
     }
     return P.base[v] + t;
 }
@@ -517,178 +526,360 @@ __device__ __forceinline__ double restated_score(const CutParams &P, int v, int 
 // lane groups (and tail ranges) that reach the band hold every vertex that can be the pick.
 // tie_rel = 0: the first strict maximum (highest score, lowest index among equal scores); > 0:
 // the lowest index within tie_rel (1 + |M|) of the maximum M (oracle_build_cut's rule).
-// One wavefront per scenario.  The candidates are compacted into an LDS list (at most 64); the
-// products pi_v[row_e] (coef_e dv[s,e]) of kFixB candidates at a time are formed by the whole
-// wave (lanes over the elements, in the restated order) into LDS, then lane c adds candidate c's
-// products in order -- the sequential dependent chain runs once per batch, not once per load.
-// A log that overflowed (or more than 64 candidates) falls back to every vertex, one lane per
-// vertex with the restated_score loop.
-constexpr int kFixB = 8;             // candidates per product batch
-constexpr int kFixLd = 129;          // doubles per product row (k <= 128; odd stride: conflict-free)
+// Rows go in batches of up to kFxR flagged whole-tile scenarios per wavefront (a tail scenario,
+// whose logs span the vertex ranges, is a batch of its own), so every memory round trip of a
+// batch -- the flags, the logs, the staged deltas, the candidates' PK rows, the sums -- serves
+// all of its rows:
+//   1. the rows' coef_e dv[s,e] in the restated element order (eord) into LDS (dvr);
+//   2. the logged candidates compacted into one LDS list, row by row (slot order);
+//   3. one lane per candidate adds its products pi_v[row_e] dvr[q] in order (the sequential
+//      chain of restated_score; the PK gathers are independent of it and run ahead);
+//   4. lane r decides row r over its candidates; then the sums of the decided rows.
+// A log that overflowed (or a list past kFxList) re-scans every vertex for that row.
+constexpr int kFxR = 8;              // flagged scenarios per batch
+constexpr int kFxLd = 129;           // doubles per staged delta row (k <= 128; odd stride)
+constexpr int kFxList = 256;         // candidate list capacity per batch (8 rows x 32 log slots)
+
+struct FixWave {                     // one wavefront's LDS
+    double dvr[kFxR][kFxLd];
+    double cs[kFxList];
+    int cvr[kFxList];                // (row << 28) | vertex
+};
+
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
 }
 
-__global__ void __launch_bounds__(256) cut_fixup_kernel(CutParams P, int slot0) {
+// t = sum_q PKO[v][q] (cq[q] dq[q]) in q order (the restated k-term dot of one candidate; the
+// products past k are 0 and leave t unchanged: t is never -0).  The PKO row is read in groups of
+// 32 elements (16 dwordx4 loads), the next group's loads issued before this group's adds.
+__device__ __forceinline__ double chain_dot(const double2 *__restrict__ po, const double *cq, const double *dq, int k4) {
 #pragma clang fp contract(off)
-    __shared__ double prod[4][kFixB][kFixLd];
-    __shared__ int clv[4][64];
-    __shared__ double cls[4][64];
+    constexpr int GQ = 8;    // pairs per group (16 elements); k4 <= 128: at most 8 groups
+    const int k2 = k4 / 2;
+    double t = 0.0;
+    double2 a[GQ], b[GQ];
+    auto load = [&](double2 (&x)[GQ], int g) {
+#pragma unroll
+        for (int u = 0; u < GQ; ++u) {
+            const int pu = g * GQ + u;
+            const double2 ld = po[pu < k2 ? pu : k2 - 1];
+            x[u] = pu < k2 ? ld : make_double2(0.0, 0.0);
+        }
+    };
+    auto add = [&](const double2 (&x)[GQ], int g) {
+#pragma unroll
+        for (int u = 0; u < GQ; ++u) {
+            const int q = 2 * (g * GQ + u);
+            if (q < k4) {   // uniform
+                t = t + x[u].x * (cq[q] * dq[q]);
+                t = t + x[u].y * (cq[q + 1] * dq[q + 1]);
+            }
+        }
+    };
+    const int ng = (k2 + GQ - 1) / GQ;
+    load(a, 0);
+    for (int g = 0; g < ng; g += 2) {   // ping-pong: group g + 1 in flight while g is added
+        if (g + 1 < ng) load(b, g + 1);
+        add(a, g);
+        if (g + 1 >= ng) break;
+        if (g + 2 < ng) load(a, g + 2);
+        add(b, g + 1);
+    }
+    return t;
+}
+
+constexpr int kFlagRescan = 0x40000000;   // flag of a scenario left to cut_rescan_kernel (an overflowed log)
+
+__global__ void __launch_bounds__(256, 3) cut_fixup_kernel(CutParams P, int slot0) {
+#pragma clang fp contract(off)
+    __shared__ FixWave fw_all[4];
+    __shared__ double cq[kFxLd];             // coef_e in the restated order (0 past k)
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    FixWave &F = fw_all[wid];
     const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int nw = (gridDim.x * blockDim.x) >> 6;
     const int t0 = P.full_units * kCutTile2, S = P.tail_S;
     const double band = P.band_scale * __longlong_as_double((long long)*P.band_bits);
-    // this lane's elements in the restated order: q = lane, lane + 64
+    // this lane's elements in the restated order: q = lane, lane + 64 (-1: padding)
     const int e0 = lane < P.k ? P.eord[lane] : -1, e1 = lane + 64 < P.k ? P.eord[lane + 64] : -1;
-    const double c0 = e0 >= 0 ? P.coef[e0] : 0.0, c1 = e1 >= 0 ? P.coef[e1] : 0.0;
-    double pv_sum = 0.0, Sacc[2] = {0.0, 0.0};
+    if (threadIdx.x < kFxLd) {
+        const int q = threadIdx.x;
+        cq[q] = q < P.k ? P.coef[P.eord[q]] : 0.0;
+    }
+    __syncthreads();
+    double pv_sum = 0.0, Sq[2] = {0.0, 0.0};  // S_e of this wave in the restated order: q = lane, lane + 64
     unsigned long long st_rows = 0, st_cands = 0, st_full = 0;
-    // the flags are read 64 at a time (one coalesced load per wave step); the flagged ones of a
-    // step in ascending order
+#ifdef TWOSD_FIX_STAMPS
+    unsigned long long fst[6] = {0, 0, 0, 0, 0, 0}, fst_t = __builtin_amdgcn_s_memtime();
+#define FSTAMP(i) { __builtin_amdgcn_s_waitcnt(0); __builtin_amdgcn_sched_barrier(0); \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); fst[i] += t_ - fst_t; fst_t = t_; }
+#else
+#define FSTAMP(i)
+#endif
     for (int sb0 = gw * 64; sb0 < P.N; sb0 += nw * 64) {
-    uint64_t todo = __ballot(sb0 + lane < P.N && P.flag[sb0 + lane] != 0);
+    const int myflag = sb0 + lane < P.N ? P.flag[sb0 + lane] : 0;
+    uint64_t todo = __ballot(myflag != 0);
     while (todo) {
-        const int s = sb0 + (int)__builtin_ctzll(todo);
-        todo &= todo - 1;
-        const bool trow = s >= t0;
-        const int ts = s - t0;
-        const int flag = P.flag[s];
-        const double thr = trow ? band_floor(P.val[s], P.tie_rel, band) : 0.0;
-        const int nslots = (trow ? S : 1) * 4 * kCandC;
-        // 1. compact the candidates into clv (slot order; overflow: > 64 or an overflowed log)
-        int nc = 0;
-        bool full = false;
-        for (int q0 = 0; q0 < nslots && !full; q0 += 64) {
-            const int q = q0 + lane;
-            int v = -1;
-            bool ovf = false;
-            if (q < nslots) {
-                const int r = q / (4 * kCandC), g = (q / kCandC) & 3, i = q % kCandC;
-                int pk = flag;
-                const int *lb;
-                if (trow) {
-                    const size_t o = (size_t)ts * S + r;
-                    const double mr = P.tp_m[o];
-                    pk = (mr != -INFINITY && mr >= thr) ? P.tp_f[o] : 0;
-                    lb = P.tcand + (o * 4 + g) * kCandC;
-                } else {
-                    lb = P.cand + ((size_t)s * 4 + g) * kCandC;
-                }
-                const int c = (pk >> (4 * g)) & 15;
-                ovf = c > kCandC;
-                if (!ovf && i < c) v = lb[i];
+        // ---- the batch: up to kFxR whole-tile rows, or one tail row
+        int nr = 0, srow = 0, frow = 0;     // lane r < nr: its row's scenario and flag
+        bool tailb = false;
+        while (todo && nr < kFxR) {
+            const int bit = (int)__builtin_ctzll(todo);
+            const int s = sb0 + bit;
+            if (s >= t0) {                       // a tail row: alone in its batch
+                if (nr > 0) break;
+                tailb = true;
             }
-            const uint64_t has = __ballot(v >= 0);
-            full = __ballot(ovf) != 0 || nc + __popcll(has) > 64;
-            if (!full && v >= 0) clv[wid][nc + __popcll(has & ((1ull << lane) - 1))] = v;
-            nc += __popcll(has);
+            todo &= todo - 1;
+            const int fl = __shfl(myflag, bit);
+            if (lane == nr) { srow = s; frow = fl; }
+            ++nr;
+            if (tailb) break;
         }
-        wave_lds_sync();
-        int best = 0x7fffffff;
-        double bv = -INFINITY;
-        if (!full) {
-            st_cands += nc;
-            // 2. restated scores of the candidates, kFixB at a time
-            const double *dr = P.dv + (size_t)s * P.k;
-            const double d0 = e0 >= 0 ? c0 * dr[e0] : 0.0, d1 = e1 >= 0 ? c1 * dr[e1] : 0.0;
-            for (int b0 = 0; b0 < nc; b0 += kFixB) {
-                const int nb = min(kFixB, nc - b0);
-                for (int c = 0; c < nb; ++c) {
-                    const double *pk = P.PK + (size_t)clv[wid][b0 + c] * P.k4;
-                    if (e0 >= 0) prod[wid][c][lane] = pk[e0] * d0;
-                    if (e1 >= 0) prod[wid][c][lane + 64] = pk[e1] * d1;
-                }
-                wave_lds_sync();
-                if (lane < nb) {
-                    double t = 0.0;
-#pragma unroll 8
-                    for (int q = 0; q < P.k; ++q) t = t + prod[wid][lane][q];
-                    cls[wid][b0 + lane] = P.base[clv[wid][b0 + lane]] + t;
-                }
-                wave_lds_sync();
+        FSTAMP(0)
+        // 1. the rows' deltas in the restated order (zero past k), all loads in one round trip
+        {
+            double d0[kFxR], d1[kFxR];
+#pragma unroll
+            for (int r = 0; r < kFxR; ++r) {
+                const int s = __shfl(srow, r < nr ? r : 0);
+                const double *dr = P.dv + (size_t)s * P.k;
+                d0[r] = dr[e0 >= 0 ? e0 : 0];
+                d1[r] = dr[e1 >= 0 ? e1 : 0];
             }
-            // 3. the rule over the list (lane c holds candidate c)
-            const int v = lane < nc ? clv[wid][lane] : 0x7fffffff;
-            const double sc = lane < nc ? cls[wid][lane] : -INFINITY;
-            double M = sc;
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) M = fmax(M, __shfl_xor(M, o));
-            if (M != -INFINITY) {   // NaN / -inf scores never win (no lane with a finite maximum: no pick)
-                const double lim = P.tie_rel > 0.0 ? M - P.tie_rel * (1.0 + fabs(M)) : M;
-                int it = (lane < nc && sc >= lim) ? v : 0x7fffffff;
+            for (int r = 0; r < kFxR; ++r) {
+                if (r < nr) {
+                    F.dvr[r][lane] = e0 >= 0 ? d0[r] : 0.0;
+                    F.dvr[r][lane + 64] = e1 >= 0 ? d1[r] : 0.0;
+                }
+            }
+        }
+        FSTAMP(1)
+        // 2. the candidate list (slot order: rows in batch order, each row's slots contiguous)
+        int nc = 0;
+        uint32_t rstart = 0, rcount = 0;        // lane r: its row's list range
+        uint32_t ovf_rows = 0;                  // rows whose log overflowed (or a list past kFxList)
+        if (!tailb) {
+            constexpr int NIT = kFxR;         // one step per row (4 kCandC == 64 slots)
+            int vv[NIT];
 #pragma unroll
-                for (int o = 32; o > 0; o >>= 1) it = min(it, __shfl_xor(it, o));
-                best = it;
-                const int src = __builtin_ctzll(__ballot(lane < nc && v == it));
-                bv = __shfl(sc, src);
+            for (int it = 0; it < NIT; ++it) {   // every log entry of the batch in one round trip
+                const int g = lane / kCandC, i = lane % kCandC;
+                const int fl = __shfl(frow, it);
+                const int sr = __shfl(srow, it);
+                const int c = (fl >> (kCandBits * g)) & 31;
+                const int lv = P.cand[((size_t)sr * 4 + g) * kCandC + i];   // rows past nr: srow = 0, a valid address
+                vv[it] = it >= nr ? -1 : (c > kCandC ? -2 : (i < c ? lv : -1));
+            }
+#pragma unroll
+            for (int it = 0; it < NIT; ++it) {
+                if (it >= nr) break;
+                const int v = vv[it];
+                const uint64_t has = __ballot(v >= 0);
+                const int na = __popcll(has);
+                if (__ballot(v == -2) != 0 || nc + na > kFxList) {   // overflowed log (or a full list): rescan
+                    ovf_rows |= 1u << it;
+                    continue;
+                }
+                if (v >= 0) F.cvr[nc + __popcll(has & ((1ull << lane) - 1))] = (it << 28) | v;
+                if (lane == it) { rstart = nc; rcount = na; }
+                nc += na;
             }
         } else {
-            ++st_full;
-            // every vertex, lanes in increasing vertex order: pass 0 the first strict maximum
-            double bm = -INFINITY;
-            int bi = 0x7fffffff;
-            for (int v = lane; v < P.nv; v += 64) {
-                const double sc = restated_score(P, v, s);
-                if (sc > bm) { bm = sc; bi = v; }
-            }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                const double m2 = __shfl_xor(bm, o);
-                const int i2 = __shfl_xor(bi, o);
-                if (m2 > bm || (m2 == bm && i2 < bi)) { bm = m2; bi = i2; }
-            }
-            best = bi;
-            bv = bm;
-            if (P.tie_rel > 0.0 && best != 0x7fffffff) {   // pass 1: the lowest vertex within the tolerance
-                const double lim = bm - P.tie_rel * (1.0 + fabs(bm));
-                int lo = 0x7fffffff;
-                double lv = -INFINITY;
-                for (int v = lane; v < best; v += 64) {
-                    const double sc = restated_score(P, v, s);
-                    if (sc >= lim && v < lo) { lo = v; lv = sc; }
+            const int s = __shfl(srow, 0);
+            const int ts = s - t0;
+            const double thr = band_floor(P.val[s], P.tie_rel, band);
+            const int nslots = S * 4 * kCandC;
+            for (int q0 = 0; q0 < nslots; q0 += 64) {
+                const int q = q0 + lane;
+                int v = -1;
+                if (q < nslots) {
+                    const int rg = q / (4 * kCandC), g = (q / kCandC) & 3, i = q % kCandC;
+                    const size_t o = (size_t)ts * S + rg;
+                    const double mr = P.tp_m[o];
+                    const int pk = (mr != -INFINITY && mr >= thr) ? P.tp_f[o] : 0;
+                    const int c = (pk >> (kCandBits * g)) & 31;
+                    if (c > kCandC) v = -2;
+                    else if (i < c) v = P.tcand[(o * 4 + g) * kCandC + i];
                 }
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) {
-                    const int i2 = __shfl_xor(lo, o);
-                    const double v2 = __shfl_xor(lv, o);
-                    if (i2 < lo) { lo = i2; lv = v2; }
+                const uint64_t has = __ballot(v >= 0);
+                if (__ballot(v == -2)) ovf_rows = 1u;
+                if (nc + __popcll(has) > kFxList) { ovf_rows = 1u; break; }
+                if (v >= 0) F.cvr[nc + __popcll(has & ((1ull << lane) - 1))] = v;
+                nc += __popcll(has);
+            }
+            if (lane == 0) { rstart = 0; rcount = nc; }
+        }
+        wave_lds_sync();
+        FSTAMP(2)
+        st_rows += nr;
+        st_cands += nc;
+        // 3. restated scores, one lane per candidate: base[v] + chain_dot (restated_score's order)
+        for (int cb = 0; cb < nc; cb += 64) {
+            const int c = cb + lane;
+            const int cr = F.cvr[c < nc ? c : 0];
+            const int r = cr >> 28, v = cr & 0x0fffffff;
+            const double bvv = P.base[v];
+            const double t = chain_dot(reinterpret_cast<const double2 *>(P.PKO + (size_t)v * P.k4), cq, F.dvr[r], P.k4);
+            if (c < nc) F.cs[c] = bvv + t;
+        }
+        wave_lds_sync();
+        FSTAMP(3)
+        // 4. lane r decides row r over its candidates (the rule takes the lowest vertex among the
+        // qualifying ones, whatever their list order)
+        int best = 0x7fffffff;
+        double bv = -INFINITY;
+        if (lane < nr && !((ovf_rows >> lane) & 1)) {
+            double M = -INFINITY;
+            for (uint32_t c = rstart; c < rstart + rcount; ++c) M = fmax(M, F.cs[c]);
+            if (M != -INFINITY) {
+                const double lim = P.tie_rel > 0.0 ? M - P.tie_rel * (1.0 + fabs(M)) : M;
+                for (uint32_t c = rstart; c < rstart + rcount; ++c) {
+                    const int v = F.cvr[c] & 0x0fffffff;
+                    const double sc = F.cs[c];
+                    if (sc >= lim && v < best) { best = v; bv = sc; }
                 }
-                if (lo < best) { best = lo; bv = lv; }
             }
         }
-        ++st_rows;
-        if (best == 0x7fffffff) {   // no finite score: no pick (as the argmax pass leaves it)
-            if (lane == 0) { P.arg[s] = -1; P.val[s] = -INFINITY; }
-            continue;
+        // overflowed rows: left to cut_rescan_kernel (every vertex), which also adds their sums
+        const bool resc = lane < nr && ((ovf_rows >> lane) & 1);
+        if (resc) P.flag[srow] = kFlagRescan;
+        st_full += __popc(ovf_rows);
+        FSTAMP(4)
+        // 5. outputs and sums, rows in batch (= scenario) order; the picks' PKO rows in one round trip
+        if (lane < nr && !resc) {
+            P.arg[srow] = best == 0x7fffffff ? -1 : best;
+            P.val[srow] = best == 0x7fffffff ? -INFINITY : bv;
         }
-        const double p = P.w[s] * P.inv_total;
-        if (lane == 0) {
-            P.arg[s] = best;
-            P.val[s] = bv;
-            pv_sum = fma(p, bv, pv_sum);
-            atomicAdd(&P.hist[best], (unsigned long long)__double2ull_rn(p * kFix));
-        }
+        {
+            double pa[kFxR], pb[kFxR];
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int e = lane + 64 * t;
-            if (e < P.k) Sacc[t] = fma(p * P.PK[(size_t)best * P.k4 + e], P.dv[(size_t)s * P.k + e], Sacc[t]);
+            for (int r = 0; r < kFxR; ++r) {
+                const int b = __shfl(best, r < nr ? r : 0);
+                const double *po = P.PKO + (size_t)(b == 0x7fffffff ? 0 : b) * P.k4;
+                pa[r] = po[lane < P.k4 ? lane : 0];
+                pb[r] = po[lane + 64 < P.k4 ? lane + 64 : 0];
+            }
+            // lane r: its row's p and histogram weight (one load, one atomic instruction for all rows)
+            const bool mine = lane < nr && best != 0x7fffffff;
+            const double pr = lane < nr ? P.w[srow] * P.inv_total : 0.0;
+            if (mine) atomicAdd(&P.hist[best], (unsigned long long)__double2ull_rn(pr * kFix));
+#pragma unroll
+            for (int r = 0; r < kFxR; ++r) {
+                if (r >= nr) break;
+                const int b = __shfl(best, r);
+                const double bvr = __shfl(bv, r);
+                const double p = __shfl(pr, r);
+                if (b == 0x7fffffff) continue;   // no finite score: no pick (as the argmax pass leaves it)
+                if (lane == 0) pv_sum = fma(p, bvr, pv_sum);
+                if (e0 >= 0) Sq[0] = fma(p * pa[r], F.dvr[r][lane], Sq[0]);
+                if (e1 >= 0) Sq[1] = fma(p * pb[r], F.dvr[r][lane + 64], Sq[1]);
+            }
         }
+        wave_lds_sync();   // the next batch rewrites the LDS lists
+        FSTAMP(5)
     }
     }
     double *out = P.partial + (size_t)(slot0 + gw) * (P.k + 1);
     if (lane == 0) out[0] = pv_sum;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const int e = lane + 64 * t;
-        if (e < P.k) out[1 + e] = Sacc[t];
-    }
+    if (e0 >= 0) out[1 + e0] = Sq[0];
+    if (e1 >= 0) out[1 + e1] = Sq[1];
     if (P.fstats && lane == 0 && st_rows) {
         atomicAdd(&P.fstats[0], st_rows);
         atomicAdd(&P.fstats[1], st_cands);
         atomicAdd(&P.fstats[2], st_full);
+#ifdef TWOSD_FIX_STAMPS
+        for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&P.fstats[3 + i_], fst[i_]);
+#endif
     }
+}
+
+// The scenarios whose candidate log overflowed (cut_fixup_kernel marked them kFlagRescan): the
+// restated rule over EVERY vertex, one wavefront per scenario, lanes taking the vertices in
+// increasing order (64 per step) with chain_dot; pass 0 the first strict maximum, pass 1
+// (tie_rel > 0) the lowest vertex within the tolerance.  Then the scenario's sums, as the fixup.
+__global__ void __launch_bounds__(256) cut_rescan_kernel(CutParams P, int slot0) {
+#pragma clang fp contract(off)
+    __shared__ double dqs[4][kFxLd];
+    __shared__ double cq[kFxLd];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    double *dq = dqs[wid];
+    const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int nw = (gridDim.x * blockDim.x) >> 6;
+    const int e0 = lane < P.k ? P.eord[lane] : -1, e1 = lane + 64 < P.k ? P.eord[lane + 64] : -1;
+    if (threadIdx.x < kFxLd) {
+        const int q = threadIdx.x;
+        cq[q] = q < P.k ? P.coef[P.eord[q]] : 0.0;
+    }
+    __syncthreads();
+    double pv_sum = 0.0, Sq[2] = {0.0, 0.0};
+    for (int sb0 = gw * 64; sb0 < P.N; sb0 += nw * 64) {
+    uint64_t todo = __ballot(sb0 + lane < P.N && P.flag[sb0 + lane] == kFlagRescan);
+    while (todo) {
+        const int s = sb0 + (int)__builtin_ctzll(todo);
+        todo &= todo - 1;
+        const double *dr = P.dv + (size_t)s * P.k;
+        dq[lane] = e0 >= 0 ? dr[e0] : 0.0;
+        dq[lane + 64] = e1 >= 0 ? dr[e1] : 0.0;
+        wave_lds_sync();
+        double bm = -INFINITY;
+        int bi = 0x7fffffff;
+        for (int v0 = 0; v0 < P.nv; v0 += 64) {
+            const int v = v0 + lane;
+            const int vc = v < P.nv ? v : P.nv - 1;
+            const double sc = P.base[vc] + chain_dot(reinterpret_cast<const double2 *>(P.PKO + (size_t)vc * P.k4), cq, dq, P.k4);
+            if (v < P.nv && sc > bm) { bm = sc; bi = v; }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const double m2 = __shfl_xor(bm, o);
+            const int i2 = __shfl_xor(bi, o);
+            if (m2 > bm || (m2 == bm && i2 < bi)) { bm = m2; bi = i2; }
+        }
+        int best = bi;
+        double bv = bm;
+        if (P.tie_rel > 0.0 && best != 0x7fffffff) {
+            const double lim = bm - P.tie_rel * (1.0 + fabs(bm));
+            int lo = 0x7fffffff;
+            double lv = -INFINITY;
+            for (int v0 = 0; v0 < best; v0 += 64) {
+                const int v = v0 + lane;
+                const int vc = v < P.nv ? v : P.nv - 1;
+                const double sc = P.base[vc] + chain_dot(reinterpret_cast<const double2 *>(P.PKO + (size_t)vc * P.k4), cq, dq, P.k4);
+                if (v < best && sc >= lim && v < lo) { lo = v; lv = sc; }
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const int i2 = __shfl_xor(lo, o);
+                const double v2 = __shfl_xor(lv, o);
+                if (i2 < lo) { lo = i2; lv = v2; }
+            }
+            if (lo < best) { best = lo; bv = lv; }
+        }
+        if (lane == 0) {
+            P.arg[s] = best == 0x7fffffff ? -1 : best;
+            P.val[s] = best == 0x7fffffff ? -INFINITY : bv;
+        }
+        if (best != 0x7fffffff) {
+            const double p = P.w[s] * P.inv_total;
+            const double *po = P.PKO + (size_t)best * P.k4;
+            if (lane == 0) {
+                pv_sum = fma(p, bv, pv_sum);
+                atomicAdd(&P.hist[best], (unsigned long long)__double2ull_rn(p * kFix));
+            }
+            if (e0 >= 0) Sq[0] = fma(p * po[lane], dq[lane], Sq[0]);
+            if (e1 >= 0) Sq[1] = fma(p * po[lane + 64], dq[lane + 64], Sq[1]);
+        }
+        wave_lds_sync();
+    }
+    }
+    double *out = P.partial + (size_t)(slot0 + gw) * (P.k + 1);
+    if (lane == 0) out[0] = pv_sum;
+    if (e0 >= 0) out[1 + e0] = Sq[0];
+    if (e1 >= 0) out[1 + e1] = Sq[1];
 }
 
 // sums[c] = sum over slots of partial[slot][c], c < k+1, in a fixed order: block b sums
@@ -744,7 +935,7 @@ __global__ void cut_g_final_kernel(int nb, int m, const double *__restrict__ gpa
 
 // ---------------------------------------------------------------------------------
 struct CutWs {
-    double *PK = nullptr, *PKT = nullptr;
+    double *PK = nullptr, *PKT = nullptr, *PKO = nullptr;
     double *PKTc = nullptr;
     size_t pktc_cap = 0;
     int pk_count = 0, pk_vcap = 0, pk_k4 = 0;
@@ -781,7 +972,7 @@ static CutWs *cws(twosd_ctx *c) {
 void cut_free(twosd_ctx *c) {
     if (!c->cut_ws) return;
     CutWs *w = (CutWs *)c->cut_ws;
-    hipFree(w->PK); hipFree(w->PKT); hipFree(w->PKTc); hipFree(w->rows); hipFree(w->eord); hipFree(w->coef); hipFree(w->bvec); hipFree(w->base);
+    hipFree(w->PK); hipFree(w->PKT); hipFree(w->PKO); hipFree(w->PKTc); hipFree(w->rows); hipFree(w->eord); hipFree(w->coef); hipFree(w->bvec); hipFree(w->base);
     hipFree(w->partial); hipFree(w->sums); hipFree(w->gpart); hipFree(w->g); hipFree(w->arg); hipFree(w->flag);
     hipFree(w->val); hipFree(w->hist); hipFree(w->part2); hipFree(w->hist_part);
     hipFree(w->tp_m); hipFree(w->tp_i); hipFree(w->tp_f);
@@ -889,7 +1080,9 @@ static int update_pk(twosd_ctx *c) {
     }
     if (nv > w->pk_vcap) {
         const int vcap = std::max(nv, 2 * w->pk_vcap + 256);
-        if ((rc = realloc_dev(&w->PK, (size_t)vcap * k4)) || (rc = realloc_dev(&w->PKT, (size_t)vcap * k4))) return rc;
+        if ((rc = realloc_dev(&w->PK, (size_t)vcap * k4)) || (rc = realloc_dev(&w->PKT, (size_t)vcap * k4)) ||
+            (rc = realloc_dev(&w->PKO, (size_t)vcap * k4)))
+            return rc;
         w->pk_vcap = vcap;
         w->pk_count = 0;
     }
@@ -897,7 +1090,7 @@ static int update_pk(twosd_ctx *c) {
     if (w->pk_count < nv) {
         const int total = (nv - w->pk_count) * k4;
         hipLaunchKernelGGL(cut_pk_kernel, dim3((total + 255) / 256), dim3(256), 0, c->stream, w->pk_count, nv, m, k, k4,
-                           w->pk_vcap, w->rows, c->dvs.V, w->PK, w->PKT);
+                           w->pk_vcap, w->rows, w->eord, c->dvs.V, w->PK, w->PKT, w->PKO);
         HIPCHK(hipGetLastError());
         w->pk_count = nv;
     }
@@ -973,7 +1166,8 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     const int fix_blocks = std::max(1, std::min((N + 255) / 256, fix_per_cu * c->num_cus));
     const int ntail = S > 1 ? N - full * kCutTile2 : 0;
     const int merge_blocks = ntail > 0 ? std::max(1, std::min((ntail + 3) / 4, c->num_cus)) : 0;
-    const size_t slots = (size_t)nblocks * 4 + (size_t)fix_blocks * 4 + (size_t)merge_blocks * 4;
+    const int resc_blocks = std::max(1, std::min((N + 255) / 256, c->num_cus));
+    const size_t slots = (size_t)nblocks * 4 + (size_t)fix_blocks * 4 + (size_t)merge_blocks * 4 + (size_t)resc_blocks * 4;
     if ((size_t)ntail * S > w->tp_cap) {
         if ((rc = realloc_dev(&w->tp_m, (size_t)ntail * S)) || (rc = realloc_dev(&w->tp_i, (size_t)ntail * S)) ||
             (rc = realloc_dev(&w->tp_f, (size_t)ntail * S)))
@@ -992,8 +1186,8 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
         w->tcand_cap = tcand_need;
     }
     if (!w->band_bits && (rc = realloc_dev(&w->band_bits, 1))) return rc;
-    if (!w->fstats && (rc = realloc_dev(&w->fstats, 4))) return rc;
-    HIPCHK(hipMemsetAsync(w->fstats, 0, sizeof(unsigned long long) * 4, c->stream));
+    if (!w->fstats && (rc = realloc_dev(&w->fstats, 16))) return rc;
+    HIPCHK(hipMemsetAsync(w->fstats, 0, sizeof(unsigned long long) * 16, c->stream));
     // the epigraph's max |dv| per element, folded in for the rows added since the last cut
     if ((int)w->dmax.size() <= epi) {
         w->dmax.resize(epi + 1, nullptr);
@@ -1039,7 +1233,7 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     }
     P.band_bits = w->band_bits;
     P.cand = w->cand; P.tcand = w->tcand; P.eord = w->eord; P.fstats = w->fstats;
-    P.dv = E.d_dv; P.w = E.d_w; P.coef = w->coef; P.PK = w->PK; P.PKT = w->PKT; P.base = w->base;
+    P.dv = E.d_dv; P.w = E.d_w; P.coef = w->coef; P.PK = w->PK; P.PKT = w->PKT; P.PKO = w->PKO; P.base = w->base;
     {
         const int vcap32 = (nv + 31) & ~31, rows = 4 * KB;
         if ((size_t)rows * vcap32 > w->pktc_cap) {
@@ -1062,6 +1256,8 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     if (merge_blocks)
         hipLaunchKernelGGL(cut_tail_merge_kernel, dim3(merge_blocks), dim3(256), 0, c->stream, P, nblocks * 4 + fix_blocks * 4);
     hipLaunchKernelGGL(cut_fixup_kernel, dim3(fix_blocks), dim3(256), 0, c->stream, P, nblocks * 4);
+    hipLaunchKernelGGL(cut_rescan_kernel, dim3(resc_blocks), dim3(256), 0, c->stream, P,
+                       nblocks * 4 + fix_blocks * 4 + merge_blocks * 4);
     if ((size_t)(k + 1) * kReduceBlocks > w->part2_cap) {
         if ((rc = realloc_dev(&w->part2, (size_t)(k + 1) * kReduceBlocks))) return rc;
         w->part2_cap = (size_t)(k + 1) * kReduceBlocks;
@@ -1079,7 +1275,8 @@ static int cut_finalize_impl(twosd_ctx *c, const double *x, const unsigned long 
     CutWs *w = cws(c);
     const int nv = c->dvs.size, m = c->L.m, k = c->k, n1 = c->n1;
     (void)x;
-    const int chunk = 256;
+    // vertex chunks of 32 or more, at most 512 of them (each block reads its chunk's rows of V once)
+    const int chunk = std::max(32, (nv + 511) / 512);
     const int nb = std::max(1, (nv + chunk - 1) / chunk);
     int rc;
     if ((size_t)nb * m > w->gpart_cap) {
@@ -1167,11 +1364,14 @@ extern "C" int twosd_cut_stats(twosd_ctx *c, int64_t *out) {
     for (int i = 0; i < 3; ++i) out[i] = 0;
     CutWs *w = c->cut_ws ? (CutWs *)c->cut_ws : nullptr;
     if (!w || !w->fstats) return TWOSD_OK;
-    unsigned long long h[4] = {0, 0, 0, 0};
+    unsigned long long h[16] = {};
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipMemcpy(h, w->fstats, sizeof(h), hipMemcpyDeviceToHost));
     for (int i = 0; i < 3; ++i) out[i] = (int64_t)h[i];
+    if (getenv("TWOSD_FIX_STAMPS_PRINT"))
+        fprintf(stderr, "fixup stamps (cycles summed over waves): rows/setup %llu deltas %llu list %llu chains %llu decide %llu sums %llu\n",
+                h[3], h[4], h[5], h[6], h[7], h[8]);
     return TWOSD_OK;
 }
 

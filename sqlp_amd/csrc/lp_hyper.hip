@@ -211,6 +211,11 @@ constexpr int EG = TWOSD_ETA_G;
 #ifndef TWOSD_REC_UNROLL
 #define TWOSD_REC_UNROLL 1
 #endif
+// ELL columns of the x_B warm start per memory round trip
+#ifndef TWOSD_XB_U
+#define TWOSD_XB_U 1
+#endif
+constexpr int XU = TWOSD_XB_U;
 #ifndef TWOSD_HYPER_WPE
 #define TWOSD_HYPER_WPE(R) ((R) >= 9 ? 2 : 3)
 #endif
@@ -351,22 +356,28 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                 wd[t] = 1.0f;
             }
             nops += (unsigned)(__builtin_amdgcn_readlane(ksv, R) - eb[0]) * 64u;
-            // column u of every slot, in increasing u per row: the same fma order as a per-row walk
-            for (int u = 0; u < w; ++u) {
-                double kvv[R];
-                int kiv[R];
+            // columns u .. u + XU - 1 of every slot per round trip (all their loads issued before the
+            // first is used), applied in increasing u per row: the same fma order as a per-row walk
+            for (int u0 = 0; u0 < w; u0 += XU) {
+                double kvv[XU][R];
+                int kiv[XU][R];
 #pragma unroll
-                for (int t = 0; t < R; ++t) {
-                    kvv[t] = 0.0;
-                    kiv[t] = 0;
-                    if (u < len[t]) {
-                        kvv[t] = kv[(size_t)(eb[t] + u) * 64 + ln];
-                        kiv[t] = kix[(size_t)(eb[t] + u) * 64 + ln];
+                for (int uu = 0; uu < XU; ++uu)
+#pragma unroll
+                    for (int t = 0; t < R; ++t) {
+                        const int u = u0 + uu;
+                        kvv[uu][t] = 0.0;
+                        kiv[uu][t] = 0;
+                        if (u < len[t]) {
+                            kvv[uu][t] = kv[(size_t)(eb[t] + u) * 64 + ln];
+                            kiv[uu][t] = kix[(size_t)(eb[t] + u) * 64 + ln];
+                        }
                     }
-                }
 #pragma unroll
-                for (int t = 0; t < R; ++t)
-                    if (u < len[t]) xB[t] = fma(kvv[t], dvl[kiv[t]], xB[t]);
+                for (int uu = 0; uu < XU; ++uu)
+#pragma unroll
+                    for (int t = 0; t < R; ++t)
+                        if (u0 + uu < len[t]) xB[t] = fma(kvv[uu][t], dvl[kiv[uu][t]], xB[t]);
             }
             // the per-slot sign masks from an opaque copy of ubm: hoisted out of the scenario loop
             // they would be 28 loop-invariant 64-bit values, spilled and re-read every scenario

@@ -2,14 +2,19 @@
 # A/B of bench.py options on the GPU box: each variant runs the driver's protocol (steps 20, warmup 5,
 # no CPU baseline / spot check / trajectory unless the variant asks) and one summary line per variant
 # goes to gpurun_out/<tag>.txt (full JSON lines to <tag>.jsonl).
-# Usage (repo root): bash tools/ab_bench.sh <tag> "<variant args>" ["<variant args>" ...]   ("" = defaults)
+# Usage (repo root): bash tools/ab_bench.sh <tag> "<variant args>" ["<variant args>" ...]   ("" = defaults;
+# NAME=value tokens of a variant go to its environment, e.g. "TWOSD_LIB=xu2 --refresh-passes 2")
 set -u
 TAG=$1; shift
 mkdir -p gpurun_out
 OUT=gpurun_out/$TAG
 : > $OUT.txt; : > $OUT.jsonl
 for v in "$@"; do
-  timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu --spot 0 --trajectory 0 $v > $OUT.cur 2> $OUT.err
+  envs=(); args=()
+  for tok in $v; do   # NAME=value tokens (not options) set the environment of the variant (e.g. TWOSD_LIB=xu2)
+    if [[ $tok == *=* && $tok != -* ]]; then envs+=("$tok"); else args+=("$tok"); fi
+  done
+  timeout -k 10 300 env "${envs[@]}" python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu --spot 0 --trajectory 0 "${args[@]}" > $OUT.cur 2> $OUT.err
   rc=$?
   if [ $rc -ne 0 ]; then echo "variant [$v] rc=$rc" >> $OUT.txt; tail -5 $OUT.err >> $OUT.txt; exit $rc; fi
   tail -1 $OUT.cur >> $OUT.jsonl

@@ -1,5 +1,5 @@
 """Development timing of build_sasa_cut alone (storm, device-drawn scenarios, |V| real duals).
-usage: [TWOSD_LIB=variant] python tools/cut_speed.py [N] [|V|] [reps]"""
+usage: [TWOSD_LIB=variant] [TIE_REL=t] python tools/cut_speed.py [N] [|V|] [reps]"""
 import json
 import os
 import sys
@@ -36,15 +36,18 @@ def main():
     epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
     twosd.add_sampled_scenarios(epi, N, 20250219)
     ts = []
+    tie = float(os.environ.get("TIE_REL", "0"))
     for _ in range(reps):
         ctx.invalidate_x()
-        cut = twosd.build_sasa_cut(epi, x, V, 1e-12)
+        cut = twosd.build_sasa_cut(epi, x, V, tie)
         ts.append(ctx.timings_us()[2] / 1e3)
+    stats = ctx.cut_stats()   # (re-decided scenarios, candidates, full re-scans) of the last cut
     k = len(ctx.rows)
     flops = 2 * N * len(V) * k + 2 * len(V) * sp2.shape[0]
     t = min(ts)
     print(json.dumps({"lib": os.environ.get("TWOSD_LIB", "default"), "N": N, "V": len(V), "cut_ms": ts,
-                      "tflops": flops / (t * 1e-3) / 1e12, "frac": flops / (t * 1e-3) / 78.6e12, "alpha": cut.alpha}))
+                      "tflops": flops / (t * 1e-3) / 1e12, "frac": flops / (t * 1e-3) / 78.6e12, "alpha": cut.alpha,
+                      "tie_rel": tie, "redecided": stats}))
 
 
 if __name__ == "__main__":

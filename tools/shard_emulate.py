@@ -26,8 +26,8 @@ sys.path.insert(0, ROOT)
 LINK_GBS = 153.0 * 0.5       # xGMI link, half of the per-link figure (RCCL efficiency assumed)
 COLLECTIVE_MS = 0.05         # latency of one small RCCL collective + its host synchronisation (assumed)
 REFRESH_COLLECTIVES = 6      # collectives of one distributed refresh (sqlp_amd.dist.refresh_sharded)
-STEP_COLLECTIVES = 5         # per step besides the refresh: V-set check, 2 for the vertex all-gather, 2 for the
-                             # cut partials (histogram, sums + incumbent objective)
+STEP_COLLECTIVES = 4         # per step besides the refresh: 2 for the vertex all-gather, 2 for the cut partials
+                             # (sums + incumbent objective + the vertex-set check, then the histogram)
 
 
 def main():
@@ -88,7 +88,7 @@ def main():
         # of every rank's last large batch, at least 32)
         ps = sum(rk["ctx"].refresh_cap_stats()[0] for rk in ranks)
         pn = sum(rk["ctx"].refresh_cap_stats()[1] for rk in ranks)
-        cap = max(32, int(np.ceil(3.0 * ps / pn))) if pn > 0 else 0
+        cap = ranks[0]["ctx"].training_cap(ps, pn)     # the native rule (twosd_training_cap)
         nopt = []
         for r, rk in enumerate(ranks):
             t = time.perf_counter()
