@@ -40,12 +40,21 @@ int twosd::fail(int code, const char *fmt, ...) {
         if (_e != hipSuccess) return fail(TWOSD_E_DEVICE, "%s: %s", #expr, hipGetErrorString(_e)); \
     } while (0)
 
+// TWOSD_POISON=<byte> (test hook): every new device allocation is filled with that byte, so a
+// result that depends on memory no kernel wrote changes with it (the fill completes before the
+// allocation returns: the context's streams do not order against the null-stream memset)
+int twosd::poison_byte(int family) {
+    static const int b = getenv("TWOSD_POISON") ? atoi(getenv("TWOSD_POISON")) : -1;
+    static const int fam = getenv("TWOSD_POISON_FAMILY") ? atoi(getenv("TWOSD_POISON_FAMILY")) : -1;
+    return (fam & family) ? b : -1;
+}
 template <typename T>
 static int dalloc(T **p, size_t count) {
     if (*p) { hipFree(*p); *p = nullptr; }
     if (count == 0) count = 1;
     hipError_t e = hipMalloc((void **)p, sizeof(T) * count);
     if (e != hipSuccess) return fail(TWOSD_E_DEVICE, "hipMalloc(%zu bytes): %s", sizeof(T) * count, hipGetErrorString(e));
+    if (poison_byte(1) >= 0) { hipMemset(*p, poison_byte(1), sizeof(T) * count); hipDeviceSynchronize(); }
     return TWOSD_OK;
 }
 template <typename T>
@@ -62,6 +71,7 @@ int twosd::dgrow(T **p, size_t *cap, size_t count, size_t keep, hipStream_t s) {
     T *np = nullptr;
     hipError_t e = hipMalloc((void **)&np, sizeof(T) * ncap);
     if (e != hipSuccess) return fail(TWOSD_E_DEVICE, "hipMalloc(%zu bytes): %s", sizeof(T) * ncap, hipGetErrorString(e));
+    if (poison_byte(2) >= 0) { hipMemset(np, poison_byte(2), sizeof(T) * ncap); hipDeviceSynchronize(); }
     if (*p && keep) {
         e = hipMemcpyAsync(np, *p, sizeof(T) * keep, hipMemcpyDeviceToDevice, s);
         if (e != hipSuccess) return fail(TWOSD_E_DEVICE, "grow copy: %s", hipGetErrorString(e));

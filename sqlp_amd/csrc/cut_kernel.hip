@@ -1002,6 +1002,7 @@ static int realloc_dev(T **p, size_t n) {
     *p = nullptr;
     hipError_t e = hipMalloc((void **)p, sizeof(T) * std::max<size_t>(n, 1));
     if (e != hipSuccess) return fail(TWOSD_E_DEVICE, "cut workspace hipMalloc(%zu): %s", sizeof(T) * n, hipGetErrorString(e));
+    if (poison_byte(4) >= 0) { hipMemset(*p, poison_byte(4), sizeof(T) * std::max<size_t>(n, 1)); hipDeviceSynchronize(); }
     return TWOSD_OK;
 }
 

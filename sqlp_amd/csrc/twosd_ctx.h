@@ -205,6 +205,7 @@ struct twosd_ctx {
 
 namespace twosd {
 int fail(int code, const char *fmt, ...);
+int poison_byte(int family);   // TWOSD_POISON test hook (-1: off); family bit 1 dalloc, 2 dgrow, 4 cut workspace
 template <typename T>
 int dgrow(T **p, size_t *cap, size_t count, size_t keep, hipStream_t s);
 int prepare_x(twosd_ctx *c, const double *x);
