@@ -615,7 +615,7 @@ def spot_check(sp2, ctx, epi, V, xs, x_iters, positions, args):
         ok = (st == 0) & (o_st == 0)
         lp_err = float(np.max(np.abs(obj[ok] - o_obj[ok]) / (1.0 + np.abs(o_obj[ok])))) if ok.any() else None
         cut = twosd.build_sasa_cut(sub, xx, V, args.tie_rel)
-        redecided, cands, full = ctx.cut_stats()
+        redecided, cands, full, twins = ctx.cut_stats()
         a, b, omv, _ = cpu.build_cut(sp2.r, T, xx, Vm, rows, DR, np.ones(n), tie_rel=args.tie_rel, nthreads=threads)
         # near ties: scenarios whose two best vertex scores agree to 1e-9 relative (there the strict
         # '>' of the reference picks by the last bits of the summation order, so alpha and beta may
@@ -631,7 +631,8 @@ def spot_check(sp2, ctx, epi, V, xs, x_iters, positions, args):
                     (1.0 + abs(float(np.mean(o_obj[ok])))) if ok.any() else None,
                     "cut_value_rel_err": abs(cv_gpu - cv_cpu) / (1.0 + abs(cv_cpu)),
                     "near_tie_scenarios": ties,
-                    "cut_redecided": {"scenarios": redecided, "candidates": cands, "full_rescans": full},
+                    "cut_redecided": {"scenarios": redecided, "candidates": cands, "full_rescans": full,
+                                      "twins_left_out": twins},
                     "alpha_rel_err": abs(cut.alpha - a) / (1.0 + abs(a)),
                     "beta_max_rel_err": float(np.max(np.abs(cut.beta - b)) / (1.0 + np.max(np.abs(b))))})
     return res

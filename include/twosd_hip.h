@@ -271,7 +271,9 @@ int twosd_build_cut(twosd_ctx *ctx, int epi, const double *x, double tie_rel,
  * Counters of the last twosd_build_cut / twosd_cut_partial (diagnostics, synchronous read):
  * out[0] scenarios re-decided in the restatement's arithmetic (several vertices within the
  * MFMA scores' error band of the maximum), out[1] candidate vertices scored for them, out[2]
- * scenarios re-scanned over every vertex (a candidate log overflowed).
+ * scenarios re-scanned over every vertex (a candidate log overflowed), out[3] vertices left out
+ * of the argmax as dominated twins (a lower vertex with a bit-identical PK row and an equal base
+ * at this x: never the pick under either tie rule).  out has 4 entries.
  */
 int twosd_cut_stats(twosd_ctx *ctx, int64_t *out);
 

@@ -106,17 +106,67 @@ __global__ void cut_pk_kernel(int from, int to, int m, int k, int k4, int vcap, 
     PKO[(size_t)v * k4 + e] = e < k ? V[(size_t)v * m + rows[eord[e]]] : 0.0;   // column q = e in the restated order
 }
 
+// Twin vertices.  Two vertices whose PK rows are bit-identical have bit-identical restated dot
+// terms t for every scenario, so at an x where their bases are equal too their restated scores
+// are equal for every scenario: the lower index wins under both rules (the first strict maximum;
+// the lowest index within the tie window), and the higher one can never be picked.  storm's
+// duals come in such groups (vertices differing only on rows where r - T x is 0), and each one
+// made every scenario it won an exact tie the fixup had to re-decide.  tprev[v] is the previous
+// vertex of v's PK-equality group (-1: none), maintained with PK; cut_pktc_kernel drops a vertex
+// whose base equals that of an earlier group member at this x (its base row -inf).
+__global__ void cut_twin_hash_kernel(int from, int to, int k4, const double *__restrict__ PK, unsigned long long *__restrict__ phash) {
+    const int v = from + blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= to) return;
+    unsigned long long h = 0x9e3779b97f4a7c15ull;
+    for (int e = 0; e < k4; ++e) {
+        h ^= (unsigned long long)__double_as_longlong(PK[(size_t)v * k4 + e]) + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
+        h *= 0xff51afd7ed558ccdull;
+    }
+    phash[v] = h;
+}
+
+// tprev[v] = the highest u < v with PK row u bit-identical to PK row v (one wavefront per vertex)
+__global__ void __launch_bounds__(256) cut_twin_prev_kernel(int from, int to, int k4, const double *__restrict__ PK,
+                                                            const unsigned long long *__restrict__ phash, int *__restrict__ tprev) {
+    const int lane = threadIdx.x & 63;
+    const int v = from + ((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    if (v >= to) return;   // wave-uniform
+    const unsigned long long hv = phash[v];
+    int best = -1;
+    for (int u = v - 1 - lane; u >= 0 && best < 0; u -= 64) {
+        if (phash[u] != hv) continue;
+        bool same = true;
+        for (int e = 0; e < k4 && same; ++e)
+            same = __double_as_longlong(PK[(size_t)u * k4 + e]) == __double_as_longlong(PK[(size_t)v * k4 + e]);
+        if (same) best = u;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o));
+    if (lane == 0) tprev[v] = best;
+}
+
 // PKTc[kk][v] = coef_kk * PKT[kk][v] over rows [0, rows) x columns [0, vcap32), zero outside
 // [0, k) x [0, nv) (the LDS-DMA source of cut_argmax2_kernel; per x)
-// With base != nullptr, row k holds base[v] (-inf for v >= nv): the MFMA then adds the vertex
-// base through a constant 1 in the scenarios' delta column k.
+// With base != nullptr, row k holds base[v] (-inf for v >= nv and for a dominated twin): the MFMA
+// then adds the vertex base through a constant 1 in the scenarios' delta column k.
 __global__ void cut_pktc_kernel(int nv, int k, int rows, int vcap, int vcap32, const double *__restrict__ PKT,
-                                const double *__restrict__ coef, const double *__restrict__ base, double *__restrict__ PKTc) {
+                                const double *__restrict__ coef, const double *__restrict__ base, const int *__restrict__ tprev,
+                                double *__restrict__ PKTc, unsigned long long *__restrict__ ntwin) {
     const size_t total = (size_t)rows * vcap32;
     for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
         const int kk = (int)(idx / vcap32), v = (int)(idx % vcap32);
         double x = (kk < k && v < nv) ? coef[kk] * PKT[(size_t)kk * vcap + v] : 0.0;
-        if (base && kk == k) x = v < nv ? base[v] : -INFINITY;
+        if (base && kk == k) {
+            x = v < nv ? base[v] : -INFINITY;
+            if (v < nv && tprev) {
+                for (int u = tprev[v]; u >= 0; u = tprev[u])   // tprev[u] < u: the walk ends
+                    if (base[u] == x) {
+                        x = -INFINITY;
+                        if (ntwin) atomicAdd(ntwin, 1ull);
+                        break;
+                    }
+            }
+        }
         PKTc[idx] = x;
     }
 }
@@ -942,6 +992,8 @@ struct CutWs {
     size_t pk_cap = 0;
     int *rows = nullptr;
     int *eord = nullptr;    // elements by ascending row: the order of the restated score's dot
+    unsigned long long *phash = nullptr;   // per vertex: hash of its PK row (bits)
+    int *tprev = nullptr;                  // per vertex: previous vertex with a bit-identical PK row, or -1
     double *coef = nullptr, *bvec = nullptr, *base = nullptr, *partial = nullptr, *sums = nullptr;
     double *gpart = nullptr, *g = nullptr;
     int *arg = nullptr, *flag = nullptr;
@@ -977,6 +1029,7 @@ void cut_free(twosd_ctx *c) {
     hipFree(w->val); hipFree(w->hist); hipFree(w->part2); hipFree(w->hist_part);
     hipFree(w->tp_m); hipFree(w->tp_i); hipFree(w->tp_f);
     hipFree(w->cand); hipFree(w->tcand); hipFree(w->band_bits); hipFree(w->fstats);
+    hipFree(w->phash); hipFree(w->tprev);
     for (auto *p : w->dmax) hipFree(p);
     delete w;
     c->cut_ws = nullptr;
@@ -1082,7 +1135,8 @@ static int update_pk(twosd_ctx *c) {
     if (nv > w->pk_vcap) {
         const int vcap = std::max(nv, 2 * w->pk_vcap + 256);
         if ((rc = realloc_dev(&w->PK, (size_t)vcap * k4)) || (rc = realloc_dev(&w->PKT, (size_t)vcap * k4)) ||
-            (rc = realloc_dev(&w->PKO, (size_t)vcap * k4)))
+            (rc = realloc_dev(&w->PKO, (size_t)vcap * k4)) || (rc = realloc_dev(&w->phash, vcap)) ||
+            (rc = realloc_dev(&w->tprev, vcap)))
             return rc;
         w->pk_vcap = vcap;
         w->pk_count = 0;
@@ -1092,6 +1146,12 @@ static int update_pk(twosd_ctx *c) {
         const int total = (nv - w->pk_count) * k4;
         hipLaunchKernelGGL(cut_pk_kernel, dim3((total + 255) / 256), dim3(256), 0, c->stream, w->pk_count, nv, m, k, k4,
                            w->pk_vcap, w->rows, w->eord, c->dvs.V, w->PK, w->PKT, w->PKO);
+        HIPCHK(hipGetLastError());
+        const int nn = nv - w->pk_count;
+        hipLaunchKernelGGL(cut_twin_hash_kernel, dim3((nn + 255) / 256), dim3(256), 0, c->stream, w->pk_count, nv, k4, w->PK,
+                           w->phash);
+        hipLaunchKernelGGL(cut_twin_prev_kernel, dim3((nn + 3) / 4), dim3(256), 0, c->stream, w->pk_count, nv, k4, w->PK,
+                           w->phash, w->tprev);
         HIPCHK(hipGetLastError());
         w->pk_count = nv;
     }
@@ -1236,6 +1296,9 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     P.cand = w->cand; P.tcand = w->tcand; P.eord = w->eord; P.fstats = w->fstats;
     P.dv = E.d_dv; P.w = E.d_w; P.coef = w->coef; P.PK = w->PK; P.PKT = w->PKT; P.PKO = w->PKO; P.base = w->base;
     {
+        // test / A-B knob, read per cut: TWOSD_CUT_TWINS=0 keeps dominated twins in the argmax (the
+        // same picks; more re-decided rows)
+        const bool twins = !getenv("TWOSD_CUT_TWINS") || atoi(getenv("TWOSD_CUT_TWINS")) != 0;
         const int vcap32 = (nv + 31) & ~31, rows = 4 * KB;
         if ((size_t)rows * vcap32 > w->pktc_cap) {
             if ((rc = realloc_dev(&w->PKTc, (size_t)rows * vcap32))) return rc;
@@ -1243,7 +1306,8 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
         }
         const size_t tot = (size_t)rows * vcap32;
         hipLaunchKernelGGL(cut_pktc_kernel, dim3((unsigned)std::min<size_t>(4096, (tot + 255) / 256)), dim3(256), 0, c->stream, nv, k,
-                           rows, w->pk_vcap, vcap32, w->PKT, w->coef, w->base, w->PKTc);
+                           rows, w->pk_vcap, vcap32, w->PKT, w->coef, w->base, twins ? w->tprev : nullptr, w->PKTc,
+                           w->fstats + 9);
         P.PKTc = w->PKTc;
         P.vcap32 = vcap32;
     }
@@ -1362,7 +1426,7 @@ extern "C" int twosd_build_cut(twosd_ctx *c, int epi, const double *x, double ti
 
 extern "C" int twosd_cut_stats(twosd_ctx *c, int64_t *out) {
     if (!c || !out) return fail(TWOSD_E_ARG, "cut_stats: NULL");
-    for (int i = 0; i < 3; ++i) out[i] = 0;
+    for (int i = 0; i < 4; ++i) out[i] = 0;
     CutWs *w = c->cut_ws ? (CutWs *)c->cut_ws : nullptr;
     if (!w || !w->fstats) return TWOSD_OK;
     unsigned long long h[16] = {};
@@ -1370,6 +1434,7 @@ extern "C" int twosd_cut_stats(twosd_ctx *c, int64_t *out) {
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipMemcpy(h, w->fstats, sizeof(h), hipMemcpyDeviceToHost));
     for (int i = 0; i < 3; ++i) out[i] = (int64_t)h[i];
+    out[3] = (int64_t)h[9];
     if (getenv("TWOSD_FIX_STAMPS_PRINT"))
         fprintf(stderr, "fixup stamps (cycles summed over waves): rows/setup %llu deltas %llu list %llu chains %llu decide %llu sums %llu\n",
                 h[3], h[4], h[5], h[6], h[7], h[8]);

@@ -206,8 +206,8 @@ class SDContext:
 
     def cut_stats(self):
         """(scenarios re-decided in the restatement's arithmetic, candidates scored, full
-        re-scans) of the last cut (twosd_cut_stats)."""
-        out = np.zeros(3, dtype=np.int64)
+        re-scans, dominated twin vertices left out) of the last cut (twosd_cut_stats)."""
+        out = np.zeros(4, dtype=np.int64)
         check(self.lib.twosd_cut_stats(self.h, ptr(out)))
         return tuple(int(v) for v in out)
 

@@ -12,6 +12,23 @@ pytestmark = pytest.mark.gpu
 G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
+class _env:
+    """Set one environment variable for a block (the library reads TWOSD_CUT_TWINS per cut)."""
+
+    def __init__(self, key, value):
+        self.key, self.value = key, value
+
+    def __enter__(self):
+        self.old = os.environ.get(self.key)
+        os.environ[self.key] = self.value
+
+    def __exit__(self, *a):
+        if self.old is None:
+            os.environ.pop(self.key, None)
+        else:
+            os.environ[self.key] = self.old
+
+
 def _setup(name, nv_src=512, seed=3):
     from sqlp_amd import smps, twosd
     inst = I.load(name)
@@ -200,20 +217,33 @@ def test_cut_storm_at_the_x_where_V_was_built():
     ties = int(((part.max(1) - part.min(1)) <= 1e-9 * (1 + np.abs(part.max(1)))).sum())
     assert ties > N // 4, ties                  # the case this test is about
     for tie_rel in (0.0, 1e-12):
-        cut, mv, ma = twosd._build_cut(epi, x, tie_rel, want_argmax=True)
         a, b, omv, oma = cpu.build_cut(sp.r, sp.T, x, Vm, ctx.rows, vals - sp.r[ctx.rows], np.ones(N), tie_rel=tie_rel,
                                        nthreads=8)
-        assert (ma == oma).all(), (tie_rel, ties, int((ma != oma).sum()))
-        np.testing.assert_allclose(mv, omv, rtol=1e-12, atol=1e-9)
-        assert cut.alpha == pytest.approx(a, rel=1e-8, abs=1e-8)
-        np.testing.assert_allclose(cut.beta, b, rtol=1e-8, atol=1e-8 * (1 + np.abs(b).max()))
+        got = {}
+        # dominated twins left out of the argmax (default) and kept in it: the same picks, bit for bit
+        for twins in ("1", "0"):
+            with _env("TWOSD_CUT_TWINS", twins):
+                cut, mv, ma = twosd._build_cut(epi, x, tie_rel, want_argmax=True)
+                got[twins] = (cut, mv, ma, ctx.cut_stats())
+            assert (ma == oma).all(), (tie_rel, twins, ties, int((ma != oma).sum()))
+            np.testing.assert_allclose(mv, omv, rtol=1e-12, atol=1e-9)
+            assert cut.alpha == pytest.approx(a, rel=1e-8, abs=1e-8)
+            np.testing.assert_allclose(cut.beta, b, rtol=1e-8, atol=1e-8 * (1 + np.abs(b).max()))
+        (c1, mv1, ma1, st1), (c0, mv0, ma0, st0) = got["1"], got["0"]
+        # picks and cut bit for bit; max_val is the MFMA score where the row was decided without the
+        # fixup (more rows are, without twins), the restated score where it was re-decided
+        assert c1.alpha == c0.alpha and np.array_equal(c1.beta, c0.beta) and np.array_equal(ma1, ma0)
+        np.testing.assert_allclose(mv1, mv0, rtol=1e-12)
+        assert st1[3] > 0 and st0[3] == 0, (st1, st0)      # storm's V has twins at x_EV
+        assert st1[0] < st0[0], (st1, st0)                 # fewer scenarios re-decided without them
 
 
 def test_cut_many_exact_ties_overflow_the_logs():
-    """41 vertices with bit-identical scores at every scenario (a real dual plus copies that
-    differ only in a row whose r - T x and deltas are exactly zero): each lane's candidate log
-    overflows (> 8 entries), so the fixup re-scans every vertex in the restatement's order.  The
-    pick is the lowest index, as the strict '>' of subprob.jl:156 keeps the first maximum."""
+    """97 vertices with bit-identical scores at every scenario (a real dual plus copies that
+    differ only in a row whose r - T x and deltas are exactly zero).  Left in the argmax, each
+    lane group's candidate log overflows (~24 > 16 entries), so the fixup re-scans every vertex in the
+    restatement's order; by default they are left out as dominated twins.  Either way the pick is
+    the lowest index, as the strict '>' of subprob.jl:156 keeps the first maximum."""
     from oracle import cpu
     from sqlp_amd import twosd
     ctx, x, V0 = _setup("transship", 512)
@@ -226,23 +256,33 @@ def test_cut_many_exact_ties_overflow_the_logs():
     Vm0 = V0.matrix()
     N = 3000
     vals = I.sample("transship", N, 47)
-    # the vertex most scenarios pick, copied 40 times ahead of the rest
+    # the vertex most scenarios pick, copied 96 times ahead of the rest
     _, _, _, oma0 = cpu.build_cut(sp.r, sp.T, x, Vm0, ctx.rows, vals - sp.r[ctx.rows], np.ones(N), tie_rel=0.0)
     top = int(np.bincount(oma0).argmax())
-    copies = np.repeat(Vm0[top][None, :], 41, axis=0)
-    copies[1:, i0] += np.arange(1, 41, dtype=np.float64)
+    copies = np.repeat(Vm0[top][None, :], 97, axis=0)
+    copies[1:, i0] += np.arange(1, 97, dtype=np.float64)
     V = twosd.sdDualVertexSet(ctx)          # the context's one set (V0): rebuilt with the copies first
     V.clear()
     V.push_batch(np.vstack([copies, Vm0]))
-    assert len(V) == 40 + len(Vm0)                      # copies[0] is Vm0[top] itself
+    assert len(V) == 96 + len(Vm0)                      # copies[0] is Vm0[top] itself
     epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
     twosd.add_scenarios(epi, vals)
     Vm = V.matrix()
     for tie_rel in (0.0, 1e-12):
-        cut, mv, ma = twosd._build_cut(epi, x, tie_rel, want_argmax=True)
         a, b, omv, oma = cpu.build_cut(sp.r, sp.T, x, Vm, ctx.rows, vals - sp.r[ctx.rows], np.ones(N), tie_rel=tie_rel)
         assert (oma == 0).sum() >= (oma0 == top).sum(), (np.bincount(oma)[:45].tolist(), int((oma0 == top).sum()),
-                                                         bool(np.array_equal(Vm[0], Vm0[top])), float(np.abs(Vm[1:41, i0] - Vm0[top, i0]).max()))
-        assert (ma == oma).all(), (tie_rel, int((ma != oma).sum()))
-        assert cut.alpha == pytest.approx(a, rel=1e-8, abs=1e-8)
-        np.testing.assert_allclose(cut.beta, b, rtol=1e-8, atol=1e-8 * (1 + np.abs(b).max()))
+                                                         bool(np.array_equal(Vm[0], Vm0[top])), float(np.abs(Vm[1:97, i0] - Vm0[top, i0]).max()))
+        # the copies' PK rows are the original's, so by default they are dominated twins left out of
+        # the argmax; with TWOSD_CUT_TWINS=0 they stay in and every log of a scenario the copied
+        # vertex wins overflows: the fixup re-scans every vertex
+        for twins in ("1", "0"):
+            with _env("TWOSD_CUT_TWINS", twins):
+                cut, mv, ma = twosd._build_cut(epi, x, tie_rel, want_argmax=True)
+                st = ctx.cut_stats()
+            assert (ma == oma).all(), (tie_rel, twins, int((ma != oma).sum()))
+            assert cut.alpha == pytest.approx(a, rel=1e-8, abs=1e-8)
+            np.testing.assert_allclose(cut.beta, b, rtol=1e-8, atol=1e-8 * (1 + np.abs(b).max()))
+            if twins == "1":
+                assert st[3] >= 96, st
+            else:
+                assert st[3] == 0 and st[2] > 0, st

@@ -86,7 +86,7 @@ def main():
             _, _, _, stp, itp = lp.solve_batch(rows, base, DR, kmax=2000, nthreads=threads)
             allit[p] = np.where(stp == 0, itp, 10 ** 6)
         lp.set_pool(heads)
-        _, _, _, stc, itc, cpick = lp.solve_batch_pool(rows, base, DR, kmax=2000, nthreads=threads)
+        _, _, stc, itc, cpick = lp.solve_batch_pool(rows, base, DR, kmax=2000, nthreads=threads)
         t_cpu = time.perf_counter() - t0
         best = allit.min(0)
         at_pick = allit[picks, np.arange(S)]
