@@ -67,8 +67,10 @@ struct CutParams {
     const double *PK;      // nv x k4
     const double *PKT;     // k4 x vcap
     const double *PKO;     // nv x k4: PK with its columns in the restated order (PKO[v][q] = PK[v][eord[q]])
-    const double *PKTc;    // 4 KB x vcap32: coef_e(x) * PKT, zero padded (cut_argmax2_kernel's LDS-DMA source)
+    const double *PKTc;    // 4 KB x vcap32: coef_e(x) * PKT over the argmax's vertices, zero padded (cut_argmax2_kernel's LDS-DMA source)
     int vcap32;            // row stride of PKTc (a multiple of 32 >= nv)
+    const int *vmap;       // the argmax's vertices (dominated twins left out), ascending: column c of PKTc is vertex vmap[c]
+    const int *nvc;        // their count (device: set per x by cut_compact_kernel)
     const double *base;    // nv: pi_v . bvec in index order (the restatement's base dot)
     const int *eord;       // k: elements by ascending row (the restated score's order)
     const unsigned long long *band_bits;   // max_v (|base[v]| + sum_e |PK[v,e] coef_e| dmax_e), as bits
@@ -113,7 +115,7 @@ __global__ void cut_pk_kernel(int from, int to, int m, int k, int k4, int vcap, 
 // duals come in such groups (vertices differing only on rows where r - T x is 0), and each one
 // made every scenario it won an exact tie the fixup had to re-decide.  tprev[v] is the previous
 // vertex of v's PK-equality group (-1: none), maintained with PK; cut_pktc_kernel drops a vertex
-// whose base equals that of an earlier group member at this x (its base row -inf).
+// whose base equals that of an earlier group member at this x (cut_compact_kernel).
 __global__ void cut_twin_hash_kernel(int from, int to, int k4, const double *__restrict__ PK, unsigned long long *__restrict__ phash) {
     const int v = from + blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= to) return;
@@ -145,28 +147,60 @@ __global__ void __launch_bounds__(256) cut_twin_prev_kernel(int from, int to, in
     if (lane == 0) tprev[v] = best;
 }
 
-// PKTc[kk][v] = coef_kk * PKT[kk][v] over rows [0, rows) x columns [0, vcap32), zero outside
-// [0, k) x [0, nv) (the LDS-DMA source of cut_argmax2_kernel; per x)
-// With base != nullptr, row k holds base[v] (-inf for v >= nv and for a dominated twin): the MFMA
-// then adds the vertex base through a constant 1 in the scenarios' delta column k.
-__global__ void cut_pktc_kernel(int nv, int k, int rows, int vcap, int vcap32, const double *__restrict__ PKT,
-                                const double *__restrict__ coef, const double *__restrict__ base, const int *__restrict__ tprev,
-                                double *__restrict__ PKTc, unsigned long long *__restrict__ ntwin) {
+// The argmax's vertex list at x: every vertex except the dominated twins (v whose base equals
+// that of an earlier member of its PK-equality group), ascending, so that the MFMA pass does no
+// work for them and "lowest index" keeps its meaning.  One block; tprev == nullptr keeps all.
+__global__ void __launch_bounds__(1024) cut_compact_kernel(int nv, const double *__restrict__ base, const int *__restrict__ tprev,
+                                                           int *__restrict__ vmap, int *__restrict__ nvc,
+                                                           unsigned long long *__restrict__ ntwin) {
+    __shared__ int wsum[16];
+    __shared__ int off;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (threadIdx.x == 0) off = 0;
+    __syncthreads();
+    for (int v0 = 0; v0 < nv; v0 += 1024) {
+        const int v = v0 + threadIdx.x;
+        bool keep = v < nv;
+        if (keep && tprev) {
+            const double b = base[v];
+            for (int u = tprev[v]; u >= 0; u = tprev[u])   // tprev[u] < u: the walk ends
+                if (base[u] == b) { keep = false; break; }
+        }
+        const unsigned long long bal = __ballot(keep);
+        const int pos = __popcll(bal & ((1ull << lane) - 1));
+        if (lane == 0) wsum[wid] = __popcll(bal);
+        __syncthreads();
+        int before = off;
+        for (int w = 0; w < wid; ++w) before += wsum[w];
+        if (keep) vmap[before + pos] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int t = 0;
+            for (int w = 0; w < 16; ++w) t += wsum[w];
+            off += t;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        *nvc = off;
+        if (ntwin) *ntwin = (unsigned long long)(nv - off);
+    }
+}
+
+// PKTc[kk][c] = coef_kk * PKT[kk][vmap[c]] over rows [0, rows) x columns [0, vcap32), zero
+// outside [0, k) x [0, nvc) (the LDS-DMA source of cut_argmax2_kernel; per x).
+// With base != nullptr, row k holds base[vmap[c]] (-inf for c >= nvc): the MFMA then adds the
+// vertex base through a constant 1 in the scenarios' delta column k.
+__global__ void cut_pktc_kernel(int k, int rows, int vcap, int vcap32, const double *__restrict__ PKT,
+                                const double *__restrict__ coef, const double *__restrict__ base, const int *__restrict__ vmap,
+                                const int *__restrict__ nvc_p, double *__restrict__ PKTc) {
+    const int nvc = *nvc_p;
     const size_t total = (size_t)rows * vcap32;
     for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
-        const int kk = (int)(idx / vcap32), v = (int)(idx % vcap32);
-        double x = (kk < k && v < nv) ? coef[kk] * PKT[(size_t)kk * vcap + v] : 0.0;
-        if (base && kk == k) {
-            x = v < nv ? base[v] : -INFINITY;
-            if (v < nv && tprev) {
-                for (int u = tprev[v]; u >= 0; u = tprev[u])   // tprev[u] < u: the walk ends
-                    if (base[u] == x) {
-                        x = -INFINITY;
-                        if (ntwin) atomicAdd(ntwin, 1ull);
-                        break;
-                    }
-            }
-        }
+        const int kk = (int)(idx / vcap32), c = (int)(idx % vcap32);
+        const int v = c < nvc ? vmap[c] : 0;
+        double x = (kk < k && c < nvc) ? coef[kk] * PKT[(size_t)kk * vcap + v] : 0.0;
+        if (base && kk == k) x = c < nvc ? base[v] : -INFINITY;
         PKTc[idx] = x;
     }
 }
@@ -311,7 +345,7 @@ __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_
         for (int v = threadIdx.x; v < P.nv; v += 256) hl[v] = 0ull;
     const int g = lane >> 4, j = lane & 15;
     const int ntiles = (P.N + kCutTile2 - 1) / kCutTile2;
-    const int nchunks = (P.nv + kVT2 - 1) / kVT2;
+    const int nchunks = (*P.nvc + kVT2 - 1) / kVT2;   // the argmax's vertices (vmap)
     const int nunits = P.full_units + (ntiles - P.full_units) * P.tail_S;
     const double band = P.band_scale * __longlong_as_double((long long)*P.band_bits);
     const double rel = P.tie_rel;
@@ -408,6 +442,9 @@ __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_
         int pk0, pk1, nt0, nt1;
         combine_ex(rb0, rel, band, g, pk0, nt0);
         combine_ex(rb1, rel, band, g, pk1, nt1);
+        // the picks as vertex indices (the logs keep vmap positions: the fixup translates them)
+        rb0.I = rb0.I >= 0 ? P.vmap[rb0.I] : -1;
+        rb1.I = rb1.I >= 0 ? P.vmap[rb1.I] : -1;
         const int sa = s0 + j, sb = s0 + 16 + j;
         if (tail) {   // this vertex range's result; cut_tail_merge_kernel decides and sums
             if (g == 0) {
@@ -722,7 +759,7 @@ __global__ void __launch_bounds__(256, 3) cut_fixup_kernel(CutParams P, int slot
                 const int sr = __shfl(srow, it);
                 const int c = (fl >> (kCandBits * g)) & 31;
                 const int lv = P.cand[((size_t)sr * 4 + g) * kCandC + i];   // rows past nr: srow = 0, a valid address
-                vv[it] = it >= nr ? -1 : (c > kCandC ? -2 : (i < c ? lv : -1));
+                vv[it] = it >= nr ? -1 : (c > kCandC ? -2 : (i < c ? P.vmap[lv] : -1));   // log entries: vmap positions
             }
 #pragma unroll
             for (int it = 0; it < NIT; ++it) {
@@ -753,7 +790,7 @@ __global__ void __launch_bounds__(256, 3) cut_fixup_kernel(CutParams P, int slot
                     const int pk = (mr != -INFINITY && mr >= thr) ? P.tp_f[o] : 0;
                     const int c = (pk >> (kCandBits * g)) & 31;
                     if (c > kCandC) v = -2;
-                    else if (i < c) v = P.tcand[(o * 4 + g) * kCandC + i];
+                    else if (i < c) v = P.vmap[P.tcand[(o * 4 + g) * kCandC + i]];
                 }
                 const uint64_t has = __ballot(v >= 0);
                 if (__ballot(v == -2)) ovf_rows = 1u;
@@ -994,6 +1031,8 @@ struct CutWs {
     int *eord = nullptr;    // elements by ascending row: the order of the restated score's dot
     unsigned long long *phash = nullptr;   // per vertex: hash of its PK row (bits)
     int *tprev = nullptr;                  // per vertex: previous vertex with a bit-identical PK row, or -1
+    int *vmap = nullptr, *nvc = nullptr;   // per x: the argmax's vertices and their count
+    size_t vmap_cap = 0;
     double *coef = nullptr, *bvec = nullptr, *base = nullptr, *partial = nullptr, *sums = nullptr;
     double *gpart = nullptr, *g = nullptr;
     int *arg = nullptr, *flag = nullptr;
@@ -1029,7 +1068,7 @@ void cut_free(twosd_ctx *c) {
     hipFree(w->val); hipFree(w->hist); hipFree(w->part2); hipFree(w->hist_part);
     hipFree(w->tp_m); hipFree(w->tp_i); hipFree(w->tp_f);
     hipFree(w->cand); hipFree(w->tcand); hipFree(w->band_bits); hipFree(w->fstats);
-    hipFree(w->phash); hipFree(w->tprev);
+    hipFree(w->phash); hipFree(w->tprev); hipFree(w->vmap); hipFree(w->nvc);
     for (auto *p : w->dmax) hipFree(p);
     delete w;
     c->cut_ws = nullptr;
@@ -1305,11 +1344,19 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
             w->pktc_cap = (size_t)rows * vcap32;
         }
         const size_t tot = (size_t)rows * vcap32;
-        hipLaunchKernelGGL(cut_pktc_kernel, dim3((unsigned)std::min<size_t>(4096, (tot + 255) / 256)), dim3(256), 0, c->stream, nv, k,
-                           rows, w->pk_vcap, vcap32, w->PKT, w->coef, w->base, twins ? w->tprev : nullptr, w->PKTc,
-                           w->fstats + 9);
+        if ((size_t)nv > w->vmap_cap) {
+            if ((rc = realloc_dev(&w->vmap, nv))) return rc;
+            w->vmap_cap = nv;
+        }
+        if (!w->nvc && (rc = realloc_dev(&w->nvc, 1))) return rc;
+        hipLaunchKernelGGL(cut_compact_kernel, dim3(1), dim3(1024), 0, c->stream, nv, w->base, twins ? w->tprev : nullptr, w->vmap,
+                           w->nvc, w->fstats + 9);
+        hipLaunchKernelGGL(cut_pktc_kernel, dim3((unsigned)std::min<size_t>(4096, (tot + 255) / 256)), dim3(256), 0, c->stream, k,
+                           rows, w->pk_vcap, vcap32, w->PKT, w->coef, w->base, w->vmap, w->nvc, w->PKTc);
         P.PKTc = w->PKTc;
         P.vcap32 = vcap32;
+        P.vmap = w->vmap;
+        P.nvc = w->nvc;
     }
     P.arg = w->arg; P.val = w->val; P.flag = w->flag; P.hist = d_hist; P.partial = w->partial;
     P.full_units = full; P.tail_S = S;

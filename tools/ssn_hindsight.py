@@ -1,4 +1,4 @@
-"""ssn warm-start diagnosis: is the pivot count limited by the pool's
+"""Warm-start diagnosis for ssn (also storm at x_EV, item 3): is the pivot count limited by the pool's
 CONTENT or by the device SELECTION?  At each bench x point of ssn (the bench protocol: the pool
 refreshed at x from the training stream, 100k-scenario shard, 512-basis pool), a sample of the
 shard's scenarios is solved
@@ -9,7 +9,7 @@ shard's scenarios is solved
     pivots of the oracle from the device's pick (the same start as the GPU).
 Also reported: the rank of the device pick among the pool bases by hindsight pivots, and the
 pivots of the best start by the selection's own key (least primal infeasibility, the CPU pick).
-Usage (GPU box): python tools/ssn_hindsight.py [sample] [threads] [x_points] > profiles/r05/ssn_hindsight.txt
+Usage (GPU box): python tools/ssn_hindsight.py [sample] [threads] [x_points] [ssn|storm] > profiles/r05/ssn_hindsight.txt
 """
 import json
 import os
@@ -32,7 +32,9 @@ def main():
     S = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
     threads = int(sys.argv[2]) if len(sys.argv) > 2 else 16
     x_iters = [int(v) for v in (sys.argv[3] if len(sys.argv) > 3 else "0,4,12,30").split(",")]
-    name, N, POOL = "ssn", 100_000, 512
+    # instance and the bench's shard / pool for it (storm: 1M scenarios, 4096-basis pool)
+    name = sys.argv[4] if len(sys.argv) > 4 else "ssn"
+    N, POOL = {"ssn": (100_000, 512), "storm": (1_000_000, 4096)}[name]
     TRAIN = 4 * POOL
     seed = 20250219
     d = os.path.join(ROOT, "data", "smps", name)
@@ -69,7 +71,7 @@ def main():
         twosd.solve_batch(epi, xx, 0, N, want_pi=False)
         shard_piv = ctx.lp_stats()[0] / N
         _, _, _, st = twosd.solve_batch(sam, xx, 0, S, want_pi=False)
-        gpu_it = ctx.last_lp_iters(S)
+        gpu_it = ctx.last_lp_iters(S)[0]
         picks = ctx.last_pool_picks(S)
         P = ctx.pool_size()
         heads = np.stack([ctx.pool_get(p) for p in range(P)])
@@ -85,8 +87,11 @@ def main():
                 continue
             _, _, _, stp, itp = lp.solve_batch(rows, base, DR, kmax=2000, nthreads=threads)
             allit[p] = np.where(stp == 0, itp, 10 ** 6)
-        lp.set_pool(heads)
-        _, _, stc, itc, cpick = lp.solve_batch_pool(rows, base, DR, kmax=2000, nthreads=threads)
+        if P <= 1024:   # the oracle's pool keeps a dense inverse per basis (storm's 4096: 9 GB): skipped there
+            lp.set_pool(heads)
+            _, _, stc, itc, cpick = lp.solve_batch_pool(rows, base, DR, kmax=2000, nthreads=threads)
+        else:
+            stc, itc = np.zeros(1, np.int32), np.full(1, -1)
         t_cpu = time.perf_counter() - t0
         best = allit.min(0)
         at_pick = allit[picks, np.arange(S)]
