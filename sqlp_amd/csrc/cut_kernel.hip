@@ -71,6 +71,8 @@ struct CutParams {
     int vcap32;            // row stride of PKTc (a multiple of 32 >= nv)
     const int *vmap;       // the argmax's vertices (dominated twins left out), ascending: column c of PKTc is vertex vmap[c]
     const int *nvc;        // their count (device: set per x by cut_compact_kernel)
+    const double *PKOc;    // PKO rows of the argmax's vertices (row c: vertex vmap[c]), per x
+    const double *basec;   // base of the argmax's vertices, per x
     const double *base;    // nv: pi_v . bvec in index order (the restatement's base dot)
     const int *eord;       // k: elements by ascending row (the restated score's order)
     const unsigned long long *band_bits;   // max_v (|base[v]| + sum_e |PK[v,e] coef_e| dmax_e), as bits
@@ -184,6 +186,22 @@ __global__ void __launch_bounds__(1024) cut_compact_kernel(int nv, const double 
     if (threadIdx.x == 0) {
         *nvc = off;
         if (ntwin) *ntwin = (unsigned long long)(nv - off);
+    }
+}
+
+// PKOc[c] = PKO[vmap[c]], basec[c] = base[vmap[c]] for c < nvc: the fixup works on the argmax's
+// positions (its logs hold them), so its candidate loads need no translation
+__global__ void cut_compact_rows_kernel(int nv, int k4, const int *__restrict__ vmap, const int *__restrict__ nvc_p,
+                                        const double *__restrict__ PKO, const double *__restrict__ base,
+                                        double *__restrict__ PKOc, double *__restrict__ basec) {
+    const int nvc = *nvc_p;
+    const size_t total = (size_t)nv * k4;
+    for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
+        const int c = (int)(idx / k4), q = (int)(idx % k4);
+        if (c >= nvc) continue;
+        const int v = vmap[c];
+        PKOc[idx] = PKO[(size_t)v * k4 + q];
+        if (q == 0) basec[c] = base[v];
     }
 }
 
@@ -705,8 +723,14 @@ __global__ void __launch_bounds__(256, 3) cut_fixup_kernel(CutParams P, int slot
 #else
 #define FSTAMP(i)
 #endif
-    for (int sb0 = gw * 64; sb0 < P.N; sb0 += nw * 64) {
-    const int myflag = sb0 + lane < P.N ? P.flag[sb0 + lane] : 0;
+    // pass 0: the whole-tile rows, 64 consecutive scenarios per wave step; pass 1: the tail rows
+    // (each a batch of its own), spread over all waves (lane L of wave gw: scenario t0 + gw + L nw)
+    // so that the waves holding the last scenarios do not run one serial batch per tail row
+    for (int pass = 0; pass < 2; ++pass) {
+    const int hi = pass ? P.N : min(t0, P.N), lstride = pass ? nw : 1;
+    for (int sb0 = pass ? t0 + gw : gw * 64; sb0 < hi; sb0 += nw * 64) {
+    const int sl = sb0 + lane * lstride;
+    const int myflag = sl < hi ? P.flag[sl] : 0;
     uint64_t todo = __ballot(myflag != 0);
     while (todo) {
         // ---- the batch: up to kFxR whole-tile rows, or one tail row
@@ -714,7 +738,7 @@ __global__ void __launch_bounds__(256, 3) cut_fixup_kernel(CutParams P, int slot
         bool tailb = false;
         while (todo && nr < kFxR) {
             const int bit = (int)__builtin_ctzll(todo);
-            const int s = sb0 + bit;
+            const int s = sb0 + bit * lstride;
             if (s >= t0) {                       // a tail row: alone in its batch
                 if (nr > 0) break;
                 tailb = true;
@@ -759,7 +783,7 @@ __global__ void __launch_bounds__(256, 3) cut_fixup_kernel(CutParams P, int slot
                 const int sr = __shfl(srow, it);
                 const int c = (fl >> (kCandBits * g)) & 31;
                 const int lv = P.cand[((size_t)sr * 4 + g) * kCandC + i];   // rows past nr: srow = 0, a valid address
-                vv[it] = it >= nr ? -1 : (c > kCandC ? -2 : (i < c ? P.vmap[lv] : -1));   // log entries: vmap positions
+                vv[it] = it >= nr ? -1 : (c > kCandC ? -2 : (i < c ? lv : -1));   // log entries: argmax positions (vmap)
             }
 #pragma unroll
             for (int it = 0; it < NIT; ++it) {
@@ -790,7 +814,7 @@ __global__ void __launch_bounds__(256, 3) cut_fixup_kernel(CutParams P, int slot
                     const int pk = (mr != -INFINITY && mr >= thr) ? P.tp_f[o] : 0;
                     const int c = (pk >> (kCandBits * g)) & 31;
                     if (c > kCandC) v = -2;
-                    else if (i < c) v = P.vmap[P.tcand[(o * 4 + g) * kCandC + i]];
+                    else if (i < c) v = P.tcand[(o * 4 + g) * kCandC + i];
                 }
                 const uint64_t has = __ballot(v >= 0);
                 if (__ballot(v == -2)) ovf_rows = 1u;
@@ -804,19 +828,20 @@ __global__ void __launch_bounds__(256, 3) cut_fixup_kernel(CutParams P, int slot
         FSTAMP(2)
         st_rows += nr;
         st_cands += nc;
-        // 3. restated scores, one lane per candidate: base[v] + chain_dot (restated_score's order)
+        // 3. restated scores, one lane per candidate: base[v] + chain_dot (restated_score's order);
+        // candidates are argmax positions (vertex vmap[c]: PKOc / basec rows)
         for (int cb = 0; cb < nc; cb += 64) {
             const int c = cb + lane;
             const int cr = F.cvr[c < nc ? c : 0];
             const int r = cr >> 28, v = cr & 0x0fffffff;
-            const double bvv = P.base[v];
-            const double t = chain_dot(reinterpret_cast<const double2 *>(P.PKO + (size_t)v * P.k4), cq, F.dvr[r], P.k4);
+            const double bvv = P.basec[v];
+            const double t = chain_dot(reinterpret_cast<const double2 *>(P.PKOc + (size_t)v * P.k4), cq, F.dvr[r], P.k4);
             if (c < nc) F.cs[c] = bvv + t;
         }
         wave_lds_sync();
         FSTAMP(3)
         // 4. lane r decides row r over its candidates (the rule takes the lowest vertex among the
-        // qualifying ones, whatever their list order)
+        // qualifying ones, whatever their list order; positions order as the vertices)
         int best = 0x7fffffff;
         double bv = -INFINITY;
         if (lane < nr && !((ovf_rows >> lane) & 1)) {
@@ -836,24 +861,26 @@ __global__ void __launch_bounds__(256, 3) cut_fixup_kernel(CutParams P, int slot
         if (resc) P.flag[srow] = kFlagRescan;
         st_full += __popc(ovf_rows);
         FSTAMP(4)
-        // 5. outputs and sums, rows in batch (= scenario) order; the picks' PKO rows in one round trip
-        if (lane < nr && !resc) {
-            P.arg[srow] = best == 0x7fffffff ? -1 : best;
-            P.val[srow] = best == 0x7fffffff ? -INFINITY : bv;
-        }
+        // 5. outputs and sums, rows in batch (= scenario) order; the picks' vertex indices and PKO
+        // rows in one round trip
+        const bool mine = lane < nr && best != 0x7fffffff;
+        const int bvx = mine ? P.vmap[best] : -1;
         {
             double pa[kFxR], pb[kFxR];
 #pragma unroll
             for (int r = 0; r < kFxR; ++r) {
                 const int b = __shfl(best, r < nr ? r : 0);
-                const double *po = P.PKO + (size_t)(b == 0x7fffffff ? 0 : b) * P.k4;
+                const double *po = P.PKOc + (size_t)(b == 0x7fffffff ? 0 : b) * P.k4;
                 pa[r] = po[lane < P.k4 ? lane : 0];
                 pb[r] = po[lane + 64 < P.k4 ? lane + 64 : 0];
             }
             // lane r: its row's p and histogram weight (one load, one atomic instruction for all rows)
-            const bool mine = lane < nr && best != 0x7fffffff;
             const double pr = lane < nr ? P.w[srow] * P.inv_total : 0.0;
-            if (mine) atomicAdd(&P.hist[best], (unsigned long long)__double2ull_rn(pr * kFix));
+            if (lane < nr && !resc) {
+                P.arg[srow] = bvx;
+                P.val[srow] = mine ? bv : -INFINITY;
+            }
+            if (mine) atomicAdd(&P.hist[bvx], (unsigned long long)__double2ull_rn(pr * kFix));
 #pragma unroll
             for (int r = 0; r < kFxR; ++r) {
                 if (r >= nr) break;
@@ -868,6 +895,7 @@ __global__ void __launch_bounds__(256, 3) cut_fixup_kernel(CutParams P, int slot
         }
         wave_lds_sync();   // the next batch rewrites the LDS lists
         FSTAMP(5)
+    }
     }
     }
     double *out = P.partial + (size_t)(slot0 + gw) * (P.k + 1);
@@ -1033,6 +1061,8 @@ struct CutWs {
     int *tprev = nullptr;                  // per vertex: previous vertex with a bit-identical PK row, or -1
     int *vmap = nullptr, *nvc = nullptr;   // per x: the argmax's vertices and their count
     size_t vmap_cap = 0;
+    double *PKOc = nullptr, *basec = nullptr;   // per x: their PKO rows and bases (vmap order)
+    size_t pkoc_cap = 0;
     double *coef = nullptr, *bvec = nullptr, *base = nullptr, *partial = nullptr, *sums = nullptr;
     double *gpart = nullptr, *g = nullptr;
     int *arg = nullptr, *flag = nullptr;
@@ -1068,7 +1098,7 @@ void cut_free(twosd_ctx *c) {
     hipFree(w->val); hipFree(w->hist); hipFree(w->part2); hipFree(w->hist_part);
     hipFree(w->tp_m); hipFree(w->tp_i); hipFree(w->tp_f);
     hipFree(w->cand); hipFree(w->tcand); hipFree(w->band_bits); hipFree(w->fstats);
-    hipFree(w->phash); hipFree(w->tprev); hipFree(w->vmap); hipFree(w->nvc);
+    hipFree(w->phash); hipFree(w->tprev); hipFree(w->vmap); hipFree(w->nvc); hipFree(w->PKOc); hipFree(w->basec);
     for (auto *p : w->dmax) hipFree(p);
     delete w;
     c->cut_ws = nullptr;
@@ -1349,14 +1379,22 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
             w->vmap_cap = nv;
         }
         if (!w->nvc && (rc = realloc_dev(&w->nvc, 1))) return rc;
+        if ((size_t)nv > w->pkoc_cap) {
+            if ((rc = realloc_dev(&w->PKOc, (size_t)nv * k4)) || (rc = realloc_dev(&w->basec, nv))) return rc;
+            w->pkoc_cap = nv;
+        }
         hipLaunchKernelGGL(cut_compact_kernel, dim3(1), dim3(1024), 0, c->stream, nv, w->base, twins ? w->tprev : nullptr, w->vmap,
                            w->nvc, w->fstats + 9);
         hipLaunchKernelGGL(cut_pktc_kernel, dim3((unsigned)std::min<size_t>(4096, (tot + 255) / 256)), dim3(256), 0, c->stream, k,
                            rows, w->pk_vcap, vcap32, w->PKT, w->coef, w->base, w->vmap, w->nvc, w->PKTc);
+        hipLaunchKernelGGL(cut_compact_rows_kernel, dim3((unsigned)std::min<size_t>(2048, ((size_t)nv * k4 + 255) / 256)), dim3(256), 0,
+                           c->stream, nv, k4, w->vmap, w->nvc, w->PKO, w->base, w->PKOc, w->basec);
         P.PKTc = w->PKTc;
         P.vcap32 = vcap32;
         P.vmap = w->vmap;
         P.nvc = w->nvc;
+        P.PKOc = w->PKOc;
+        P.basec = w->basec;
     }
     P.arg = w->arg; P.val = w->val; P.flag = w->flag; P.hist = d_hist; P.partial = w->partial;
     P.full_units = full; P.tail_S = S;

@@ -81,6 +81,8 @@ def main():
         _, _, _, st0, it0 = lp.solve_batch(rows, base, DR, kmax=2000, nthreads=threads)
         allit = np.full((P, S), 10 ** 6, dtype=np.int64)
         for p in range(P):
+            if p % 128 == 0:
+                print(f"x {it}: basis {p} of {P}", file=sys.stderr, flush=True)   # progress (a long storm pass)
             try:
                 lp.set_basis(heads[p])
             except RuntimeError:
@@ -93,6 +95,9 @@ def main():
         else:
             stc, itc = np.zeros(1, np.int32), np.full(1, -1)
         t_cpu = time.perf_counter() - t0
+        if os.environ.get("HINDSIGHT_DUMP"):   # the per-(basis, scenario) pivots for an offline study of selection keys
+            np.savez_compressed(f"{os.environ['HINDSIGHT_DUMP']}_{name}_x{it}.npz", allit=allit.astype(np.int32), heads=heads,
+                                picks=picks, gpu_it=gpu_it, vals=vals, x=xx, rows=rows, it0=it0)
         best = allit.min(0)
         at_pick = allit[picks, np.arange(S)]
         rank = (allit < at_pick[None, :]).sum(0)      # pool bases strictly better than the pick
