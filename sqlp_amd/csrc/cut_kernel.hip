@@ -656,9 +656,46 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-// t = sum_q PKO[v][q] (cq[q] dq[q]) in q order (the restated k-term dot of one candidate; the
-// products past k are 0 and leave t unchanged: t is never -0).  The PKO row is read in groups of
-// 32 elements (16 dwordx4 loads), the next group's loads issued before this group's adds.
+// t = sum_q PKO[v][q] wq[q] in q order, wq[q] = cq[q] dq[q] (the restated k-term dot of one
+// candidate; the products past k are 0 and leave t unchanged: t is never -0).  The PKO row is read
+// in groups of 32 elements (16 dwordx4 loads), the next group's loads issued before this group's adds.
+__device__ __forceinline__ double chain_dot_w(const double2 *__restrict__ po, const double *wq, int k4) {
+#pragma clang fp contract(off)
+    constexpr int GQ = 8;    // pairs per group (16 elements); k4 <= 128: at most 8 groups
+    const int k2 = k4 / 2;
+    double t = 0.0;
+    double2 a[GQ], b[GQ];
+    auto load = [&](double2 (&x)[GQ], int g) {
+#pragma unroll
+        for (int u = 0; u < GQ; ++u) {
+            const int pu = g * GQ + u;
+            const double2 ld = po[pu < k2 ? pu : k2 - 1];
+            x[u] = pu < k2 ? ld : make_double2(0.0, 0.0);
+        }
+    };
+    auto add = [&](const double2 (&x)[GQ], int g) {
+#pragma unroll
+        for (int u = 0; u < GQ; ++u) {
+            const int q = 2 * (g * GQ + u);
+            if (q < k4) {   // uniform
+                t = t + x[u].x * wq[q];
+                t = t + x[u].y * wq[q + 1];
+            }
+        }
+    };
+    const int ng = (k2 + GQ - 1) / GQ;
+    load(a, 0);
+    for (int g = 0; g < ng; g += 2) {   // ping-pong: group g + 1 in flight while g is added
+        if (g + 1 < ng) load(b, g + 1);
+        add(a, g);
+        if (g + 1 >= ng) break;
+        if (g + 2 < ng) load(a, g + 2);
+        add(b, g + 1);
+    }
+    return t;
+}
+
+// chain_dot_w with the products cq[q] dq[q] formed in the loop (the rescan's one-row form)
 __device__ __forceinline__ double chain_dot(const double2 *__restrict__ po, const double *cq, const double *dq, int k4) {
 #pragma clang fp contract(off)
     constexpr int GQ = 8;    // pairs per group (16 elements); k4 <= 128: at most 8 groups
@@ -750,21 +787,24 @@ __global__ void __launch_bounds__(256, 3) cut_fixup_kernel(CutParams P, int slot
             if (tailb) break;
         }
         FSTAMP(0)
-        // 1. the rows' deltas in the restated order (zero past k), all loads in one round trip
+        // 1. the rows' deltas in the restated order, all loads in one round trip: the products
+        // coef_e dv_e of the restated dot into LDS (zero past k; the same operation the chain would
+        // do), the raw deltas kept in registers for the S_e sums
+        double d0[kFxR], d1[kFxR];
         {
-            double d0[kFxR], d1[kFxR];
 #pragma unroll
             for (int r = 0; r < kFxR; ++r) {
                 const int s = __shfl(srow, r < nr ? r : 0);
                 const double *dr = P.dv + (size_t)s * P.k;
-                d0[r] = dr[e0 >= 0 ? e0 : 0];
-                d1[r] = dr[e1 >= 0 ? e1 : 0];
+                d0[r] = e0 >= 0 ? dr[e0] : 0.0;
+                d1[r] = e1 >= 0 ? dr[e1] : 0.0;
             }
+            const double c0 = cq[lane], c1 = cq[lane + 64];
 #pragma unroll
             for (int r = 0; r < kFxR; ++r) {
                 if (r < nr) {
-                    F.dvr[r][lane] = e0 >= 0 ? d0[r] : 0.0;
-                    F.dvr[r][lane + 64] = e1 >= 0 ? d1[r] : 0.0;
+                    F.dvr[r][lane] = c0 * d0[r];
+                    F.dvr[r][lane + 64] = c1 * d1[r];
                 }
             }
         }
@@ -835,7 +875,7 @@ __global__ void __launch_bounds__(256, 3) cut_fixup_kernel(CutParams P, int slot
             const int cr = F.cvr[c < nc ? c : 0];
             const int r = cr >> 28, v = cr & 0x0fffffff;
             const double bvv = P.basec[v];
-            const double t = chain_dot(reinterpret_cast<const double2 *>(P.PKOc + (size_t)v * P.k4), cq, F.dvr[r], P.k4);
+            const double t = chain_dot_w(reinterpret_cast<const double2 *>(P.PKOc + (size_t)v * P.k4), F.dvr[r], P.k4);
             if (c < nc) F.cs[c] = bvv + t;
         }
         wave_lds_sync();
@@ -889,8 +929,8 @@ __global__ void __launch_bounds__(256, 3) cut_fixup_kernel(CutParams P, int slot
                 const double p = __shfl(pr, r);
                 if (b == 0x7fffffff) continue;   // no finite score: no pick (as the argmax pass leaves it)
                 if (lane == 0) pv_sum = fma(p, bvr, pv_sum);
-                if (e0 >= 0) Sq[0] = fma(p * pa[r], F.dvr[r][lane], Sq[0]);
-                if (e1 >= 0) Sq[1] = fma(p * pb[r], F.dvr[r][lane + 64], Sq[1]);
+                if (e0 >= 0) Sq[0] = fma(p * pa[r], d0[r], Sq[0]);
+                if (e1 >= 0) Sq[1] = fma(p * pb[r], d1[r], Sq[1]);
             }
         }
         wave_lds_sync();   // the next batch rewrites the LDS lists

@@ -329,7 +329,7 @@ def test_training_cap_setting_and_env(monkeypatch):
     TWOSD_TRAIN_KCAP is read as a setting (0 = auto) on the native side for every caller."""
     ctx = _storm_ctx()
     monkeypatch.delenv("TWOSD_TRAIN_KCAP", raising=False)
-    assert ctx.training_cap(3 * 11 * 1000, 1000) == 33          # exact integer 3 x mean: no round-up
+    assert ctx.training_cap(11 * 1000, 1000) == 33              # 3 x the mean, an exact integer: no round-up
     assert ctx.training_cap(100, 1000) == 32                    # floor 32
     ctx.set_refresh_kcap(40)
     assert ctx.training_cap(100, 1000) == 40
