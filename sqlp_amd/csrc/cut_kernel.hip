@@ -282,18 +282,21 @@ __device__ __forceinline__ double band_floor(double M, double rel, double band) 
 
 // Running state of one scenario row over the vertices one lane sees, in increasing vertex
 // order: M = max so far, thr = band_floor(M), I = the first vertex scoring M, n = entries in
-// this lane's candidate log (kCandC + 1: overflowed).
-struct RowEx { double M, thr; int I, n; };
+// this lane's candidate log (kCandC + 1: overflowed), f = its first entry.  The first entry
+// stays in a register and is stored (log[0]) only for a row the fixup will read: most rows
+// just raise their maximum past the band again and again, and each raise restarts the log.
+struct RowEx { double M, thr; int I, n, f; };
 
 // s >= thr: s enters the band of the running max (or raises it)
 __device__ __forceinline__ void row_log(RowEx &b, double s, int v, double rel, double band, int *log) {
     if (s == -INFINITY) return;                  // padding vertices (-inf base row) never enter
     const double tn = band_floor(s, rel, band);
     if (tn > b.M) {                              // every earlier entry is below the band for good
-        log[0] = v;
+        b.f = v;
         b.n = 1;
     } else {
-        if (b.n < kCandC) log[b.n] = v;
+        if (b.n == 0) b.f = v;
+        else if (b.n < kCandC) log[b.n] = v;
         b.n = min(b.n + 1, kCandC + 1);
     }
     if (s > b.M) { b.M = s; b.I = v; b.thr = tn; }
@@ -390,7 +393,7 @@ __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_
             if (e == P.k) a0[kb] = a1[kb] = 1.0;   // x the base row of the chunk
         }
         RowEx rb0, rb1;   // scenario s0 + j / s0 + 16 + j over this lane's vertices v0 + g + 4r (+16)
-        rb0.M = -INFINITY; rb0.thr = -INFINITY; rb0.I = -1; rb0.n = 0;
+        rb0.M = -INFINITY; rb0.thr = -INFINITY; rb0.I = -1; rb0.n = 0; rb0.f = 0;
         rb1 = rb0;
         // this lane's candidate logs of the two scenarios (rows padded to whole tiles)
         int *log0 = tail ? P.tcand + ((((size_t)(s0 + j - P.full_units * kCutTile2)) * P.tail_S + range) * 4 + g) * kCandC
@@ -460,6 +463,9 @@ __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_
         int pk0, pk1, nt0, nt1;
         combine_ex(rb0, rel, band, g, pk0, nt0);
         combine_ex(rb1, rel, band, g, pk1, nt1);
+        // the logs' first entries, for the rows the fixup reads (every tail row: the merge decides)
+        if (rb0.n > 0 && (tail || nt0 >= 2)) log0[0] = rb0.f;
+        if (rb1.n > 0 && (tail || nt1 >= 2)) log0[lstep] = rb1.f;
         // the picks as vertex indices (the logs keep vmap positions: the fixup translates them)
         rb0.I = rb0.I >= 0 ? P.vmap[rb0.I] : -1;
         rb1.I = rb1.I >= 0 ? P.vmap[rb1.I] : -1;
