@@ -1683,8 +1683,7 @@ extern "C" int twosd_last_pool_picks(twosd_ctx *c, int N, int *picks) {
 
 extern "C" int twosd_invalidate_x(twosd_ctx *c) {
     if (!c) return fail(TWOSD_E_ARG, "invalidate_x: NULL context");
-    c->prep_valid = false;
-    cut_invalidate_pk(c);
+    c->prep_valid = false;   // (the cut's PK rows do not depend on x: kept)
     return TWOSD_OK;
 }
 

@@ -43,6 +43,7 @@
 //   cut_reduce_kernel  deterministic fixed-order sum of the partial slots
 //   cut_g_kernel(s)    g = sum_v h_v pi_v (two-level, fixed order)
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 #include <math.h>
 #include <algorithm>
 #include <cstdlib>
@@ -129,6 +130,11 @@ __global__ void cut_twin_hash_kernel(int from, int to, int k4, const double *__r
     phash[v] = h;
 }
 
+__global__ void cut_iota_kernel(int *v, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = i;
+}
+
 // tprev[v] = the highest u < v with PK row u bit-identical to PK row v (one wavefront per vertex)
 __global__ void __launch_bounds__(256) cut_twin_prev_kernel(int from, int to, int k4, const double *__restrict__ PK,
                                                             const unsigned long long *__restrict__ phash, int *__restrict__ tprev) {
@@ -187,6 +193,25 @@ __global__ void __launch_bounds__(1024) cut_compact_kernel(int nv, const double 
         *nvc = off;
         if (ntwin) *ntwin = (unsigned long long)(nv - off);
     }
+}
+
+// The same links for all vertices at once from the (hash, vertex) pairs sorted by hash (stable:
+// vertices ascending within a hash): the previous entry of a run with a bit-identical row is the
+// highest lower twin.  O(nv log nv) instead of cut_twin_prev_kernel's O(nv^2) for a rebuild.
+__global__ void cut_twin_sorted_kernel(int nv, int k4, const double *__restrict__ PK, const unsigned long long *__restrict__ hs,
+                                       const int *__restrict__ vs, int *__restrict__ tprev) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nv) return;
+    const int v = vs[i];
+    int prev = -1;
+    for (int j = i - 1; j >= 0 && hs[j] == hs[i]; --j) {   // runs are short (twin groups)
+        const int u = vs[j];
+        bool same = true;
+        for (int e = 0; e < k4 && same; ++e)
+            same = __double_as_longlong(PK[(size_t)u * k4 + e]) == __double_as_longlong(PK[(size_t)v * k4 + e]);
+        if (same) { prev = u; break; }
+    }
+    tprev[v] = prev;
 }
 
 // PKOc[c] = PKO[vmap[c]], basec[c] = base[vmap[c]] for c < nvc: the fixup works on the argmax's
@@ -287,23 +312,28 @@ __device__ __forceinline__ double band_floor(double M, double rel, double band) 
 // just raise their maximum past the band again and again, and each raise restarts the log.
 struct RowEx { double M, thr; int I, n, f; };
 
-// s >= thr: s enters the band of the running max (or raises it)
-__device__ __forceinline__ void row_log(RowEx &b, double s, int v, double rel, double band, int *log) {
+// s >= thr: s enters the band of the running max (or raises it).  HOLD: the first entry is kept
+// in b.f (stored at the end of the tile for the rows the fixup reads); otherwise it is stored at
+// once (the instantiations at 3 blocks per CU have no register to spare for it)
+template <bool HOLD>
+__device__ __forceinline__ void row_log(RowEx &b, double s, int v, double rel, double band, int *lbase, unsigned lo) {
     if (s == -INFINITY) return;                  // padding vertices (-inf base row) never enter
     const double tn = band_floor(s, rel, band);
     if (tn > b.M) {                              // every earlier entry is below the band for good
-        b.f = v;
+        if (HOLD) b.f = v;
+        else lbase[lo] = v;
         b.n = 1;
     } else {
-        if (b.n == 0) b.f = v;
-        else if (b.n < kCandC) log[b.n] = v;
+        if (HOLD && b.n == 0) b.f = v;
+        else if (b.n < kCandC) lbase[lo + b.n] = v;
         b.n = min(b.n + 1, kCandC + 1);
     }
     if (s > b.M) { b.M = s; b.I = v; b.thr = tn; }
 }
 
-__device__ __forceinline__ void row_fast(RowEx &b, double s, int v, double rel, double band, int *log) {
-    if (__builtin_expect(s >= b.thr, 0)) row_log(b, s, v, rel, band, log);
+template <bool HOLD>
+__device__ __forceinline__ void row_fast(RowEx &b, double s, int v, double rel, double band, int *lbase, unsigned lo) {
+    if (__builtin_expect(s >= b.thr, 0)) row_log<HOLD>(b, s, v, rel, band, lbase, lo);
 }
 
 // ---- v2: the score tile transposed -- MFMA A operand = the staged vertex chunk, B operand =
@@ -359,6 +389,7 @@ __device__ __forceinline__ void combine_ex(RowEx &rb, double rel, double band, i
 template <int KB>
 __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_argmax2_kernel(CutParams P) {
     __shared__ double Bs[2][4 * KB * kLdsRow2];     // double-buffered chunk (k-major)
+    constexpr bool kHold = !(TWOSD_CUT_LB3 && KB <= 22);   // a register for the logs' first entries (2 blocks per CU)
     extern __shared__ unsigned long long hl[];      // nv entries when P.hist_lds
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar staging loop
@@ -396,9 +427,11 @@ __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_
         rb0.M = -INFINITY; rb0.thr = -INFINITY; rb0.I = -1; rb0.n = 0; rb0.f = 0;
         rb1 = rb0;
         // this lane's candidate logs of the two scenarios (rows padded to whole tiles)
-        int *log0 = tail ? P.tcand + ((((size_t)(s0 + j - P.full_units * kCutTile2)) * P.tail_S + range) * 4 + g) * kCandC
-                         : P.cand + (((size_t)(s0 + j)) * 4 + g) * kCandC;
-        const size_t lstep = (size_t)16 * (tail ? P.tail_S : 1) * 4 * kCandC;   // scenario + 16
+        // (a wave-uniform base and a 32-bit element offset: one VGPR per lane instead of a pointer pair)
+        int *const lbase = tail ? P.tcand : P.cand;
+        const unsigned log0 = tail ? (unsigned)(((((size_t)(s0 + j - P.full_units * kCutTile2)) * P.tail_S + range) * 4 + g) * kCandC)
+                                      : (unsigned)((((size_t)(s0 + j)) * 4 + g) * kCandC);
+        const unsigned lstep = 16u * (tail ? P.tail_S : 1) * 4 * kCandC;   // scenario + 16
 
         // chunk staging by LDS-DMA (global_load_lds_dwordx4, no VGPR round trip): instruction i
         // of the chunk writes k-rows 4i .. 4i+3 (1 KiB, lane-linear), lane L the 16 bytes of
@@ -450,13 +483,13 @@ __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_
             // include the base (-inf past nv).
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                row_fast(rb0, c00[r], v0 + g + 4 * r, rel, band, log0);
-                row_fast(rb1, c01[r], v0 + g + 4 * r, rel, band, log0 + lstep);
+                row_fast<kHold>(rb0, c00[r], v0 + g + 4 * r, rel, band, lbase, log0);
+                row_fast<kHold>(rb1, c01[r], v0 + g + 4 * r, rel, band, lbase, log0 + lstep);
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                row_fast(rb0, c10[r], v0 + 16 + g + 4 * r, rel, band, log0);
-                row_fast(rb1, c11[r], v0 + 16 + g + 4 * r, rel, band, log0 + lstep);
+                row_fast<kHold>(rb0, c10[r], v0 + 16 + g + 4 * r, rel, band, lbase, log0);
+                row_fast<kHold>(rb1, c11[r], v0 + 16 + g + 4 * r, rel, band, lbase, log0 + lstep);
             }
             __syncthreads();
         }
@@ -464,8 +497,8 @@ __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_
         combine_ex(rb0, rel, band, g, pk0, nt0);
         combine_ex(rb1, rel, band, g, pk1, nt1);
         // the logs' first entries, for the rows the fixup reads (every tail row: the merge decides)
-        if (rb0.n > 0 && (tail || nt0 >= 2)) log0[0] = rb0.f;
-        if (rb1.n > 0 && (tail || nt1 >= 2)) log0[lstep] = rb1.f;
+        if (kHold && rb0.n > 0 && (tail || nt0 >= 2)) lbase[log0] = rb0.f;
+        if (kHold && rb1.n > 0 && (tail || nt1 >= 2)) lbase[log0 + lstep] = rb1.f;
         // the picks as vertex indices (the logs keep vmap positions: the fixup translates them)
         rb0.I = rb0.I >= 0 ? P.vmap[rb0.I] : -1;
         rb1.I = rb1.I >= 0 ? P.vmap[rb1.I] : -1;
@@ -1105,6 +1138,10 @@ struct CutWs {
     int *eord = nullptr;    // elements by ascending row: the order of the restated score's dot
     unsigned long long *phash = nullptr;   // per vertex: hash of its PK row (bits)
     int *tprev = nullptr;                  // per vertex: previous vertex with a bit-identical PK row, or -1
+    unsigned long long *tw_hs = nullptr;   // twin rebuild by sort: sorted hashes, vertex ids in / out, cub scratch
+    int *tw_vin = nullptr, *tw_vout = nullptr;
+    void *tw_tmp = nullptr;
+    size_t tw_cap = 0, tw_tmp_bytes = 0;
     int *vmap = nullptr, *nvc = nullptr;   // per x: the argmax's vertices and their count
     size_t vmap_cap = 0;
     double *PKOc = nullptr, *basec = nullptr;   // per x: their PKO rows and bases (vmap order)
@@ -1144,10 +1181,16 @@ void cut_free(twosd_ctx *c) {
     hipFree(w->val); hipFree(w->hist); hipFree(w->part2); hipFree(w->hist_part);
     hipFree(w->tp_m); hipFree(w->tp_i); hipFree(w->tp_f);
     hipFree(w->cand); hipFree(w->tcand); hipFree(w->band_bits); hipFree(w->fstats);
-    hipFree(w->phash); hipFree(w->tprev); hipFree(w->vmap); hipFree(w->nvc); hipFree(w->PKOc); hipFree(w->basec);
+    hipFree(w->phash); hipFree(w->tprev); hipFree(w->tw_hs); hipFree(w->tw_vin); hipFree(w->tw_vout); hipFree(w->tw_tmp); hipFree(w->vmap); hipFree(w->nvc); hipFree(w->PKOc); hipFree(w->basec);
     for (auto *p : w->dmax) hipFree(p);
     delete w;
     c->cut_ws = nullptr;
+}
+
+void cut_truncate_pk(twosd_ctx *c, int size) {
+    if (!c->cut_ws) return;
+    CutWs *w = (CutWs *)c->cut_ws;
+    if (w->pk_count > size) w->pk_count = size;   // twin links point to lower vertices: still valid
 }
 
 void cut_invalidate_pk(twosd_ctx *c) {
@@ -1265,8 +1308,31 @@ static int update_pk(twosd_ctx *c) {
         const int nn = nv - w->pk_count;
         hipLaunchKernelGGL(cut_twin_hash_kernel, dim3((nn + 255) / 256), dim3(256), 0, c->stream, w->pk_count, nv, k4, w->PK,
                            w->phash);
-        hipLaunchKernelGGL(cut_twin_prev_kernel, dim3((nn + 3) / 4), dim3(256), 0, c->stream, w->pk_count, nv, k4, w->PK,
-                           w->phash, w->tprev);
+        if ((long long)nn * nv <= (1ll << 22)) {   // a few new vertices: scan the earlier ones
+            hipLaunchKernelGGL(cut_twin_prev_kernel, dim3((nn + 3) / 4), dim3(256), 0, c->stream, w->pk_count, nv, k4, w->PK,
+                               w->phash, w->tprev);
+        } else {                                             // a rebuild: sort every vertex by hash
+            if ((size_t)nv > w->tw_cap) {
+                hipFree(w->tw_hs); hipFree(w->tw_vin); hipFree(w->tw_vout);
+                w->tw_hs = nullptr; w->tw_vin = w->tw_vout = nullptr;
+                if ((rc = realloc_dev(&w->tw_hs, nv)) || (rc = realloc_dev(&w->tw_vin, nv)) || (rc = realloc_dev(&w->tw_vout, nv))) return rc;
+                w->tw_cap = nv;
+            }
+            size_t need = 0;
+            HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, need, w->phash, w->tw_hs, w->tw_vin, w->tw_vout, nv, 0, 64, c->stream));
+            if (need > w->tw_tmp_bytes) {
+                hipFree(w->tw_tmp);
+                w->tw_tmp = nullptr;
+                HIPCHK(hipMalloc(&w->tw_tmp, need));
+                w->tw_tmp_bytes = need;
+            }
+            hipLaunchKernelGGL(cut_iota_kernel, dim3((nv + 255) / 256), dim3(256), 0, c->stream, w->tw_vin, nv);
+            // (the earlier vertices' hashes are kept in phash; only the new ones were hashed above)
+            HIPCHK(hipcub::DeviceRadixSort::SortPairs(w->tw_tmp, need, w->phash, w->tw_hs, w->tw_vin, w->tw_vout, nv, 0, 64,
+                                                      c->stream));
+            hipLaunchKernelGGL(cut_twin_sorted_kernel, dim3((nv + 255) / 256), dim3(256), 0, c->stream, nv, k4, w->PK, w->tw_hs,
+                               w->tw_vout, w->tprev);
+        }
         HIPCHK(hipGetLastError());
         w->pk_count = nv;
     }

@@ -218,6 +218,7 @@ int dvs_init(twosd_ctx *c) {
     dvs_free(c);
     c->dvs.m = c->L.m;
     c->dvs.size = 0;
+    cut_truncate_pk(c, 0);
     return TWOSD_OK;
 }
 
@@ -417,7 +418,7 @@ extern "C" int twosd_dvs_truncate(twosd_ctx *c, int size) {
     HIPCHK(hipSetDevice(c->device));
     DvsDevice &D = c->dvs;
     D.size = size;
-    cut_invalidate_pk(c);
+    cut_truncate_pk(c, size);   // the cut's PK rows below size stay valid (V[0, size) is unchanged)
     if (D.table) {
         hipLaunchKernelGGL(dvs_fill_kernel, dim3((D.tcap + 255) / 256), dim3(256), 0, c->stream, D.table, D.tcap, -1);
         if (size)

@@ -235,4 +235,5 @@ int dvs_push_device(twosd_ctx *c, int count, const double *d_pis, int *d_out_ind
 // cut (cut_kernel.hip)
 void cut_free(twosd_ctx *c);
 void cut_invalidate_pk(twosd_ctx *c);
+void cut_truncate_pk(twosd_ctx *c, int size);   // V truncated to size: PK rows past it are stale
 }  // namespace twosd
