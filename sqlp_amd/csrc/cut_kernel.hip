@@ -90,6 +90,7 @@ struct CutParams {
     // vertex ranges each, and such a unit leaves its per-scenario (M, I, log counts) in tp_* at
     // [(s - 128 full_units) tail_S + range] for cut_tail_merge_kernel
     int full_units, tail_S;
+    int fx_gs;             // cut_fixup_kernel: whole-tile scenarios per wave step (64; 32 / 16 for small batches)
     double *tp_m;
     int *tp_i, *tp_f;
 };
@@ -804,9 +805,10 @@ __global__ void __launch_bounds__(256, 3) cut_fixup_kernel(CutParams P, int slot
     // so that the waves holding the last scenarios do not run one serial batch per tail row
     for (int pass = 0; pass < 2; ++pass) {
     const int hi = pass ? P.N : min(t0, P.N), lstride = pass ? nw : 1;
-    for (int sb0 = pass ? t0 + gw : gw * 64; sb0 < hi; sb0 += nw * 64) {
+    const int gs = pass ? 64 : P.fx_gs;     // a small batch: fewer scenarios per wave step, more waves
+    for (int sb0 = pass ? t0 + gw : gw * gs; sb0 < hi; sb0 += nw * gs) {
     const int sl = sb0 + lane * lstride;
-    const int myflag = sl < hi ? P.flag[sl] : 0;
+    const int myflag = (lane < gs && sl < hi) ? P.flag[sl] : 0;
     uint64_t todo = __ballot(myflag != 0);
     while (todo) {
         // ---- the batch: up to kFxR whole-tile rows, or one tail row
@@ -1405,7 +1407,12 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     const int nblocks = std::max(1, std::min(nunits, B));
     // the fixup takes 64 scenarios per wave step: enough waves that every SIMD holds several
     static const int fix_per_cu = getenv("TWOSD_FIX_BPC") ? std::max(1, atoi(getenv("TWOSD_FIX_BPC"))) : 4;
-    const int fix_blocks = std::max(1, std::min((N + 255) / 256, fix_per_cu * c->num_cus));
+    // scenarios per wave step: 64, or 32 / 16 when 64 would leave fewer waves than 3 resident blocks
+    // per CU hold (a 125k shard at N = 8: 1953 waves of one step each, every flagged row's batch
+    // latency in series)
+    int fx_gs = 64;
+    while (fx_gs > 16 && (long long)(N + fx_gs - 1) / fx_gs < 12ll * c->num_cus) fx_gs /= 2;
+    const int fix_blocks = std::max(1, std::min((N + 4 * fx_gs - 1) / (4 * fx_gs), fix_per_cu * c->num_cus));
     const int ntail = S > 1 ? N - full * kCutTile2 : 0;
     const int merge_blocks = ntail > 0 ? std::max(1, std::min((ntail + 3) / 4, c->num_cus)) : 0;
     const int resc_blocks = std::max(1, std::min((N + 255) / 256, c->num_cus));
@@ -1509,7 +1516,7 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
         P.basec = w->basec;
     }
     P.arg = w->arg; P.val = w->val; P.flag = w->flag; P.hist = d_hist; P.partial = w->partial;
-    P.full_units = full; P.tail_S = S;
+    P.full_units = full; P.tail_S = S; P.fx_gs = fx_gs;
     P.tp_m = w->tp_m; P.tp_i = w->tp_i; P.tp_f = w->tp_f;
     launch_argmax(KB, P, nblocks, c->stream);
     if (P.hist_lds)
