@@ -109,6 +109,9 @@ def main():
                          "candidate lists, inside the timed step); 0: keep the x_EV pool for every x")
     ap.add_argument("--refresh-train", type=int, default=0,
                     help="training scenarios of a pool refresh (0: 4 x the refresh pool)")
+    ap.add_argument("--refresh-cand-train", type=int, default=0,
+                    help="training scenarios whose flat picks build the two-level candidate lists after a refresh "
+                         "(0: all --refresh-train of them)")
     ap.add_argument("--refresh-pool", type=int, default=0,
                     help="pool size after a refresh (0: 4096 per 1M scenarios of the refreshing ranks, at least 512)")
     ap.add_argument("--refresh-dist", type=int, default=1,
@@ -294,7 +297,8 @@ def main():
             ctx.pool_refresh(rtr, xx, 0, args.refresh_train, args.refresh_pool)
         t1 = time.perf_counter()
         if args.pool_level1 > 0 and ctx.pool_size() > args.pool_level1:
-            ctx.pool_build_candidates(rtr, xx, 0, args.refresh_train, args.pool_level1, args.pool_cands)
+            nct = args.refresh_train if args.refresh_cand_train <= 0 else min(args.refresh_cand_train, args.refresh_train)
+            ctx.pool_build_candidates(rtr, xx, 0, nct, args.pool_level1, args.pool_cands)
         pool_at["x"] = xx.copy()
         # ms: training solves (with eta files), basis keys + selection, pool build (device:
         # B^-1 FTRAN + pool arrays; host path: composition), host upload (host path only),
