@@ -111,7 +111,7 @@ def main():
                     help="training scenarios of a pool refresh (0: 4 x the refresh pool)")
     ap.add_argument("--refresh-cand-train", type=int, default=0,
                     help="training scenarios whose flat picks build the two-level candidate lists after a refresh "
-                         "(0: all --refresh-train of them)")
+                         "(0: the --refresh-train ones; more extends the same stream)")
     ap.add_argument("--refresh-pool", type=int, default=0,
                     help="pool size after a refresh (0: 4096 per 1M scenarios of the refreshing ranks, at least 512)")
     ap.add_argument("--refresh-dist", type=int, default=1,
@@ -273,6 +273,10 @@ def main():
     # the distributed refresh its contiguous slice)
     rtr = None
     t_lo, t_hi = sdist.shard_range(args.refresh_train, rank, world) if dist_refresh else (0, args.refresh_train)
+    # the candidate lists may take more training scenarios than the pool (single-rank refresh): the
+    # same stream, extended
+    if not dist_refresh and args.refresh_cand_train > args.refresh_train:
+        t_hi = args.refresh_cand_train
     if args.refresh:
         rtr = twosd.sdEpigraph(ctx, 1.0, 0.0)
         scenarios(rtr, t_lo, t_hi, args.seed + 4)
@@ -297,7 +301,7 @@ def main():
             ctx.pool_refresh(rtr, xx, 0, args.refresh_train, args.refresh_pool)
         t1 = time.perf_counter()
         if args.pool_level1 > 0 and ctx.pool_size() > args.pool_level1:
-            nct = args.refresh_train if args.refresh_cand_train <= 0 else min(args.refresh_cand_train, args.refresh_train)
+            nct = args.refresh_train if args.refresh_cand_train <= 0 else args.refresh_cand_train
             ctx.pool_build_candidates(rtr, xx, 0, nct, args.pool_level1, args.pool_cands)
         pool_at["x"] = xx.copy()
         # ms: training solves (with eta files), basis keys + selection, pool build (device:
