@@ -41,7 +41,7 @@ def main():
         ctx.invalidate_x()
         cut = twosd.build_sasa_cut(epi, x, V, tie)
         ts.append(ctx.timings_us()[2] / 1e3)
-    stats = ctx.cut_stats()   # (re-decided scenarios, candidates, full re-scans) of the last cut
+    stats = ctx.cut_stats()   # (re-decided scenarios, candidates, full re-scans, twins left out) of the last cut
     k = len(ctx.rows)
     flops = 2 * N * len(V) * k + 2 * len(V) * sp2.shape[0]
     t = min(ts)
