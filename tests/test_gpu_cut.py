@@ -317,3 +317,35 @@ def test_cut_after_truncate_and_different_pushes():
         assert (ma == oma).all(), (tie_rel, int((ma != oma).sum()))
         assert cut.alpha == pytest.approx(a, rel=1e-8, abs=1e-8)
         np.testing.assert_allclose(cut.beta, b, rtol=1e-8, atol=1e-8 * (1 + np.abs(b).max()))
+
+
+def test_cut_storm_twins_with_vertex_split_tail():
+    """storm at x_EV with its twin-rich V (the duals of 16,384 scenarios solved there) over 100,000
+    scenarios: 782 tiles on the persistent grid leave a vertex-split tail, so tail rows are merged
+    across ranges and re-decided from the range logs, with the dominated twins left out of the MFMA
+    pass.  max_arg equal to the C oracle for EVERY scenario, alpha / beta to 1e-8."""
+    from oracle import cpu
+    from sqlp_amd import smps, twosd
+    inst = I.load("storm")
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    x = I.x_ev("storm")
+    ctx.compute_basis(x, smps.mean_values(inst["sto"]))
+    src = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(src, I.sample("storm", 16384, 41))
+    _, st, _ = twosd.solve_push(src, x, 0, 16384)
+    assert (st == 0).all()
+    V = twosd.sdDualVertexSet(ctx)
+    N = 100_000
+    vals = I.sample("storm", N, 67)
+    epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(epi, vals)
+    sp = inst["osp2"]
+    Vm = V.matrix()
+    cut, mv, ma = twosd._build_cut(epi, x, 0.0, want_argmax=True)
+    assert ctx.cut_stats()[3] > 0                                  # twins left out
+    a, b, omv, oma = cpu.build_cut(sp.r, sp.T, x, Vm, ctx.rows, vals - sp.r[ctx.rows], np.ones(N), tie_rel=0.0,
+                                   nthreads=8)
+    assert (ma == oma).all(), int((ma != oma).sum())
+    np.testing.assert_allclose(mv, omv, rtol=1e-12, atol=1e-9)
+    assert cut.alpha == pytest.approx(a, rel=1e-8, abs=1e-8)
+    np.testing.assert_allclose(cut.beta, b, rtol=1e-8, atol=1e-8 * (1 + np.abs(b).max()))
