@@ -76,8 +76,8 @@ struct CutParams {
     const double *basec;   // base of the argmax's vertices, per x
     const double *base;    // nv: pi_v . bvec in index order (the restatement's base dot)
     const int *eord;       // k: elements by ascending row (the restated score's order)
-    const unsigned long long *band_bits;   // max_v (|base[v]| + sum_e |PK[v,e] coef_e| dmax_e), as bits
-    double band_scale;     // band = band_scale * that maximum (4 gamma_{k+4}: twice the 2 gamma bound)
+    const unsigned long long *band_bits;   // the band: band_scale x max_v (|base[v]| + sum_e |PK[v,e] coef_e| dmax_e), as bits
+    double band_scale;     // 4 gamma_{k+4}: twice the 2 gamma bound
     int *arg; double *val; int *flag;   // N; flag != 0: re-decide (main rows: 4-bit log counts per lane group)
     int *cand;             // candidate logs of the whole tiles: [(s * 4 + g) * kCandC + i]
     unsigned long long *fstats;   // fixup counters: re-decided scenarios, candidates scored, full re-scans
@@ -257,7 +257,8 @@ constexpr int kVbSlice = 512;
 __global__ void __launch_bounds__(256) cut_vbase_kernel(int nv, int m, int k, int k4, const double *__restrict__ V,
                                                         const double *__restrict__ bvec, const double *__restrict__ PK,
                                                         const double *__restrict__ coef, const unsigned long long *__restrict__ dmax,
-                                                        double *__restrict__ base, unsigned long long *__restrict__ band_bits) {
+                                                        double *__restrict__ base, unsigned long long *__restrict__ band_bits,
+                                                        double band_scale) {
 #pragma clang fp contract(off)
     __shared__ double prod[4][kVbSlice];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -286,7 +287,8 @@ __global__ void __launch_bounds__(256) cut_vbase_kernel(int nv, int m, int k, in
         if (lane == 0) {
             base[v] = s;
             const double t = fabs(s) + a;
-            atomicMax(band_bits, (unsigned long long)__double_as_longlong(isfinite(t) ? t : INFINITY));
+            // the band itself (a positive scale keeps the order of the maxima, rounding included)
+            atomicMax(band_bits, (unsigned long long)__double_as_longlong(isfinite(t) ? band_scale * t : INFINITY));
         }
     }
 }
@@ -300,6 +302,13 @@ __global__ void __launch_bounds__(256) cut_dmax_kernel(int from, int to, int k, 
     double mx = 0.0;
     for (int s = from + blockIdx.x; s < to; s += gridDim.x) mx = fmax(mx, fabs(dv[(size_t)s * k + e]));   // NaN ignored: its scores never win
     atomicMax(&dmax[e], (unsigned long long)__double_as_longlong(mx));
+}
+
+// the decision band of this cut (written by cut_vbase_kernel) through the scalar cache: a
+// wave-uniform value held in SGPRs rather than a VGPR pair (the 3-blocks-per-CU argmax would
+// spill it)
+__device__ __forceinline__ double cut_band_scalar(const CutParams &P) {
+    return __longlong_as_double((long long)((const __attribute__((address_space(4))) unsigned long long *)P.band_bits)[0]);
 }
 
 // floor of the decision band around a running maximum M: a vertex below it cannot be the
@@ -319,6 +328,9 @@ struct RowEx { double M, thr; int I, n, f; };
 template <bool HOLD>
 __device__ __forceinline__ void row_log(RowEx &b, double s, int v, double rel, double band, int *lbase, unsigned lo) {
     if (s == -INFINITY) return;                  // padding vertices (-inf base row) never enter
+    // the 3-blocks build: an opaque copy, so the entry addresses are formed here, on this rare path,
+    // instead of being hoisted out of the chunk loop as 64-bit values that would spill
+    if (!HOLD) asm volatile("" : "+v"(lo));
     const double tn = band_floor(s, rel, band);
     if (tn > b.M) {                              // every earlier entry is below the band for good
         if (HOLD) b.f = v;
@@ -400,7 +412,7 @@ __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_
     const int ntiles = (P.N + kCutTile2 - 1) / kCutTile2;
     const int nchunks = (*P.nvc + kVT2 - 1) / kVT2;   // the argmax's vertices (vmap)
     const int nunits = P.full_units + (ntiles - P.full_units) * P.tail_S;
-    const double band = P.band_scale * __longlong_as_double((long long)*P.band_bits);
+    const double band = kHold ? __longlong_as_double((long long)*P.band_bits) : cut_band_scalar(P);
     const double rel = P.tie_rel;
     double pv_sum = 0.0;
     double Sacc[2] = {0.0, 0.0};   // lane (g, j): e = 4 kb + g for kb = j, j + 16
@@ -605,7 +617,7 @@ __global__ void __launch_bounds__(256) cut_tail_merge_kernel(CutParams P, int sl
     const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int nw = (gridDim.x * blockDim.x) >> 6;
     const int t0 = P.full_units * kCutTile2, S = P.tail_S;
-    const double band = P.band_scale * __longlong_as_double((long long)*P.band_bits);
+    const double band = __longlong_as_double((long long)*P.band_bits);
     double pv_sum = 0.0, Sacc[2] = {0.0, 0.0};
     for (int ts = gw; ts < P.N - t0; ts += nw) {
         const int s = t0 + ts;
@@ -783,7 +795,7 @@ __global__ void __launch_bounds__(256, 3) cut_fixup_kernel(CutParams P, int slot
     const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int nw = (gridDim.x * blockDim.x) >> 6;
     const int t0 = P.full_units * kCutTile2, S = P.tail_S;
-    const double band = P.band_scale * __longlong_as_double((long long)*P.band_bits);
+    const double band = cut_band_scalar(P);
     // this lane's elements in the restated order: q = lane, lane + 64 (-1: padding)
     const int e0 = lane < P.k ? P.eord[lane] : -1, e1 = lane + 64 < P.k ? P.eord[lane + 64] : -1;
     if (threadIdx.x < kFxLd) {
@@ -1461,9 +1473,18 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     }
     HIPCHK(hipMemsetAsync(d_hist, 0, sizeof(unsigned long long) * std::max(nv, 1), c->stream));
     HIPCHK(hipMemsetAsync(w->band_bits, 0, sizeof(unsigned long long), c->stream));
+    // band: the MFMA score and the restated one both add base[v] to a (k + 1)-term dot and differ
+    // by at most 2 gamma_{k+4} (|base[v]| + sum_e |PK coef dv|) (one more rounding per T element
+    // term, coef folded on the other side); twice that for safety
+    double band_scale;
+    {
+        const double u = ldexp(1.0, -53), nk = (double)(k + 4);
+        band_scale = 2.0 * 2.0 * (nk * u / (1.0 - nk * u));
+    }
     hipLaunchKernelGGL(cut_vbase_kernel, dim3(std::max(1, std::min((nv + 3) / 4, 4096))), dim3(256), 0, c->stream, nv, m, k, k4,
-                       c->dvs.V, w->bvec, w->PK, w->coef, w->dmax[epi], w->base, w->band_bits);
+                       c->dvs.V, w->bvec, w->PK, w->coef, w->dmax[epi], w->base, w->band_bits, band_scale);
     CutParams P{};
+    P.band_scale = band_scale;
     P.N = N; P.k = k; P.k4 = k4; P.nv = nv; P.vcap = w->pk_vcap; P.m = m;
     static const int hist_lds_max = getenv("TWOSD_HIST_LDS") ? atoi(getenv("TWOSD_HIST_LDS")) : kHistLds;
     P.hist_lds = nv <= hist_lds_max ? 1 : 0;
@@ -1473,13 +1494,6 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     }
     P.hist_part = w->hist_part;
     P.tie_rel = tie_rel; P.inv_total = 1.0 / total_weight;
-    // band: the MFMA score and the restated one both add base[v] to a (k + 1)-term dot and differ
-    // by at most 2 gamma_{k+4} (|base[v]| + sum_e |PK coef dv|) (one more rounding per T element
-    // term, coef folded on the other side); twice that for safety
-    {
-        const double u = ldexp(1.0, -53), nk = (double)(k + 4);
-        P.band_scale = 2.0 * 2.0 * (nk * u / (1.0 - nk * u));
-    }
     P.band_bits = w->band_bits;
     P.cand = w->cand; P.tcand = w->tcand; P.eord = w->eord; P.fstats = w->fstats;
     P.dv = E.d_dv; P.w = E.d_w; P.coef = w->coef; P.PK = w->PK; P.PKT = w->PKT; P.PKO = w->PKO; P.base = w->base;
