@@ -260,6 +260,10 @@ def main():
     # B^-1 composition, upload grow with the pool), so a smaller shard takes a smaller pool
     # a distributed refresh builds one pool for all ranks, so it is sized by the whole batch
     dist_refresh = world > 1 and args.refresh_dist == 1
+    if dist_refresh and args.refresh_cand_train > 0:
+        # the distributed refresh builds the candidate lists from each rank's slice of the
+        # refresh-training scenarios (sqlp_amd.dist.refresh_sharded): the knob would be ignored
+        raise SystemExit("--refresh-cand-train applies to the single-rank refresh only (use --refresh-dist 0)")
     # pool size by the shard: 4096 per 1M scenarios on one rank, at least 512; the distributed
     # refresh builds four times that (at least 1024): its training and composition are split over
     # the ranks (profiles/r04/n8/shard_emulate_pool*.txt: at N = 8 with the bench warmup, pools of
@@ -523,8 +527,8 @@ def main():
 
     # HBM traffic and MFMA counters of the dominant kernels from the committed rocprofv3 PMC
     # summary of this exact workload (separate --pmc passes, tools/profile_round.sh), per launch
-    pmc = latest_pmc_summary()
-    if pmc and world == 1 and pmc.get("scenarios") == N:
+    pmc = latest_pmc_summary(name, N, nv, E, world)
+    if pmc:
         kl = pmc["kernels"].get("lp_hyper_kernel")
         if kl:
             out["roofline"]["traffic"] = kl["hbm_bytes_per_launch"]
@@ -646,16 +650,30 @@ def spot_check(sp2, ctx, epi, V, xs, x_iters, positions, args):
     return res
 
 
-def latest_pmc_summary():
+def pmc_key(d):
+    """The workload a PMC summary was measured on: its "key" (instance, scenarios, vertices,
+    epigraphs, n_gpus), or for a summary written before keys existed (profiles/r05) the storm
+    bench default it was taken from (|V| = 4096, one epigraph, one GPU)."""
+    k = d.get("key")
+    if k:
+        return (k["instance"], int(k["scenarios"]), int(k["vertices"]), int(k["epigraphs"]), int(k["n_gpus"]))
+    return (d.get("workload", "").split(" ")[0], int(d.get("scenarios", 0)), 4096, 1, 1)
+
+
+def latest_pmc_summary(instance, scenarios, vertices, epigraphs, n_gpus):
+    """The newest committed PMC summary (profiles/r*/pmc_summary*.json) of exactly this workload
+    -- instance, scenario count, |V|, epigraphs and GPU count -- or None: a line whose workload
+    has no profile of its own reports traffic null instead of another workload's counters."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")))
-    if not files:
-        return None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    d["file"] = os.path.relpath(files[-1], ROOT)
-    d.setdefault("scenarios", 1_000_000)
-    return d
+    want = (instance, int(scenarios), int(vertices), int(epigraphs), int(n_gpus))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary*.json")))
+    for fn in reversed(files):
+        with open(fn) as f:
+            d = json.load(f)
+        if pmc_key(d) == want:
+            d["file"] = os.path.relpath(fn, ROOT)
+            return d
+    return None
 
 
 def cpu_baseline(sp2, ctx, xs, x_iters, heads_at, vals, Vmat, args):

@@ -434,7 +434,9 @@ int oracle_lp_solve_batch(void *p, int N, int k, const int *rows, const double *
  *   scenario s: dr = DR[s,:] on rows[]; weights w[s].
  * Scores are computed as the reference does: dot(pi, r - T x) + dot(pi, dvec)
  * (subprob.jl:147-155), each dot sequential in row order with every product and sum rounded
- * on its own (built with -ffp-contract=off): base[i] = r[i] - T[i][0] x[0] - ...;
+ * on its own (built with -ffp-contract=off): base[i] = r[i] - tx[i] with tx[i] = T[i][0] x[0] + T[i][1] x[1] + ...
+ * accumulated from zero in column order (`coef.rhs - coef.transfer * x`, subprob.jl:147: SparseArrays'
+ * CSC mat-vec adds column by column; a zero entry adds an exact 0);
  * vb[v] = sum_i pi[i] base[i]; t = sum over the random rows in ascending order of
  * pi[row] dvec[row] (the zero rows of the dense dvec add exactly nothing).  This is the
  * arithmetic every tie decision of the build is pinned to (the GPU re-decides rows with
@@ -447,7 +449,7 @@ void oracle_build_cut(int m, int n1, int nv, int N, int k, const int *rows, cons
                       const double *x, const double *V, const double *DR, const double *w, double tie_rel,
                       double *alpha, double *beta, double *max_val, int *max_arg, int nthreads) {
     double *base = (double *)malloc(sizeof(double) * m);
-    for (int i = 0; i < m; ++i) { double s = r[i]; for (int j = 0; j < n1; ++j) s -= T[(size_t)i * n1 + j] * x[j]; base[i] = s; }
+    for (int i = 0; i < m; ++i) { double tx = 0.0; for (int j = 0; j < n1; ++j) tx += T[(size_t)i * n1 + j] * x[j]; base[i] = r[i] - tx; }
     double *vb = (double *)malloc(sizeof(double) * (nv ? nv : 1));
     for (int v = 0; v < nv; ++v) { double s = 0; for (int i = 0; i < m; ++i) s += V[(size_t)v * m + i] * base[i]; vb[v] = s; }
     /* elements by ascending row (element order within a row): insertion sort, k is small */

@@ -52,6 +52,28 @@ def round16_array(v) -> np.ndarray:
     return np.array([round16(t) for t in np.asarray(v, dtype=np.float64)], dtype=np.float64)
 
 
+def round16_vec(a) -> np.ndarray:
+    """round16 elementwise, vectorised (the same values as round16 on every element): the scale
+    by 2**digits is exact, np.round rounds half to even like Python's round, and the cases where
+    round16 returns x itself -- 0, non-finite, a scale 2**digits that overflows (digits > 1023),
+    a non-finite result -- keep x."""
+    x = np.asarray(a, dtype=np.float64)
+    out = x.copy()
+    fin = np.isfinite(x) & (x != 0.0)
+    _, e2 = np.frexp(np.where(fin, x, 1.0))
+    digits = SIGNIFICANT_DIGITS - e2
+    pos = fin & (digits >= 0) & (digits <= 1023)
+    neg = fin & (digits < 0)
+    with np.errstate(over="ignore", invalid="ignore"):
+        rp = np.round(np.ldexp(np.where(pos, x, 0.0), np.where(pos, digits, 0))) / np.ldexp(1.0, np.where(pos, digits, 0))
+        isc = np.ldexp(1.0, np.where(neg, -digits, 0))
+        rn = np.round(np.where(neg, x, 0.0) / isc) * isc
+    r = np.where(pos, rp, np.where(neg, rn, x))
+    ok = (pos | neg) & np.isfinite(r)
+    out[ok] = r[ok]
+    return out
+
+
 def hash_dual_vector(vec) -> int:
     s = 0.0
     for v in np.asarray(vec, dtype=np.float64):   # sequential sum, dual_set.jl:47-50
@@ -88,6 +110,39 @@ class DualVertexSet:
         self.hashes.append(h)
         self.data.append(vec)
         return len(self.data) - 1
+
+    def push_batch(self, pis) -> np.ndarray:
+        """push! of every row of pis in order (dual_set.jl:84-94), vectorised for large batches:
+        the same hashes (sequential L1 sum, round16) and the same equality test (equal hash, then
+        every component equal after round16), with the linear scan restricted to the vertices of
+        equal hash -- dual_isequal is false for any other, so the first match in insertion order
+        is the same.  Returns the vertex index of every row."""
+        P = np.atleast_2d(np.asarray(pis, dtype=np.float64))
+        if not hasattr(self, "_by_hash"):
+            self._by_hash = {}
+            self._r16 = []
+            for i, (h, d) in enumerate(zip(self.hashes, self.data)):
+                self._by_hash.setdefault(h, []).append(i)
+                self._r16.append(round16_vec(d))
+        sums = np.cumsum(np.abs(P), axis=1)[:, -1] if P.shape[1] else np.zeros(P.shape[0])
+        hb = round16_vec(sums).view(np.uint64)
+        R = round16_vec(P)
+        out = np.empty(P.shape[0], dtype=np.int64)
+        for s in range(P.shape[0]):
+            h = int(hb[s])
+            hit = -1
+            for i in self._by_hash.get(h, ()):
+                if len(self.data[i]) == P.shape[1] and np.array_equal(self._r16[i], R[s]):
+                    hit = i
+                    break
+            if hit < 0:
+                hit = len(self.data)
+                self.hashes.append(h)
+                self.data.append(P[s].copy())
+                self._r16.append(R[s])
+                self._by_hash.setdefault(h, []).append(hit)
+            out[s] = hit
+        return out
 
     def __len__(self):
         return len(self.data)
@@ -137,13 +192,15 @@ def tie_tolerance(M: float, rel: float) -> float:
 
 
 def _seq_base(coef: Coefficients, x):
-    """r - T x as oracle_build_cut forms it: r[i], then minus T[i, j] x[j] for j = 0, 1, ...,
-    each product and difference rounded on its own."""
+    """r - (T x) as the reference writes it (`coef.rhs - coef.transfer * x`, subprob.jl:147):
+    T x accumulated from zero column by column (SparseArrays' CSC mat-vec, tx[i] += T[i, j] x[j]
+    for j ascending; a structural zero adds an exact 0), then subtracted from r; each product
+    and sum rounded on its own (oracle_build_cut's arithmetic)."""
     prod = coef.transfer * x[None, :]
-    base = np.array(coef.rhs, dtype=np.float64)
+    tx = np.zeros(prod.shape[0])
     for j in range(prod.shape[1]):
-        base = base - prod[:, j]
-    return base
+        tx = tx + prod[:, j]
+    return np.array(coef.rhs, dtype=np.float64) - tx
 
 
 def _seq_rowdot(A, b):
@@ -154,16 +211,34 @@ def _seq_rowdot(A, b):
     return np.cumsum(A * b[None, :], axis=1)[:, -1]
 
 
+def _element_terms(dr, dT, x):
+    """(row, coef_e * dv_e) of every nonzero random element of a scenario, by ascending row (RHS
+    element first, then T columns ascending): the terms restated_score adds one at a time."""
+    rows, fac = [], []
+    dT = np.asarray(dT)
+    for i in np.flatnonzero((np.asarray(dr) != 0) | (dT != 0).any(axis=1)):
+        if dr[i] != 0:
+            rows.append(i)
+            fac.append(float(dr[i]))
+        for j in np.flatnonzero(dT[i]):
+            rows.append(i)
+            fac.append(float(-x[j]) * float(dT[i, j]))
+    return np.array(rows, dtype=np.int64), np.array(fac, dtype=np.float64)
+
+
 def argmax_procedure(coef: Coefficients, deltas, x, V, tie_rel: float = 0.0):
     """subprob.jl:141-169 (MIN_SENSE).  tie_rel == 0 is the reference rule exactly (strict
     '>' so the first maximum in insertion order wins).  tie_rel > 0 is the build's
     documented near-tie rule: the lowest vertex index whose score is within
     tie_rel*(1+|max|) of the maximum.
-    Scores s = dot(pi, r - T x) + dot(pi, dvec) (:147-155) with both dots sequential in row order
-    and no contraction -- oracle_build_cut's arithmetic, which the GPU's decisions are pinned to
-    (dvec's zero rows are dropped: adding an exact 0 changes nothing).  The reference's OpenBLAS
-    ddot adds in a CPU-dependent blocked order, so at rounding-level ties its pick is not
-    reproducible by any restatement."""
+    Scores s = dot(pi, r - T x) + dot(pi, dvec) (:147-155) with both dots sequential and no
+    contraction -- oracle_build_cut's arithmetic, which the GPU's decisions are pinned to: the
+    base dot in row order, the delta dot over the random elements by ascending row, one term
+    pi[row] * (coef_e * dv_e) per element (coef_e = 1 for an RHS element, -x[col] for a T
+    element; within a row the RHS element first, then T columns ascending).  With one random
+    element per row this is the dense dot(pi, dvec) with its zero rows dropped (adding an exact
+    0 changes nothing).  The reference's OpenBLAS ddot adds in a CPU-dependent blocked order, so
+    at rounding-level ties its pick is not reproducible by any restatement."""
     x = np.asarray(x, dtype=np.float64)
     base = _seq_base(coef, x)
     Vl = list(V)
@@ -171,9 +246,8 @@ def argmax_procedure(coef: Coefficients, deltas, x, V, tie_rel: float = 0.0):
     Vm = np.array(Vl, dtype=np.float64).reshape(len(Vl), -1)
     vb = _seq_rowdot(Vm, base)
     for dr, dT in deltas:
-        dvec = dr - dT @ x
-        nz = np.flatnonzero(dvec)
-        t = _seq_rowdot(Vm[:, nz], dvec[nz]) if len(nz) else np.zeros(len(Vl))
+        rows, fac = _element_terms(dr, dT, x)
+        t = _seq_rowdot(Vm[:, rows], fac) if len(rows) else np.zeros(len(Vl))
         scores = [float(s) for s in (vb + t)]
         if tie_rel == 0.0:
             best, arg = -math.inf, -1

@@ -46,6 +46,9 @@ int twosd::fail(int code, const char *fmt, ...) {
 int twosd::poison_byte(int family) {
     static const int b = getenv("TWOSD_POISON") ? atoi(getenv("TWOSD_POISON")) : -1;
     static const int fam = getenv("TWOSD_POISON_FAMILY") ? atoi(getenv("TWOSD_POISON_FAMILY")) : -1;
+    static const bool said = b >= 0 && fprintf(stderr, "TWOSD_POISON: new device allocations filled with 0x%02x (families %d)\n",
+                                               b & 0xff, fam) > 0;
+    (void)said;
     return (fam & family) ? b : -1;
 }
 template <typename T>

@@ -1187,6 +1187,7 @@ static CutWs *cws(twosd_ctx *c) {
     return (CutWs *)c->cut_ws;
 }
 
+
 void cut_free(twosd_ctx *c) {
     if (!c->cut_ws) return;
     CutWs *w = (CutWs *)c->cut_ws;
@@ -1220,6 +1221,17 @@ void cut_invalidate_pk(twosd_ctx *c) {
         hipError_t _e = (expr);                                                                    \
         if (_e != hipSuccess) return fail(TWOSD_E_DEVICE, "%s: %s", #expr, hipGetErrorString(_e)); \
     } while (0)
+
+// a cut that returns before the argmax (no scenarios) leaves no fixup counters: clear the last
+// cut's, so twosd_cut_stats does not report them as this cut's
+static int clear_cut_stats(twosd_ctx *c) {
+    CutWs *w = c->cut_ws ? (CutWs *)c->cut_ws : nullptr;
+    if (w && w->fstats) {
+        HIPCHK(hipMemsetAsync(w->fstats, 0, sizeof(unsigned long long) * 16, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    return TWOSD_OK;
+}
 
 template <typename T>
 static int realloc_dev(T **p, size_t n) {
@@ -1366,16 +1378,18 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     if (KB < 0) return fail(TWOSD_E_UNSUPPORTED, "k = %d random elements exceeds the cut kernel envelope (127)", k);
     int rc;
     if ((rc = update_pk(c))) return rc;
-    // host: bvec = r - T x as the restatement forms it (oracle_build_cut: r[i], then minus each
-    // T[i][j] x[j] in column order, no contraction), coef
+    // host: bvec = r - (T x) as the reference writes it (`coef.rhs - coef.transfer * x`,
+    // subprob.jl:147): T x accumulated from zero column by column, as SparseArrays' CSC mat-vec
+    // does (tx[i] += T[i][j] * x[j] for j ascending, no contraction), then subtracted from r
+    // (oracle_build_cut, twosd_ref._seq_base); coef
     std::vector<double> &bvec = w->h_bvec, &coef = w->h_coef;
     bvec.assign(m, 0.0);
     coef.assign(k4, 0.0);
     for (int i = 0; i < m; ++i) {
 #pragma clang fp contract(off)
-        double s = c->r[i];
-        for (int jj = 0; jj < n1; ++jj) s = s - c->T[(size_t)i * n1 + jj] * x[jj];
-        bvec[i] = s;
+        double tx = 0.0;
+        for (int jj = 0; jj < n1; ++jj) tx = tx + c->T[(size_t)i * n1 + jj] * x[jj];
+        bvec[i] = c->r[i] - tx;
     }
     for (int e = 0; e < k; ++e) coef[e] = c->pos_col[e] < 0 ? 1.0 : -x[c->pos_col[e]];
     if (!w->coef || !w->bvec || !w->g || w->vec_m != m) {
@@ -1438,6 +1452,15 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     // candidate logs: rows padded to whole tiles (the padding scenarios of a tile log too)
     const size_t cand_need = (size_t)full * kCutTile2 * 4 * kCandC;
     const size_t tcand_need = (size_t)(ntiles - full) * kCutTile2 * S * 4 * kCandC;
+    // the argmax forms log offsets as 32-bit indices (log0 / lstep): past 2^32 slots (~67M
+    // scenarios in one epigraph) they would wrap and the fixup would read slots no kernel wrote
+    {
+        size_t log_max = UINT32_MAX;
+        if (const char *e = getenv("TWOSD_CUT_LOG_MAX")) log_max = (size_t)atoll(e);   // test hook
+        if (cand_need > log_max || tcand_need > log_max)
+            return fail(TWOSD_E_UNSUPPORTED, "cut: %d scenarios need %zu candidate-log slots (32-bit offsets: at most %zu)", N,
+                        std::max(cand_need, tcand_need), log_max);
+    }
     if (cand_need > w->cand_cap) {
         if ((rc = realloc_dev(&w->cand, cand_need))) return rc;
         w->cand_cap = cand_need;
@@ -1455,7 +1478,12 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
         w->dmax_rows.resize(epi + 1, 0);
         w->dmax_k.resize(epi + 1, -1);
     }
-    if (w->dmax_k[epi] != k) {
+    // Invariant: an epigraph's scenario rows are append-only (twosd_add_scenarios /
+    // twosd_add_sampled_scenarios append; no entry point rewrites or removes rows), so the
+    // cached max folds in only rows [dmax_rows, N).  A row count below the cached one can only
+    // mean the rows were replaced: fold everything in again (a too-small dmax would narrow the
+    // decision band and mark near-tied rows decided without a fixup).
+    if (w->dmax_k[epi] != k || w->dmax_rows[epi] > N) {
         if ((rc = realloc_dev(&w->dmax[epi], std::max(k, 1)))) return rc;
         HIPCHK(hipMemsetAsync(w->dmax[epi], 0, sizeof(unsigned long long) * std::max(k, 1), c->stream));
         w->dmax_k[epi] = k;
@@ -1623,7 +1651,7 @@ extern "C" int twosd_build_cut(twosd_ctx *c, int epi, const double *x, double ti
         *alpha = 0.0;
         for (int j = 0; j < c->n1; ++j) beta[j] = 0.0;
         if (weight_mark) *weight_mark = E.total_weight;
-        return TWOSD_OK;
+        return clear_cut_stats(c);
     }
     HIPCHK(hipEventRecord(c->ev[4], c->stream));
     if ((rc = cut_partial_impl(c, epi, x, tie_rel, E.total_weight, w->hist, w->sums))) return rc;
@@ -1678,7 +1706,7 @@ extern "C" int twosd_cut_partial(twosd_ctx *c, int epi, const double *x, double 
         HIPCHK(hipMemsetAsync(d_hist, 0, sizeof(uint64_t) * std::max(c->dvs.size, 1), c->stream));
         HIPCHK(hipMemsetAsync(d_sums, 0, sizeof(double) * (c->k + 1), c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
-        return TWOSD_OK;
+        return clear_cut_stats(c);
     }
     HIPCHK(hipEventRecord(c->ev[4], c->stream));
     if ((rc = cut_partial_impl(c, epi, x, tie_rel, total_weight, (unsigned long long *)d_hist, d_sums))) return rc;

@@ -349,3 +349,25 @@ def test_cut_storm_twins_with_vertex_split_tail():
     np.testing.assert_allclose(mv, omv, rtol=1e-12, atol=1e-9)
     assert cut.alpha == pytest.approx(a, rel=1e-8, abs=1e-8)
     np.testing.assert_allclose(cut.beta, b, rtol=1e-8, atol=1e-8 * (1 + np.abs(b).max()))
+
+
+def test_cut_log_offset_guard_and_empty_epigraph_stats():
+    """The argmax's candidate-log offsets are 32-bit: a cut needing more log slots than that is
+    refused with TWOSD_E_UNSUPPORTED instead of wrapping (limit lowered by the TWOSD_CUT_LOG_MAX
+    test hook), and the same cut runs once the limit allows it.  A cut over an epigraph with no
+    scenarios reports no fixup counters (not the previous cut's)."""
+    from sqlp_amd import twosd
+    from sqlp_amd._lib import TwoSDError
+    ctx, x, V = _setup("ssn", 512)
+    epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(epi, I.sample("ssn", 5000, 71))
+    with _env("TWOSD_CUT_LOG_MAX", "4096"):
+        with pytest.raises(TwoSDError) as ei:
+            twosd.build_sasa_cut(epi, x, V)
+        assert ei.value.code == -5 and "32-bit" in str(ei.value)
+    cut = twosd.build_sasa_cut(epi, x, V)
+    assert np.isfinite(cut.alpha)
+    empty = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    c0 = twosd.build_sasa_cut(empty, x, V)
+    assert c0.alpha == 0.0 and not c0.beta.any()
+    assert ctx.cut_stats()[:3] == (0, 0, 0)

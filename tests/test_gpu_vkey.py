@@ -126,3 +126,39 @@ def test_keyed_push_equals_push_all_at_scale(monkeypatch):
     assert r_all == N and r_key < N // 4
     assert (n_key, f_key) == (n_all, f_all), (n_key, n_all)
     print(f"storm {N} at SD candidate 4: |V| = {n_key}, representatives re-solved {r_key}")
+
+
+def test_keyed_push_equals_reference_push_at_100k():
+    """The keyed push against the reference rule itself, not the GPU's own push-all: storm, 131,072
+    scenarios at x_EV from a refreshed 4096-basis pool.  Every scenario's pi (the same solves, pi
+    recovered) is pushed in scenario order by the oracle's push! restatement (dual_set.jl:84-94,
+    twosd_ref.DualVertexSet.push_batch); the device's keyed solve_push must build the identical
+    ordered vertex set, bit for bit."""
+    from oracle import twosd_ref
+    from sqlp_amd import smps, twosd
+    inst = I.load("storm")
+    x = I.x_ev("storm")
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    ctx.compute_basis(x, smps.mean_values(inst["sto"]))
+    ctx.set_distributions(inst["sto"])
+    tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_sampled_scenarios(tr, 16384, 4243)
+    ctx.pool_refresh(tr, x, 0, 16384, 4096)
+    N = 131072
+    epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_sampled_scenarios(epi, N, 778)
+    V = twosd.sdDualVertexSet(ctx)
+    obj, st, _ = twosd.solve_push(epi, x, 0, N)
+    assert (st == 0).all()
+    reps = ctx.last_push_reps()
+    Vkey = V.matrix()
+    ref = twosd_ref.DualVertexSet()
+    for lo in range(0, N, 16384):                      # pi of every scenario, in order
+        o2, _, pis, st2 = twosd.solve_batch(epi, x, lo, 16384, want_pi=True)
+        assert (st2 == 0).all()
+        np.testing.assert_array_equal(o2, obj[lo:lo + 16384])
+        ref.push_batch(pis)
+    assert reps < N // 8
+    assert Vkey.shape == ref.matrix().shape, (Vkey.shape, len(ref))
+    np.testing.assert_array_equal(Vkey, ref.matrix())
+    print(f"storm {N} at x_EV: |V| = {len(ref)}, representatives re-solved {reps}")
