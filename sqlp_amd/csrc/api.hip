@@ -2341,10 +2341,19 @@ int twosd::run_lp_ex(twosd_ctx *c, const double *x, const double *d_dv, int N, c
     }
     if (!c->d_queue && (rc = dalloc(&c->d_queue, (size_t)kMaxQueueGroups * kQueueStride))) return rc;
     {
-        // eta capacity (pivots per scenario): 256 keeps two 4-wave blocks per CU within the LDS
-        const int kmax = c->kmax_override > 0 ? c->kmax_override : std::min(256, std::max(64, 2 * m + 32));
-        const int ecap = std::max(4096, 32 * MP);
+        // eta capacity (pivots per scenario): 2m + 32, at least 64.  256 keeps storm's two 4-wave
+        // blocks per CU within the LDS; past 256 the file grows (up to 1024, in steps of 32) as far as
+        // the LDS keeps the occupancy of 256 -- a scenario that needs more pivots from its pool start
+        // than the file holds is retried from the primary basis (ssn 100k: 11 in 8 steps at 256)
         const int CH = c->CH;
+        int kmax = c->kmax_override > 0 ? c->kmax_override : std::min(256, std::max(64, 2 * m + 32));
+        if (c->kmax_override <= 0 && 2 * m + 32 > kmax) {
+            const int b0 = hyper_max_blocks_per_cu(R, CH, kmax, c->k);
+            for (int k2 = std::min(1024, (2 * m + 32) & ~31); k2 > kmax; k2 -= 32)
+                if (hyper_max_blocks_per_cu(R, CH, k2, c->k) >= b0) { kmax = k2; break; }
+        }
+        // per-wave eta arena: 32 entries per row, scaled with the file past 256 pivots
+        const int ecap = (int)std::min<long long>(INT32_MAX / 2, (long long)std::max(4096, 32 * MP) * std::max(256, kmax) / 256);
         int bpc = hyper_max_blocks_per_cu(R, CH, kmax, c->k);
         if (const char *e = getenv("TWOSD_BPC")) bpc = std::min(bpc, std::max(1, atoi(e)));   // diagnostics: occupancy sweep
         if (bpc < 1) return fail(TWOSD_E_UNSUPPORTED, "LP kernel: LDS slice too large (m = %d, k = %d)", m, c->k);
