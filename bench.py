@@ -247,10 +247,14 @@ def main():
     src = twosd.sdEpigraph(ctx, 1.0, 0.0)
     scenarios(src, 0, 1 << 18, args.seed + 1)
     at = 0
+    piv_primary = [0, 0]   # pivots / scenarios of these solves: the instance's LP cost from the primary basis
     while len(V) < args.vertices and at < (1 << 18):
         _, _, pis, st = twosd.solve_batch(src, x, at, 16384, want_pi=True)
         V.push_batch(pis[st == 0])
+        piv_primary[0] += ctx.lp_stats()[0]
+        piv_primary[1] += 16384
         at += 16384
+    piv_primary = piv_primary[0] / max(piv_primary[1], 1)
     if len(V) > args.vertices:
         V.truncate(args.vertices)
     nv = len(V)
@@ -268,9 +272,14 @@ def main():
     # refresh builds four times that (at least 1024): its training and composition are split over
     # the ranks (profiles/r04/n8/shard_emulate_pool*.txt: at N = 8 with the bench warmup, pools of
     # 1024 / 1536 / 2048 / 3072 / 4096 bases give 18.7 / 18.3 / 18.4 / 20.3 / 22.1 ms per rank)
+    # instances whose LPs are long from the primary basis (ssn: ~39 pivots, ~20 etas traversed per
+    # pivot) take at least 2048 bases: the training solves cost more, the main solve saves more
+    # (ssn 100k on the driver protocol, profiles/r06/ab_ssn_pool.txt: 512 / 1024 / 2048 / 4096 bases
+    # -> 88.1 / 88.2 / 83.4 / 85.1 ms per step)
     if args.refresh_pool <= 0:
         scope = 4 * n_local * E if dist_refresh else n_local * E
-        args.refresh_pool = max(1024 if dist_refresh else 512, min(4096, int(4096 * scope / 1_000_000) // 256 * 256))
+        floor = 2048 if piv_primary > 16 else (1024 if dist_refresh else 512)
+        args.refresh_pool = max(floor, min(4096, int(4096 * scope / 1_000_000) // 256 * 256))
     if args.refresh_train <= 0:
         args.refresh_train = 4 * args.refresh_pool
     # pool refresh training scenarios (stream seed + 4; every rank holds all of them, or with
@@ -494,6 +503,7 @@ def main():
                                "LP solve + dual dedup + build_sasa_cut per step",
                    "instance": name, "scenarios": N, "epigraphs": E, "vertices": nv, "k": k, "m2": m,
                    "basis_pool": pool_size, "pool_build_s": round(t_pool, 3),
+                   "primary_basis_pivots_mean": round(piv_primary, 2),
                    "pool_refresh": ({"train": args.refresh_train, "pool": args.refresh_pool,
                                      "distributed": dist_refresh} if args.refresh else None),
                    "pool_selection": (f"two-level: {args.pool_level1} + {args.pool_cands} candidates"

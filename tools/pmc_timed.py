@@ -1,6 +1,9 @@
 """PMC counters of the TIMED launches of the driver's bench protocol, per x point.
 
 Usage: python tools/pmc_timed.py <gpurun_out/tag> <profiles/tag> [steps] [x_points]
+(steps, x points and epigraphs are taken from the passes' own bench JSON lines when present; the
+summary carries the workload key bench.py matches on -- pmc_summary.json for the storm driver
+workload, pmc_summary_<instance>_<N>_V<|V|>_E<E>.json for any other)
 
 Reads the rocprofv3 runs of tools/profile_r04.sh -- every pass is the driver's command
 `bench.py --gpus 1 --steps K --warmup W` (with --no-cpu --spot 0 --trajectory 0, so nothing
@@ -80,10 +83,28 @@ def timed_steps(disp, K):
     return steps
 
 
+def bench_config(src):
+    """(steps, warmup, x points, epigraphs, key) of the bench command the passes ran, from the JSON line
+    of any pass (every pass runs the same command)"""
+    for bj in sorted(glob.glob(os.path.join(src, "*_bench.json"))):
+        lines = [l for l in open(bj) if l.startswith("{")]
+        if lines:
+            d = json.loads(lines[-1])
+            c = d["config"]
+            key = {"instance": c["instance"], "scenarios": c["scenarios"], "vertices": c["vertices"],
+                   "epigraphs": c["epigraphs"], "n_gpus": d["n_gpus"]}
+            return d["steps"], d["warmup"], c["x_points"], c["epigraphs"], key, c["workload"]
+    return None
+
+
 def main():
     src, dst = sys.argv[1], sys.argv[2]
     K = int(sys.argv[3]) if len(sys.argv) > 3 else 20
     X = int(sys.argv[4]) if len(sys.argv) > 4 else 4
+    E, key, W, workload = 1, None, 5, None
+    cfg = bench_config(src)
+    if cfg:   # the command's own steps / x points / epigraphs and the workload key
+        K, W, X, E, key, workload = cfg
     os.makedirs(dst, exist_ok=True)
     per = defaultdict(lambda: defaultdict(lambda: defaultdict(list)))   # kernel -> x -> counter -> values
     meta = {}
@@ -99,20 +120,23 @@ def main():
     for tag, path in sorted(passes.items()):
         fs = [path]
         disp = load_pass(fs[0])
-        steps = timed_steps(disp, K)
+        # one cut launch per epigraph and step: every epigraph's pass is a sub-step
+        steps = timed_steps(disp, K * E)
         for i, st in enumerate(steps):
+            xi = (i // E) % X
             for k, d in st.items():
                 for cn, v in d["c"].items():
-                    per[k][i % X][cn].append(v)
-                per[k][i % X]["profiled_ms_" + tag].append(d["ms"])
+                    per[k][xi][cn].append(v)
+                per[k][xi]["profiled_ms_" + tag].append(d["ms"])
                 meta[k] = {"scratch_bytes_per_lane": d["scratch"], "vgpr": d["vgpr"]}
         bj = os.path.join(src, f"{tag}_bench.json")
         if os.path.exists(bj):
             lines = [l for l in open(bj) if l.startswith("{")]
             if lines:
                 bench_lines[tag] = json.loads(lines[-1])
-    out = {"protocol": f"driver command bench.py --gpus 1 --steps {K} --warmup 5 (--no-cpu --spot 0 --trajectory 0): "
-                       f"the {K} timed steps of each PMC pass, step i at x point i % {X}",
+    out = {"protocol": f"bench.py --gpus 1 --steps {K} --warmup {W} (--no-cpu --spot 0 --trajectory 0): "
+                       f"the {K} timed steps of each PMC pass ({E} epigraph pass(es) each), step i at x point i % {X}",
+           "key": key, "workload": workload,
            "units": "FETCH_SIZE / WRITE_SIZE: bytes per launch (rocprofv3 KiB x 1024); fetch_corrected = 2 x raw "
                     "(gfx950 wide-read calibration, MI355X_MICROARCH.md); SQ_*: per launch",
            "kernels": {}}
@@ -137,7 +161,7 @@ def main():
     # WRITE = a * scenarios + b * eta_bytes over the x points
     bw = bench_lines.get("pmc_write")
     lp = per.get("lp_hyper_kernel", {})
-    if bw and lp:
+    if bw and lp and E == 1:
         n = bw["config"]["scenarios"]
         xs, ws, eb = [], [], []
         for x, cs in sorted(lp.items()):
@@ -164,7 +188,7 @@ def main():
     dur = defaultdict(list)
     tr = glob.glob(os.path.join(src, "trace_trace.csv.gz")) + glob.glob(os.path.join(src, "trace", "**", "*kernel_trace.csv"), recursive=True)
     if tr:
-        for st in timed_steps(load_trace(tr[0]), K):
+        for st in timed_steps(load_trace(tr[0]), K * E):
             for k, d in st.items():
                 dur[k].append(d["ms"])
     out["trace_ms"] = {k: float(np.mean(v)) for k, v in dur.items()}
@@ -172,14 +196,15 @@ def main():
         json.dump(out, f, indent=1)
     # the summary bench.py reads (latest profiles/r*/pmc_summary.json): per kernel, the mean over
     # the timed launches of the driver's protocol
-    summ = {"workload": "storm 1000000 scenarios, the driver's bench.py --gpus 1 --steps %d --warmup 5, 1 MI355X" % K,
+    summ = {"workload": (workload or "storm 1000000 scenarios") + f"; bench.py --gpus 1 --steps {K} --warmup {W}, 1 MI355X",
+            "key": key or {"instance": "storm", "scenarios": 1_000_000, "vertices": 4096, "epigraphs": 1, "n_gpus": 1},
             "source": "rocprofv3 --kernel-trace --stats and separate --pmc passes over that command "
                       "(tools/profile_r04.sh, reduced on the box by tools/prof_reduce.py); means over the timed steps' "
                       "launches (tools/pmc_timed.py)",
             "correction": "FETCH_SIZE/WRITE_SIZE are KiB; hbm_bytes = 1024*(2*FETCH_SIZE + WRITE_SIZE) (the guide's gfx950 "
                           "correction for wide reads; an upper estimate for narrow accesses); hbm_bytes_raw = "
                           "1024*(FETCH_SIZE + WRITE_SIZE)",
-            "scenarios": 1_000_000, "kernels": {}}
+            "scenarios": (key or {}).get("scenarios", 1_000_000), "kernels": {}}
     for k, ent in out["kernels"].items():
         m = ent["mean"]
         f_kib = m.get("FETCH_SIZE", 0.0) / 1024.0
@@ -203,8 +228,14 @@ def main():
         summ["kernels"][k] = e
     if "lp_write_split" in out:
         summ["lp_write_split"] = out["lp_write_split"]["fit"]
-    with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
+    k_ = summ["key"]
+    default = (k_["instance"], k_["scenarios"], k_["vertices"], k_["epigraphs"]) == ("storm", 1_000_000, 4096, 1)
+    name = "pmc_summary.json" if default else \
+        f"pmc_summary_{k_['instance']}_{k_['scenarios']}_V{k_['vertices']}_E{k_['epigraphs']}.json"
+    with open(os.path.join(dst, name), "w") as f:
         json.dump(summ, f, indent=1)
+    if not default:
+        os.replace(os.path.join(dst, "pmc_timed.json"), os.path.join(dst, name.replace("pmc_summary", "pmc_timed")))
     print(json.dumps({k: v["mean"] for k, v in out["kernels"].items()}, indent=1))
     if "lp_write_split" in out:
         print(json.dumps(out["lp_write_split"], indent=1))
