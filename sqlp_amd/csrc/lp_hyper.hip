@@ -465,7 +465,17 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                     for (int g = 0; g < EG; ++g) {
                         const int tt = tg - g;
                         if (tt < 0) break;
-                        double acc = gv[g] != 0.0 ? ut[gi[g]] * gv[g] : 0.0;
+                        const double ug = gv[g] != 0.0 ? ut[gi[g]] : 0.0;
+                        // a dead eta: u is zero on all its rows (u holds only r and the pivot rows
+                        // set so far), so u . eta_t = 0 and u[p_t] -- one of those rows (the pivot
+                        // entry 1 / alpha_r is never zero) -- is zero already: nothing to write.
+                        // (Skipped, the pivot row keeps its zero instead of being rewritten with a
+                        // zero of either sign; every later use tests u != 0.)
+                        if (gn[g] <= 64 && __builtin_amdgcn_ballot_w64(ug != 0.0) == 0) {
+                            nops += gn[g];
+                            continue;
+                        }
+                        double acc = ug * gv[g];
                         for (int e = 64 + lane; e < gn[g]; e += 64) acc = fma(ut[eidx[go[g] + e]], evals[go[g] + e], acc);
                         acc = wsum(acc);
                         nops += gn[g];
@@ -696,8 +706,8 @@ __global__ void __launch_bounds__(256, TWOSD_HYPER_WPE(R)) lp_hyper_kernel(Hyper
                                 else lds_add(&ut[i], ev * vp);
                             }
                             nops += gn[g];
+                            h_wave_sync();   // (an eta that wrote nothing needs no ordering)
                         }
-                        h_wave_sync();
                     }
                 };
                 int ai[EG], an[EG], ao[EG], bi[EG], bn[EG], bo[EG];
