@@ -278,6 +278,15 @@ int twosd_build_cut(twosd_ctx *ctx, int epi, const double *x, double tie_rel,
 int twosd_cut_stats(twosd_ctx *ctx, int64_t *out);
 
 /*
+ * The MFMA pass the last twosd_build_cut / twosd_cut_partial ran (diagnostics, synchronous read):
+ * *fp32 = 1 the fp32 pass (v_mfma_f32_16x16x4f32, decisions within its wider error band), 0 the
+ * fp64 pass (TWOSD_CUT_F32=0, or operands outside the fp32 envelope); *band = that pass's
+ * decision band.  Either pass gives the restatement's picks (cut_fixup_kernel re-decides every
+ * row with several vertices in the band).
+ */
+int twosd_cut_pass(twosd_ctx *ctx, int *fp32, double *band);
+
+/*
  * Multi-GPU split of twosd_build_cut: each rank computes partial sums over its own
  * scenarios into a caller-provided DEVICE buffer (layout in twosd_cut_partial_len),
  * the caller all-reduces it (sum; e.g. torch.distributed / RCCL), then finalize.

@@ -76,6 +76,7 @@ SIGNATURES = [
     ("twosd_refresh_cap_stats", I, [P, P, P]),
     ("twosd_training_cap", I, [P, C.c_int64, C.c_int64, P]),
     ("twosd_cut_stats", I, [P, P]),
+    ("twosd_cut_pass", I, [P, P, P]),
     ("twosd_select_refresh_bases", I, [P, P, P, P, I, I, P, P, P]),
     ("twosd_last_objective", I, [P, P, P]),
     ("twosd_refresh_train_bases", I, [P, P, P, P]),

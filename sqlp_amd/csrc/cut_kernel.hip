@@ -47,6 +47,7 @@
 #include <math.h>
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 #include "twosd_ctx.h"
 
@@ -76,7 +77,9 @@ struct CutParams {
     const double *basec;   // base of the argmax's vertices, per x
     const double *base;    // nv: pi_v . bvec in index order (the restatement's base dot)
     const int *eord;       // k: elements by ascending row (the restated score's order)
-    const unsigned long long *band_bits;   // the band: band_scale x max_v (|base[v]| + sum_e |PK[v,e] coef_e| dmax_e), as bits
+    const unsigned long long *band_bits;   // the ACTIVE band of this cut, as bits (cut_band_select_kernel)
+    const unsigned long long *mode;        // 1: this cut's MFMA pass runs in fp32 (cut_argmax3_kernel), 0: fp64 (cut_argmax2_kernel)
+    const float *PKTc32;   // KR32 x vcap32: PKTc's element rows rounded to fp32, no base row (cut_argmax3_kernel's LDS-DMA source)
     double band_scale;     // 4 gamma_{k+4}: twice the 2 gamma bound
     int *arg; double *val; int *flag;   // N; flag != 0: re-decide (main rows: 4-bit log counts per lane group)
     int *cand;             // candidate logs of the whole tiles: [(s * 4 + g) * kCandC + i]
@@ -235,17 +238,21 @@ __global__ void cut_compact_rows_kernel(int nv, int k4, const int *__restrict__ 
 // outside [0, k) x [0, nvc) (the LDS-DMA source of cut_argmax2_kernel; per x).
 // With base != nullptr, row k holds base[vmap[c]] (-inf for c >= nvc): the MFMA then adds the
 // vertex base through a constant 1 in the scenarios' delta column k.
+// PKTc32 (rows32 rows, may be null): the element rows of PKTc rounded to fp32, zero past k (the
+// fp32 pass adds the base in fp64 outside the MFMA)
 __global__ void cut_pktc_kernel(int k, int rows, int vcap, int vcap32, const double *__restrict__ PKT,
                                 const double *__restrict__ coef, const double *__restrict__ base, const int *__restrict__ vmap,
-                                const int *__restrict__ nvc_p, double *__restrict__ PKTc) {
+                                const int *__restrict__ nvc_p, double *__restrict__ PKTc, int rows32, float *__restrict__ PKTc32) {
     const int nvc = *nvc_p;
-    const size_t total = (size_t)rows * vcap32;
+    const size_t total = (size_t)std::max(rows, PKTc32 ? rows32 : 0) * vcap32;
     for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
         const int kk = (int)(idx / vcap32), c = (int)(idx % vcap32);
         const int v = c < nvc ? vmap[c] : 0;
-        double x = (kk < k && c < nvc) ? coef[kk] * PKT[(size_t)kk * vcap + v] : 0.0;
+        const double pc = (kk < k && c < nvc) ? coef[kk] * PKT[(size_t)kk * vcap + v] : 0.0;
+        double x = pc;
         if (base && kk == k) x = c < nvc ? base[v] : -INFINITY;
-        PKTc[idx] = x;
+        if (kk < rows) PKTc[idx] = x;
+        if (PKTc32 && kk < rows32) PKTc32[idx] = (float)pc;
     }
 }
 
@@ -258,7 +265,7 @@ __global__ void __launch_bounds__(256) cut_vbase_kernel(int nv, int m, int k, in
                                                         const double *__restrict__ bvec, const double *__restrict__ PK,
                                                         const double *__restrict__ coef, const unsigned long long *__restrict__ dmax,
                                                         double *__restrict__ base, unsigned long long *__restrict__ band_bits,
-                                                        double band_scale) {
+                                                        double band_scale, double band_scale32) {
 #pragma clang fp contract(off)
     __shared__ double prod[4][kVbSlice];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -279,18 +286,46 @@ __global__ void __launch_bounds__(256) cut_vbase_kernel(int nv, int m, int k, in
             __syncthreads();
         }
         if (!act) continue;
-        double a = 0.0;
-        for (int e = lane; e < k; e += 64)
-            a += fabs(PK[(size_t)v * k4 + e] * coef[e]) * __longlong_as_double((long long)dmax[e]);
+        double a = 0.0, pm = 0.0, dm = 0.0;
+        for (int e = lane; e < k; e += 64) {
+            const double pc = fabs(PK[(size_t)v * k4 + e] * coef[e]), de = __longlong_as_double((long long)dmax[e]);
+            a += pc * de;
+            pm = fmax(pm, pc);
+            dm = fmax(dm, de);
+        }
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+        for (int o = 32; o > 0; o >>= 1) {
+            a += __shfl_xor(a, o);
+            pm = fmax(pm, __shfl_xor(pm, o));
+            dm = fmax(dm, __shfl_xor(dm, o));
+        }
         if (lane == 0) {
             base[v] = s;
             const double t = fabs(s) + a;
             // the band itself (a positive scale keeps the order of the maxima, rounding included)
-            atomicMax(band_bits, (unsigned long long)__double_as_longlong(isfinite(t) ? band_scale * t : INFINITY));
+            const double b64 = isfinite(t) ? band_scale * t : INFINITY;
+            atomicMax(band_bits, (unsigned long long)__double_as_longlong(b64));
+            // the fp32 pass: the element terms rounded to fp32 and summed by an fmaf chain (the f32
+            // MFMA's arithmetic) differ from the exact dot by at most gamma_{k+2}(u32) a, plus
+            // 2^-126 (1 + max|PK coef| + max dmax) per term for operands and partial sums below
+            // the normal range; scale32 = 4 gamma_{k+4}(u32) doubles that bound as band_scale does.
+            // The base stays fp64 (the restatement's own value), so the fp64 band is added.
+            const double b32 = b64 + band_scale32 * a + 4.0 * (k + 4) * ldexp(1.0, -126) * (1.0 + pm + dm);
+            atomicMax(band_bits + 1, (unsigned long long)__double_as_longlong(isfinite(b32) ? b32 : INFINITY));
+            // operands and sums well inside the fp32 range, or the cut runs the fp64 pass
+            const double lim = ldexp(1.0, 100);
+            if (!(a < lim && pm < lim && dm < lim)) atomicOr(band_bits + 2, 1ull);
         }
     }
+}
+
+// the cut's pass: fp32 when asked and every vertex's operands fit (band_bits[2] == 0), else
+// fp64; band_bits[3] = that pass's band (what every later kernel of the cut reads), [4] = the pass
+__global__ void cut_band_select_kernel(unsigned long long *band_bits, int want32) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const unsigned long long m = (want32 && band_bits[2] == 0) ? 1ull : 0ull;
+    band_bits[3] = m ? band_bits[1] : band_bits[0];
+    band_bits[4] = m;
 }
 
 // dmax[e] = max |dv[s][e]| over scenarios [from, to) folded into the epigraph's running maximum
@@ -371,6 +406,25 @@ constexpr int kLdsRow2 = 32;             // doubles per k-row of a chunk
 // two k-rows a half-wave reads together (g = 0, 1 / 2, 3) fall on disjoint banks
 __device__ __forceinline__ int lds2(int kk, int vv) { return kk * kLdsRow2 + (vv ^ ((kk & 1) << 4)); }
 
+// The value of a decided row in fp64, the same bits in every pass, split and kernel: base[I] + t,
+// t = (c_0 + c_1) + (c_2 + c_3), c_g the fma chain over e = g, g + 4, g + 8, ... < k of
+// (PK[I,e] coef_e) dv_e from 0.  dec_lane_chain is lane (g, .)'s c_g from its register deltas
+// d[kb] (e = 4 kb + g); dec_combine the xor-16 / xor-32 sum that forms t on every lane of the column.
+template <int KB, typename D>
+__device__ __forceinline__ double dec_lane_chain(const CutParams &P, const double *pk, const D (&d)[KB], int g) {
+    double c = 0.0;
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+        const int e = 4 * kb + g;
+        if (e < P.k) c = fma(pk[e] * P.coef[e], (double)d[kb], c);
+    }
+    return c;
+}
+__device__ __forceinline__ double dec_combine(double c) {
+    c += __shfl_xor(c, 16);
+    return c + __shfl_xor(c, 32);
+}
+
 // Combine the 4 lanes (g) of a scenario column: the row maximum M, and for each lane the number
 // of its logged entries that can lie in the band of M (0 when the lane's own max is below the
 // band floor).  tot == 1: the row is decided, its pick the first vertex of the one lane that
@@ -401,6 +455,7 @@ __device__ __forceinline__ void combine_ex(RowEx &rb, double rel, double band, i
 #endif
 template <int KB>
 __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_argmax2_kernel(CutParams P) {
+    if (*P.mode != 0) return;                       // the fp32 pass runs this cut (cut_argmax3_kernel)
     __shared__ double Bs[2][4 * KB * kLdsRow2];     // double-buffered chunk (k-major)
     constexpr bool kHold = !(TWOSD_CUT_LB3 && KB <= 22);   // a register for the logs' first entries (2 blocks per CU)
     extern __shared__ unsigned long long hl[];      // nv entries when P.hist_lds
@@ -534,12 +589,17 @@ __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_
         }
         if (nt0 < 2) pk0 = 0;   // decided
         if (nt1 < 2) pk1 = 0;
-        if (g == 0) {
-            if (sa < P.N) { P.arg[sa] = rb0.I; P.val[sa] = rb0.M; P.flag[sa] = pk0; }
-            if (sb < P.N) { P.arg[sb] = rb1.I; P.val[sb] = rb1.M; P.flag[sb] = pk1; }
-        }
         const bool ok0 = sa < P.N && !pk0 && rb0.I >= 0, ok1 = sb < P.N && !pk1 && rb1.I >= 0;
         const double p0 = ok0 ? P.w[sa] * P.inv_total : 0.0, p1 = ok1 ? P.w[sb] * P.inv_total : 0.0;
+        // decided rows: the pick's fp64 value (dec_lane_chain; flagged rows keep the pass's maximum,
+        // the fixup writes their restated value)
+        const double tv0 = dec_combine(dec_lane_chain<KB>(P, P.PK + (size_t)(rb0.I >= 0 ? rb0.I : 0) * P.k4, a0, g));
+        const double tv1 = dec_combine(dec_lane_chain<KB>(P, P.PK + (size_t)(rb1.I >= 0 ? rb1.I : 0) * P.k4, a1, g));
+        const double vl0 = ok0 ? P.base[rb0.I] + tv0 : rb0.M, vl1 = ok1 ? P.base[rb1.I] + tv1 : rb1.M;
+        if (g == 0) {
+            if (sa < P.N) { P.arg[sa] = rb0.I; P.val[sa] = vl0; P.flag[sa] = pk0; }
+            if (sb < P.N) { P.arg[sb] = rb1.I; P.val[sb] = vl1; P.flag[sb] = pk1; }
+        }
         // sum p * val and the vertex histogram, scenarios in order (lane 0 reads them from lanes 0-15)
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
@@ -548,7 +608,7 @@ __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_
                 const int ok = __shfl(t == 0 ? (int)ok0 : (int)ok1, jj);
                 const int ai = __shfl(t == 0 ? rb0.I : rb1.I, jj);
                 const double pp = __shfl(t == 0 ? p0 : p1, jj);
-                const double vl = __shfl(t == 0 ? rb0.M : rb1.M, jj);
+                const double vl = __shfl(t == 0 ? vl0 : vl1, jj);
                 if (lane == 0 && ok) {
                     pv_sum = fma(pp, vl, pv_sum);
                     const unsigned long long hq = (unsigned long long)__double2ull_rn(pp * kFix);
@@ -586,6 +646,222 @@ __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_
     double *out = P.partial + (size_t)slot * (P.k + 1);
     if (lane == 0) out[0] = pv_sum;
     // lane (g, j) owns e = 4 j + g (kb = j) and e = 4 (j + 16) + g (kb = j + 16)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int e = 4 * (j + 16 * t) + g;
+        if (e < P.k) out[1 + e] = Sacc[t];
+    }
+}
+
+// ---- v3: the fp32 MFMA pass (v_mfma_f32_16x16x4f32: twice the fp64 rate on gfx950, an exact
+// fmaf chain).  The layout of v2 with fp32 operands: the vertex chunk (coef_e(x) PK rows rounded
+// to fp32, no base row) DMA'd into LDS, the scenario deltas rounded to fp32 in registers.  The
+// MFMA gives t32 ~ sum_e PK[v,e] coef_e dv[w,e]; the score is base[v] + t32 in fp64 (the base is
+// the restatement's own fp64 value), within the fp32 band of the restated score
+// (cut_vbase_kernel), and the decisions, logs, tail ranges and fixup are those of v2 with that
+// band.  The f32 C/D layout: register r of a tile is vertex row 4g + r, scenario column j.  At the
+// end of a tile the two scenarios' fp64 deltas are read again for the S_e sums and the decided
+// rows' values (fp64, from the pick's PK row).
+constexpr int kLdsRow3 = 32;             // floats per k-row of an fp32 chunk (32 vertices)
+// LDS position of (k-row kk, vertex vv): a 128-byte k-row puts rows kk and kk + 2 on the same
+// banks, so rows with (kk >> 1) odd have their 16-float halves swapped: the four k-rows a wave
+// reads together (g = 0..3) fall on disjoint banks
+__device__ __forceinline__ int lds3(int kk, int vv) { return kk * kLdsRow3 + (vv ^ (((kk >> 1) & 1) << 4)); }
+// k-rows staged per chunk: KB k-blocks of 4, rounded up to whole 8-row (1 KiB) DMA instructions
+__host__ __device__ constexpr int kr32(int KB) { return 8 * ((KB + 1) / 2); }
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+#ifndef TWOSD_CUT3_BPC
+#define TWOSD_CUT3_BPC 2                 // blocks per CU the fp32 pass is compiled for
+#endif
+
+template <int KB>
+__global__ void __launch_bounds__(256, TWOSD_CUT3_BPC) cut_argmax3_kernel(CutParams P) {
+    if (*P.mode != 1) return;                       // the fp64 pass runs this cut (cut_argmax2_kernel)
+    constexpr int KR = kr32(KB);
+    __shared__ float Bs[2][KR * kLdsRow3];          // double-buffered chunk (k-major)
+    extern __shared__ unsigned long long hl[];      // nv entries when P.hist_lds
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (P.hist_lds)
+        for (int v = threadIdx.x; v < P.nv; v += 256) hl[v] = 0ull;
+    const int g = lane >> 4, j = lane & 15;
+    const int ntiles = (P.N + kCutTile2 - 1) / kCutTile2;
+    const int nvc = *P.nvc;
+    const int nchunks = (nvc + kVT2 - 1) / kVT2;
+    const int nunits = P.full_units + (ntiles - P.full_units) * P.tail_S;
+    const double band = cut_band_scalar(P);
+    const double rel = P.tie_rel;
+    double pv_sum = 0.0;
+    double Sacc[2] = {0.0, 0.0};   // lane (g, j): e = 4 kb + g for kb = j, j + 16
+
+    for (int unit = blockIdx.x; unit < nunits; unit += gridDim.x) {
+        const bool tail = unit >= P.full_units;
+        const int tile = tail ? P.full_units + (unit - P.full_units) / P.tail_S : unit;
+        const int range = tail ? (unit - P.full_units) % P.tail_S : 0;
+        const int c_lo = tail ? (int)((long long)nchunks * range / P.tail_S) : 0;
+        const int c_hi = tail ? (int)((long long)nchunks * (range + 1) / P.tail_S) : nchunks;
+        const int s0 = tile * kCutTile2 + wid * 32;
+        const int sa = s0 + j, sb = s0 + 16 + j;
+        float a0[KB], a1[KB];
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+            const int e = 4 * kb + g;
+            a0[kb] = (sa < P.N && e < P.k) ? (float)P.dv[(size_t)sa * P.k + e] : 0.0f;
+            a1[kb] = (sb < P.N && e < P.k) ? (float)P.dv[(size_t)sb * P.k + e] : 0.0f;
+        }
+        RowEx rb0, rb1;
+        rb0.M = -INFINITY; rb0.thr = -INFINITY; rb0.I = -1; rb0.n = 0; rb0.f = 0;
+        rb1 = rb0;
+        int *const lbase = tail ? P.tcand : P.cand;
+        const unsigned log0 = tail ? (unsigned)(((((size_t)(s0 + j - P.full_units * kCutTile2)) * P.tail_S + range) * 4 + g) * kCandC)
+                                      : (unsigned)((((size_t)(s0 + j)) * 4 + g) * kCandC);
+        const unsigned lstep = 16u * (tail ? P.tail_S : 1) * 4 * kCandC;
+
+        // LDS-DMA staging (global_load_lds_dwordx4): instruction i writes k-rows 8i .. 8i+7 (1 KiB,
+        // lane-linear), lane L the 4 floats at LDS position 4 (L % 8) of row 8i + L/8; the source
+        // vertices are that position with lds3's half swap applied
+        auto stage = [&](int buf, int v0) {
+            for (int i = wid; i < KR / 8; i += 4) {
+                const int kk = 8 * i + (lane >> 3);
+                const int vv = (4 * (lane & 7)) ^ (((kk >> 1) & 1) << 4);
+                __builtin_amdgcn_global_load_lds((const void *)(P.PKTc32 + (size_t)kk * P.vcap32 + v0 + vv),
+                                                 (__attribute__((address_space(3))) void *)&Bs[buf][i * 8 * kLdsRow3], 16, 0, 0);
+            }
+        };
+        stage(0, c_lo * kVT2);
+        __syncthreads();
+        for (int ch = c_lo; ch < c_hi; ++ch) {
+            const int buf = (ch - c_lo) & 1;
+            const int v0 = ch * kVT2;
+            if (ch + 1 < c_hi) stage(buf ^ 1, v0 + kVT2);
+            // the fp64 bases of this lane's 8 vertices (positions v0 + 4g + r, v0 + 16 + 4g + r;
+            // -inf past the argmax's vertices), in flight under the MFMAs
+            double bq[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int c = v0 + (r >> 2) * 16 + 4 * g + (r & 3);
+                const double b = P.basec[c < nvc ? c : 0];
+                bq[r] = c < nvc ? b : -INFINITY;
+            }
+            f4 c00 = {0.0f, 0.0f, 0.0f, 0.0f}, c01 = c00, c10 = c00, c11 = c00;
+            constexpr int KG = TWOSD_CUT_KG;
+#pragma unroll
+            for (int k0 = 0; k0 < KB; k0 += KG) {
+                float x0[KG], x1[KG];
+#pragma unroll
+                for (int u = 0; u < KG; ++u) {
+                    if (k0 + u < KB) {
+                        x0[u] = Bs[buf][lds3(4 * (k0 + u) + g, j)];
+                        x1[u] = Bs[buf][lds3(4 * (k0 + u) + g, 16 + j)];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < KG; ++u) {
+                    if (k0 + u < KB) {
+                        c00 = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[u], a0[k0 + u], c00, 0, 0, 0);
+                        c01 = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[u], a1[k0 + u], c01, 0, 0, 0);
+                        c10 = __builtin_amdgcn_mfma_f32_16x16x4f32(x1[u], a0[k0 + u], c10, 0, 0, 0);
+                        c11 = __builtin_amdgcn_mfma_f32_16x16x4f32(x1[u], a1[k0 + u], c11, 0, 0, 0);
+                    }
+                }
+                if (TWOSD_CUT_SB) __builtin_amdgcn_sched_barrier(0);
+            }
+            // this lane's vertices in increasing order: v0 + 4g + r, then v0 + 16 + 4g + r
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                row_fast<false>(rb0, bq[r] + (double)c00[r], v0 + 4 * g + r, rel, band, lbase, log0);
+                row_fast<false>(rb1, bq[r] + (double)c01[r], v0 + 4 * g + r, rel, band, lbase, log0 + lstep);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                row_fast<false>(rb0, bq[4 + r] + (double)c10[r], v0 + 16 + 4 * g + r, rel, band, lbase, log0);
+                row_fast<false>(rb1, bq[4 + r] + (double)c11[r], v0 + 16 + 4 * g + r, rel, band, lbase, log0 + lstep);
+            }
+            __syncthreads();
+        }
+        int pk0, pk1, nt0, nt1;
+        combine_ex(rb0, rel, band, g, pk0, nt0);
+        combine_ex(rb1, rel, band, g, pk1, nt1);
+        rb0.I = rb0.I >= 0 ? P.vmap[rb0.I] : -1;
+        rb1.I = rb1.I >= 0 ? P.vmap[rb1.I] : -1;
+        if (tail) {
+            if (g == 0) {
+                const int t0 = P.full_units * kCutTile2;
+                if (sa < P.N) {
+                    const size_t o = (size_t)(sa - t0) * P.tail_S + range;
+                    P.tp_m[o] = rb0.M; P.tp_i[o] = rb0.I; P.tp_f[o] = pk0;
+                }
+                if (sb < P.N) {
+                    const size_t o = (size_t)(sb - t0) * P.tail_S + range;
+                    P.tp_m[o] = rb1.M; P.tp_i[o] = rb1.I; P.tp_f[o] = pk1;
+                }
+            }
+            continue;
+        }
+        if (nt0 < 2) pk0 = 0;
+        if (nt1 < 2) pk1 = 0;
+        const bool ok0 = sa < P.N && !pk0 && rb0.I >= 0, ok1 = sb < P.N && !pk1 && rb1.I >= 0;
+        const double p0 = ok0 ? P.w[sa] * P.inv_total : 0.0, p1 = ok1 ? P.w[sb] * P.inv_total : 0.0;
+        // per scenario of the tile: its fp64 deltas again (this lane's e = 4 kb + g), the S_e terms
+        // of its pick (the xor tree of v2's s_pass) and its value base[a] + sum_e PK[a,e] coef_e dv_e
+        // in fp64 (the lanes' partial sums combined over g in a fixed order)
+        auto fin = [&](int sx, bool ok, int ai, double pp) -> double {
+            const double *pk = P.PK + (size_t)(ai >= 0 ? ai : 0) * P.k4;
+            const double pu = ok ? pp : 0.0;
+            double d64[KB];
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb) {
+                const int e = 4 * kb + g;
+                d64[kb] = (sx < P.N && e < P.k) ? P.dv[(size_t)sx * P.k + e] : 0.0;
+            }
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb) {
+                const int e = 4 * kb + g;
+                const double pke = e < P.k ? pk[e] : 0.0;
+                double v = (e < P.k) ? pu * pke * d64[kb] : 0.0;
+#pragma unroll
+                for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o);
+                if (j == (kb & 15)) {
+                    if (kb < 16) Sacc[0] += v;
+                    else Sacc[1] += v;
+                }
+            }
+            return dec_combine(dec_lane_chain<KB>(P, pk, d64, g));
+        };
+        const double tv0 = fin(sa, ok0, rb0.I, p0);
+        const double tv1 = fin(sb, ok1, rb1.I, p1);
+        // decided rows: the fp64 value of the pick; flagged rows keep the MFMA maximum (the fixup
+        // re-scores them and writes the restated value)
+        const double vl0 = ok0 ? P.base[rb0.I] + tv0 : rb0.M, vl1 = ok1 ? P.base[rb1.I] + tv1 : rb1.M;
+        if (g == 0) {
+            if (sa < P.N) { P.arg[sa] = rb0.I; P.val[sa] = vl0; P.flag[sa] = pk0; }
+            if (sb < P.N) { P.arg[sb] = rb1.I; P.val[sb] = vl1; P.flag[sb] = pk1; }
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) {
+                const int ok = __shfl(t == 0 ? (int)ok0 : (int)ok1, jj);
+                const int ai = __shfl(t == 0 ? rb0.I : rb1.I, jj);
+                const double pp = __shfl(t == 0 ? p0 : p1, jj);
+                const double vl = __shfl(t == 0 ? vl0 : vl1, jj);
+                if (lane == 0 && ok) {
+                    pv_sum = fma(pp, vl, pv_sum);
+                    const unsigned long long hq = (unsigned long long)__double2ull_rn(pp * kFix);
+                    if (P.hist_lds) __hip_atomic_fetch_add(&hl[ai], hq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    else atomicAdd(&P.hist[ai], hq);
+                }
+            }
+        }
+    }
+    if (P.hist_lds) {
+        __syncthreads();
+        for (int v = threadIdx.x; v < P.nv; v += 256) P.hist_part[(size_t)blockIdx.x * P.nv + v] = hl[v];
+    }
+    const int slot = blockIdx.x * 4 + wid;
+    double *out = P.partial + (size_t)slot * (P.k + 1);
+    if (lane == 0) out[0] = pv_sum;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
         const int e = 4 * (j + 16 * t) + g;
@@ -643,14 +919,25 @@ __global__ void __launch_bounds__(256) cut_tail_merge_kernel(CutParams P, int sl
         if (lane == 0) { P.arg[s] = I; P.val[s] = M; P.flag[s] = fl; }
         if (fl || I < 0) continue;
         const double p = P.w[s] * P.inv_total;
-        if (lane == 0) {
-            pv_sum = fma(p, M, pv_sum);
-            atomicAdd(&P.hist[I], (unsigned long long)__double2ull_rn(p * kFix));
-        }
+        // the S_e terms of the pick and its value in fp64, base[I] + sum_e PK[I,e] coef_e dv_e (the
+        // lanes' terms summed by a fixed xor tree; the pass's maximum M may be an fp32-MFMA score)
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             const int e = lane + 64 * t;
             if (e < P.k) Sacc[t] = fma(p * P.PK[(size_t)I * P.k4 + e], P.dv[(size_t)s * P.k + e], Sacc[t]);
+        }
+        // lane g < 4: the chain c_g of dec_lane_chain, then (c_0 + c_1) + (c_2 + c_3) as dec_combine
+        double cg = 0.0;
+        if (lane < 4) {
+            const double *pk = P.PK + (size_t)I * P.k4, *dr = P.dv + (size_t)s * P.k;
+            for (int e = lane; e < P.k; e += 4) cg = fma(pk[e] * P.coef[e], dr[e], cg);
+        }
+        const double c01 = __shfl(cg, 0) + __shfl(cg, 1), c23 = __shfl(cg, 2) + __shfl(cg, 3);
+        const double vl = P.base[I] + (c01 + c23);
+        if (lane == 0) {
+            P.val[s] = vl;
+            pv_sum = fma(p, vl, pv_sum);
+            atomicAdd(&P.hist[I], (unsigned long long)__double2ull_rn(p * kFix));
         }
     }
     double *out = P.partial + (size_t)(slot0 + gw) * (P.k + 1);
@@ -1146,6 +1433,8 @@ struct CutWs {
     double *PK = nullptr, *PKT = nullptr, *PKO = nullptr;
     double *PKTc = nullptr;
     size_t pktc_cap = 0;
+    float *PKTc32 = nullptr;               // the fp32 pass's chunk source
+    size_t pktc32_cap = 0;
     int pk_count = 0, pk_vcap = 0, pk_k4 = 0;
     size_t pk_cap = 0;
     int *rows = nullptr;
@@ -1191,7 +1480,7 @@ static CutWs *cws(twosd_ctx *c) {
 void cut_free(twosd_ctx *c) {
     if (!c->cut_ws) return;
     CutWs *w = (CutWs *)c->cut_ws;
-    hipFree(w->PK); hipFree(w->PKT); hipFree(w->PKO); hipFree(w->PKTc); hipFree(w->rows); hipFree(w->eord); hipFree(w->coef); hipFree(w->bvec); hipFree(w->base);
+    hipFree(w->PK); hipFree(w->PKT); hipFree(w->PKO); hipFree(w->PKTc); hipFree(w->PKTc32); hipFree(w->rows); hipFree(w->eord); hipFree(w->coef); hipFree(w->bvec); hipFree(w->base);
     hipFree(w->partial); hipFree(w->sums); hipFree(w->gpart); hipFree(w->g); hipFree(w->arg); hipFree(w->flag);
     hipFree(w->val); hipFree(w->hist); hipFree(w->part2); hipFree(w->hist_part);
     hipFree(w->tp_m); hipFree(w->tp_i); hipFree(w->tp_f);
@@ -1280,6 +1569,38 @@ static int argmax_occupancy(int KB, size_t dyn_lds) {
         case 32: return argmax_occupancy_t<32>(dyn_lds);
     }
     return 0;
+}
+
+template <int KB>
+static void launch_argmax3_t(const CutParams &P, int nblocks, hipStream_t s) {
+    hipLaunchKernelGGL(cut_argmax3_kernel<KB>, dim3(nblocks), dim3(256), P.hist_lds ? sizeof(unsigned long long) * P.nv : 0, s, P);
+}
+template <int KB>
+static int argmax3_occupancy_t(size_t dyn_lds) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cut_argmax3_kernel<KB>, 256, dyn_lds) != hipSuccess) nb = 0;
+    return nb;
+}
+#define CUT_KB_SWITCH(FN, ...)                          \
+    switch (KB) {                                       \
+        case 1: return FN<1>(__VA_ARGS__);              \
+        case 2: return FN<2>(__VA_ARGS__);              \
+        case 4: return FN<4>(__VA_ARGS__);              \
+        case 6: return FN<6>(__VA_ARGS__);              \
+        case 8: return FN<8>(__VA_ARGS__);              \
+        case 12: return FN<12>(__VA_ARGS__);            \
+        case 16: return FN<16>(__VA_ARGS__);            \
+        case 22: return FN<22>(__VA_ARGS__);            \
+        case 24: return FN<24>(__VA_ARGS__);            \
+        case 30: return FN<30>(__VA_ARGS__);            \
+        case 32: return FN<32>(__VA_ARGS__);            \
+    }
+static int argmax3_occupancy(int KB, size_t dyn_lds) {
+    CUT_KB_SWITCH(argmax3_occupancy_t, dyn_lds)
+    return 0;
+}
+static void launch_argmax3(int KB, const CutParams &P, int nblocks, hipStream_t s) {
+    CUT_KB_SWITCH(launch_argmax3_t, P, nblocks, s)
 }
 
 static void launch_argmax(int KB, const CutParams &P, int nblocks, hipStream_t s) {
@@ -1376,6 +1697,11 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     // the chunk's k-rows: k element rows plus the vertex base row
     const int KB = kb_for((k + 1 + 3) & ~3);
     if (KB < 0) return fail(TWOSD_E_UNSUPPORTED, "k = %d random elements exceeds the cut kernel envelope (127)", k);
+    // the MFMA pass in fp32 (cut_argmax3_kernel, the element rows only: no base row) unless
+    // TWOSD_CUT_F32=0 (A/B and test knob, read per cut); a cut whose operands leave the fp32 range
+    // runs the fp64 pass anyway (decided on the device, cut_band_select_kernel)
+    const int KB32 = kb_for(k4);
+    const bool want32 = KB32 > 0 && (!getenv("TWOSD_CUT_F32") || atoi(getenv("TWOSD_CUT_F32")) != 0);
     int rc;
     if ((rc = update_pk(c))) return rc;
     // host: bvec = r - (T x) as the reference writes it (`coef.rhs - coef.transfer * x`,
@@ -1411,7 +1737,8 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     // |V| <= kHistLds case adds the LDS histogram, at most 2 KB)
     static const int bpc_env = getenv("TWOSD_CUT_BPC") ? atoi(getenv("TWOSD_CUT_BPC")) : 0;
     int bpc = bpc_env;
-    if (bpc <= 0) bpc = argmax_occupancy(KB, sizeof(unsigned long long) * kHistLds);
+    if (bpc <= 0)
+        bpc = want32 ? argmax3_occupancy(KB32, sizeof(unsigned long long) * kHistLds) : argmax_occupancy(KB, sizeof(unsigned long long) * kHistLds);
     if (bpc <= 0) bpc = 2;
     const int nchunks = (nv + kVT2 - 1) / kVT2;
     // The persistent grid runs whole tiles round after round; the tiles past the last full
@@ -1469,7 +1796,8 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
         if ((rc = realloc_dev(&w->tcand, tcand_need))) return rc;
         w->tcand_cap = tcand_need;
     }
-    if (!w->band_bits && (rc = realloc_dev(&w->band_bits, 1))) return rc;
+    // band_bits: [0] fp64 band, [1] fp32 band, [2] fp32 operands out of range, [3] the active band, [4] the pass
+    if (!w->band_bits && (rc = realloc_dev(&w->band_bits, 8))) return rc;
     if (!w->fstats && (rc = realloc_dev(&w->fstats, 16))) return rc;
     HIPCHK(hipMemsetAsync(w->fstats, 0, sizeof(unsigned long long) * 16, c->stream));
     // the epigraph's max |dv| per element, folded in for the rows added since the last cut
@@ -1500,17 +1828,19 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
         w->part_cap = slots * (k + 1);
     }
     HIPCHK(hipMemsetAsync(d_hist, 0, sizeof(unsigned long long) * std::max(nv, 1), c->stream));
-    HIPCHK(hipMemsetAsync(w->band_bits, 0, sizeof(unsigned long long), c->stream));
+    HIPCHK(hipMemsetAsync(w->band_bits, 0, sizeof(unsigned long long) * 8, c->stream));
     // band: the MFMA score and the restated one both add base[v] to a (k + 1)-term dot and differ
     // by at most 2 gamma_{k+4} (|base[v]| + sum_e |PK coef dv|) (one more rounding per T element
     // term, coef folded on the other side); twice that for safety
-    double band_scale;
+    double band_scale, band_scale32;
     {
-        const double u = ldexp(1.0, -53), nk = (double)(k + 4);
+        const double u = ldexp(1.0, -53), u32 = ldexp(1.0, -24), nk = (double)(k + 4);
         band_scale = 2.0 * 2.0 * (nk * u / (1.0 - nk * u));
+        band_scale32 = 2.0 * 2.0 * (nk * u32 / (1.0 - nk * u32));
     }
     hipLaunchKernelGGL(cut_vbase_kernel, dim3(std::max(1, std::min((nv + 3) / 4, 4096))), dim3(256), 0, c->stream, nv, m, k, k4,
-                       c->dvs.V, w->bvec, w->PK, w->coef, w->dmax[epi], w->base, w->band_bits, band_scale);
+                       c->dvs.V, w->bvec, w->PK, w->coef, w->dmax[epi], w->base, w->band_bits, band_scale, band_scale32);
+    hipLaunchKernelGGL(cut_band_select_kernel, dim3(1), dim3(64), 0, c->stream, w->band_bits, want32 ? 1 : 0);
     CutParams P{};
     P.band_scale = band_scale;
     P.N = N; P.k = k; P.k4 = k4; P.nv = nv; P.vcap = w->pk_vcap; P.m = m;
@@ -1522,7 +1852,8 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     }
     P.hist_part = w->hist_part;
     P.tie_rel = tie_rel; P.inv_total = 1.0 / total_weight;
-    P.band_bits = w->band_bits;
+    P.band_bits = w->band_bits + 3;
+    P.mode = w->band_bits + 4;
     P.cand = w->cand; P.tcand = w->tcand; P.eord = w->eord; P.fstats = w->fstats;
     P.dv = E.d_dv; P.w = E.d_w; P.coef = w->coef; P.PK = w->PK; P.PKT = w->PKT; P.PKO = w->PKO; P.base = w->base;
     {
@@ -1534,7 +1865,6 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
             if ((rc = realloc_dev(&w->PKTc, (size_t)rows * vcap32))) return rc;
             w->pktc_cap = (size_t)rows * vcap32;
         }
-        const size_t tot = (size_t)rows * vcap32;
         if ((size_t)nv > w->vmap_cap) {
             if ((rc = realloc_dev(&w->vmap, nv))) return rc;
             w->vmap_cap = nv;
@@ -1546,8 +1876,16 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
         }
         hipLaunchKernelGGL(cut_compact_kernel, dim3(1), dim3(1024), 0, c->stream, nv, w->base, twins ? w->tprev : nullptr, w->vmap,
                            w->nvc, w->fstats + 9);
-        hipLaunchKernelGGL(cut_pktc_kernel, dim3((unsigned)std::min<size_t>(4096, (tot + 255) / 256)), dim3(256), 0, c->stream, k,
-                           rows, w->pk_vcap, vcap32, w->PKT, w->coef, w->base, w->vmap, w->nvc, w->PKTc);
+        const int rows32 = want32 ? kr32(KB32) : 0;
+        if (want32 && (size_t)rows32 * vcap32 > w->pktc32_cap) {
+            if ((rc = realloc_dev(&w->PKTc32, (size_t)rows32 * vcap32))) return rc;
+            w->pktc32_cap = (size_t)rows32 * vcap32;
+        }
+        const size_t tot2 = (size_t)std::max(rows, rows32) * vcap32;
+        hipLaunchKernelGGL(cut_pktc_kernel, dim3((unsigned)std::min<size_t>(4096, (tot2 + 255) / 256)), dim3(256), 0, c->stream, k,
+                           rows, w->pk_vcap, vcap32, w->PKT, w->coef, w->base, w->vmap, w->nvc, w->PKTc, rows32,
+                           want32 ? w->PKTc32 : nullptr);
+        P.PKTc32 = w->PKTc32;
         hipLaunchKernelGGL(cut_compact_rows_kernel, dim3((unsigned)std::min<size_t>(2048, ((size_t)nv * k4 + 255) / 256)), dim3(256), 0,
                            c->stream, nv, k4, w->vmap, w->nvc, w->PKO, w->base, w->PKOc, w->basec);
         P.PKTc = w->PKTc;
@@ -1560,6 +1898,7 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     P.arg = w->arg; P.val = w->val; P.flag = w->flag; P.hist = d_hist; P.partial = w->partial;
     P.full_units = full; P.tail_S = S; P.fx_gs = fx_gs;
     P.tp_m = w->tp_m; P.tp_i = w->tp_i; P.tp_f = w->tp_f;
+    if (want32) launch_argmax3(KB32, P, nblocks, c->stream);   // each of the two returns at once unless its pass runs
     launch_argmax(KB, P, nblocks, c->stream);
     if (P.hist_lds)
         hipLaunchKernelGGL(cut_hist_reduce_kernel, dim3((nv + 255) / 256), dim3(256), 0, c->stream, nblocks, nv, w->hist_part,
@@ -1684,6 +2023,21 @@ extern "C" int twosd_cut_stats(twosd_ctx *c, int64_t *out) {
     if (getenv("TWOSD_FIX_STAMPS_PRINT"))
         fprintf(stderr, "fixup stamps (cycles summed over waves): rows/setup %llu deltas %llu list %llu chains %llu decide %llu sums %llu\n",
                 h[3], h[4], h[5], h[6], h[7], h[8]);
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_cut_pass(twosd_ctx *c, int *fp32, double *band) {
+    if (!c || !fp32) return fail(TWOSD_E_ARG, "cut_pass: NULL");
+    *fp32 = 0;
+    if (band) *band = 0.0;
+    CutWs *w = c->cut_ws ? (CutWs *)c->cut_ws : nullptr;
+    if (!w || !w->band_bits) return TWOSD_OK;
+    unsigned long long h[8] = {};
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpy(h, w->band_bits, sizeof(h), hipMemcpyDeviceToHost));
+    *fp32 = (int)h[4];
+    if (band) memcpy(band, &h[3], sizeof(double));
     return TWOSD_OK;
 }
 

@@ -211,6 +211,14 @@ class SDContext:
         check(self.lib.twosd_cut_stats(self.h, ptr(out)))
         return tuple(int(v) for v in out)
 
+    def cut_pass(self):
+        """(fp32, band) of the last cut: 1 if its MFMA pass ran in fp32, 0 for fp64, and that
+        pass's decision band (twosd_cut_pass)."""
+        f = C.c_int()
+        b = C.c_double()
+        check(self.lib.twosd_cut_pass(self.h, C.byref(f), C.byref(b)))
+        return f.value, b.value
+
     def training_cap(self, pivots_sum, scenarios) -> int:
         """The refresh's training pivot cap for a last large batch of `scenarios` solves with
         `pivots_sum` pivots (twosd_training_cap: the native rule, this context's setting)."""

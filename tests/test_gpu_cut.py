@@ -371,3 +371,64 @@ def test_cut_log_offset_guard_and_empty_epigraph_stats():
     c0 = twosd.build_sasa_cut(empty, x, V)
     assert c0.alpha == 0.0 and not c0.beta.any()
     assert ctx.cut_stats()[:3] == (0, 0, 0)
+
+
+@pytest.mark.parametrize("name,N", [("storm", 6000), ("ssn", 5000)])
+def test_cut_fp32_pass_equals_fp64_pass(name, N):
+    """The fp32 MFMA pass (default) and the fp64 one (TWOSD_CUT_F32=0) decide the same rows: both
+    give the C oracle's pick for every scenario under both tie rules; alpha / beta to 1e-8 of the
+    oracle.  storm at x_EV with V built there (twin-rich, many exact ties)."""
+    from oracle import cpu
+    from sqlp_amd import smps, twosd
+    inst = I.load(name)
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    x = I.x_ev(name)
+    ctx.compute_basis(x, smps.mean_values(inst["sto"]))
+    src = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(src, I.sample(name, 8192, 41))
+    _, st, _ = twosd.solve_push(src, x, 0, 8192)
+    assert (st == 0).all()
+    V = twosd.sdDualVertexSet(ctx)
+    vals = I.sample(name, N, 43)
+    w = np.random.default_rng(9).uniform(0.5, 1.5, size=N)
+    epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(epi, vals, w)
+    sp = inst["osp2"]
+    Vm = V.matrix()
+    for tie_rel in (0.0, 1e-12):
+        a, b, omv, oma = cpu.build_cut(sp.r, sp.T, x, Vm, ctx.rows, vals - sp.r[ctx.rows], w, tie_rel=tie_rel, nthreads=8)
+        got = {}
+        for f32 in ("1", "0"):
+            with _env("TWOSD_CUT_F32", f32):
+                cut, mv, ma = twosd._build_cut(epi, x, tie_rel, want_argmax=True)
+                got[f32] = (cut, ctx.cut_pass())
+            assert got[f32][1][0] == int(f32)
+            assert (ma == oma).all(), (f32, tie_rel, int((ma != oma).sum()))
+            np.testing.assert_allclose(mv, omv, rtol=1e-12, atol=1e-9)
+            assert cut.alpha == pytest.approx(a, rel=1e-8, abs=1e-8)
+            np.testing.assert_allclose(cut.beta, b, rtol=1e-8, atol=1e-8 * (1 + np.abs(b).max()))
+        assert got["1"][1][1] > got["0"][1][1] > 0.0          # the fp32 band is the wider one
+
+
+def test_cut_operands_past_fp32_envelope_run_the_fp64_pass():
+    """A vertex whose entries on the random rows are ~1e32 puts the fp32 operands' products past
+    the pass's envelope: the cut runs the fp64 pass (decided on the device) and still gives the
+    oracle's picks."""
+    from oracle import cpu
+    from sqlp_amd import twosd
+    ctx, x, V0 = _setup("ssn", 300)
+    Vm0 = V0.matrix()
+    big = Vm0[1].copy()
+    big[ctx.rows] *= 1e32
+    V0.push_batch(big[None, :])
+    Vm = V0.matrix()
+    N = 2000
+    vals = I.sample("ssn", N, 73)
+    epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(epi, vals)
+    sp = I.load("ssn")["osp2"]
+    cut, mv, ma = twosd._build_cut(epi, x, 0.0, want_argmax=True)
+    assert ctx.cut_pass()[0] == 0
+    a, b, omv, oma = cpu.build_cut(sp.r, sp.T, x, Vm, ctx.rows, vals - sp.r[ctx.rows], np.ones(N), tie_rel=0.0, nthreads=8)
+    assert (ma == oma).all(), int((ma != oma).sum())
+    assert cut.alpha == pytest.approx(a, rel=1e-8, abs=1e-8)
