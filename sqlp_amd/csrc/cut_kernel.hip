@@ -672,7 +672,7 @@ __host__ __device__ constexpr int kr32(int KB) { return 8 * ((KB + 1) / 2); }
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 #ifndef TWOSD_CUT3_BPC
-#define TWOSD_CUT3_BPC 2                 // blocks per CU the fp32 pass is compiled for
+#define TWOSD_CUT3_BPC 3                 // blocks per CU the fp32 pass is compiled for (2: storm cut 11.0 ms, ssn 4.7; 3: 10.6, 3.6)
 #endif
 
 template <int KB>
@@ -729,21 +729,53 @@ __global__ void __launch_bounds__(256, TWOSD_CUT3_BPC) cut_argmax3_kernel(CutPar
                                                  (__attribute__((address_space(3))) void *)&Bs[buf][i * 8 * kLdsRow3], 16, 0, 0);
             }
         };
-        stage(0, c_lo * kVT2);
-        __syncthreads();
-        for (int ch = c_lo; ch < c_hi; ++ch) {
-            const int buf = (ch - c_lo) & 1;
-            const int v0 = ch * kVT2;
-            if (ch + 1 < c_hi) stage(buf ^ 1, v0 + kVT2);
-            // the fp64 bases of this lane's 8 vertices (positions v0 + 4g + r, v0 + 16 + 4g + r;
-            // -inf past the argmax's vertices), in flight under the MFMAs
-            double bq[8];
+        // the fp64 bases of this lane's 8 vertices of a chunk (positions v0 + 4g + r, v0 + 16 + 4g + r;
+        // -inf past the argmax's vertices), loaded one chunk ahead of their use
+        auto load_bases = [&](double (&bq)[8], int v0) {
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
                 const int c = v0 + (r >> 2) * 16 + 4 * g + (r & 3);
                 const double b = P.basec[c < nvc ? c : 0];
                 bq[r] = c < nvc ? b : -INFINITY;
             }
+        };
+        // the chunk's 16 scores of this lane (base + MFMA), finished one chunk late: chunk ch's
+        // scores are tested and logged while chunk ch + 1's MFMAs run.  Most chunks raise no row's
+        // band floor and log nothing, so one wave-wide test (against the floors before the chunk:
+        // they only rise within it) skips the per-score steps
+        auto finish = [&](const f4 &q00, const f4 &q01, const f4 &q10, const f4 &q11, const double (&bb)[8], int vb) {
+            double sc0[8], sc1[8];
+            bool any = false;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                sc0[r] = bb[r] + (double)q00[r];
+                sc1[r] = bb[r] + (double)q01[r];
+                sc0[4 + r] = bb[4 + r] + (double)q10[r];
+                sc1[4 + r] = bb[4 + r] + (double)q11[r];
+            }
+#pragma unroll
+            for (int r = 0; r < 8; ++r) any |= (sc0[r] >= rb0.thr) | (sc1[r] >= rb1.thr);
+            if (__builtin_amdgcn_ballot_w64(any) != 0) {
+                // this lane's vertices in increasing order: vb + 4g + r, then vb + 16 + 4g + r
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    const int v = vb + (r >> 2) * 16 + 4 * g + (r & 3);
+                    row_fast<false>(rb0, sc0[r], v, rel, band, lbase, log0);
+                    row_fast<false>(rb1, sc1[r], v, rel, band, lbase, log0 + lstep);
+                }
+            }
+        };
+        f4 p00 = {0.0f, 0.0f, 0.0f, 0.0f}, p01 = p00, p10 = p00, p11 = p00;
+        double bp[8];
+        int pv0 = 0;
+        stage(0, c_lo * kVT2);
+        __syncthreads();
+        for (int ch = c_lo; ch < c_hi; ++ch) {
+            const int buf = (ch - c_lo) & 1;
+            const int v0 = ch * kVT2;
+            double bq[8];
+            load_bases(bq, v0);                     // in flight under the MFMAs
+            if (ch + 1 < c_hi) stage(buf ^ 1, v0 + kVT2);
             f4 c00 = {0.0f, 0.0f, 0.0f, 0.0f}, c01 = c00, c10 = c00, c11 = c00;
             constexpr int KG = TWOSD_CUT_KG;
 #pragma unroll
@@ -767,19 +799,14 @@ __global__ void __launch_bounds__(256, TWOSD_CUT3_BPC) cut_argmax3_kernel(CutPar
                 }
                 if (TWOSD_CUT_SB) __builtin_amdgcn_sched_barrier(0);
             }
-            // this lane's vertices in increasing order: v0 + 4g + r, then v0 + 16 + 4g + r
+            if (ch > c_lo) finish(p00, p01, p10, p11, bp, pv0);   // the previous chunk, under these MFMAs
+            p00 = c00; p01 = c01; p10 = c10; p11 = c11;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                row_fast<false>(rb0, bq[r] + (double)c00[r], v0 + 4 * g + r, rel, band, lbase, log0);
-                row_fast<false>(rb1, bq[r] + (double)c01[r], v0 + 4 * g + r, rel, band, lbase, log0 + lstep);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                row_fast<false>(rb0, bq[4 + r] + (double)c10[r], v0 + 16 + 4 * g + r, rel, band, lbase, log0);
-                row_fast<false>(rb1, bq[4 + r] + (double)c11[r], v0 + 16 + 4 * g + r, rel, band, lbase, log0 + lstep);
-            }
+            for (int r = 0; r < 8; ++r) bp[r] = bq[r];
+            pv0 = v0;
             __syncthreads();
         }
+        if (c_hi > c_lo) finish(p00, p01, p10, p11, bp, pv0);
         int pk0, pk1, nt0, nt1;
         combine_ex(rb0, rel, band, g, pk0, nt0);
         combine_ex(rb1, rel, band, g, pk1, nt1);
