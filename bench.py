@@ -39,6 +39,7 @@ sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_FP64_TFS = 78.6         # MI355X fp64 (vector == matrix on gfx950), spec
+PEAK_F32_MFMA_TFS = 157.3    # MI355X fp32-input MFMA (v_mfma_f32_16x16x4_f32), spec (MI355X_MICROARCH.md)
 CHUNK = 1 << 16
 
 
@@ -463,7 +464,10 @@ def main():
     flops_alg = 2 * n_local * nv * k + 2 * nv * m
     cut_us = t_cut / passes
     cut_gbs = bytes_alg / (cut_us * 1e-6) / 1e9
-    t_roof = max(bytes_alg / (PEAK_HBM_GBS * 1e9), flops_alg / (PEAK_FP64_TFS * 1e12))
+    # the cut's MFMA pass (fp32 by default; fp64 with TWOSD_CUT_F32=0 or out-of-envelope operands)
+    cut_fp32, cut_band = ctx.cut_pass()
+    peak_cut = PEAK_F32_MFMA_TFS if cut_fp32 else PEAK_FP64_TFS
+    t_roof = max(bytes_alg / (PEAK_HBM_GBS * 1e9), flops_alg / (peak_cut * 1e12))
     xnorm = float(np.linalg.norm(xs[0]))
     x_points = [{"x": ("EV (pool training point)" if it == 0 else f"SD candidate, iteration {it}"),
                  "rel_dist_from_ev": float(np.linalg.norm(xx - xs[0]) / xnorm),
@@ -528,11 +532,14 @@ def main():
                      # the main launch's eta-arena stores (row index + value per entry): the algorithmic
                      # part of its HBM writes, next to the PMC WRITE_SIZE of the same launch
                      "eta_write_bytes_per_launch": 12.0 * acc["eta"] / passes},
-        "cutgen": {"kernel": "cut_argmax2_kernel (+pktc/vbase/fixup/reduce)", "hbm_gbs": cut_gbs,
+        "cutgen": {"kernel": ("cut_argmax3_kernel (fp32 MFMA pass)" if cut_fp32 else "cut_argmax2_kernel (fp64 MFMA pass)") +
+                             " + vbase/pktc/fixup/merge/reduce",
+                   "mfma_pass": "fp32" if cut_fp32 else "fp64", "decision_band": cut_band,
+                   "peak_tflops": peak_cut, "hbm_gbs": cut_gbs,
                    "bytes_alg": bytes_alg, "flops_alg": flops_alg, "t_roof_ms": t_roof * 1e3,
                    "t_ms": cut_us / 1e3, "frac": t_roof / (cut_us * 1e-6),
                    "mfma_tflops": flops_alg / (cut_us * 1e-6) / 1e12,
-                   "bound": "mfma" if flops_alg / (PEAK_FP64_TFS * 1e12) > bytes_alg / (PEAK_HBM_GBS * 1e9) else "hbm"},
+                   "bound": "mfma" if flops_alg / (peak_cut * 1e12) > bytes_alg / (PEAK_HBM_GBS * 1e9) else "hbm"},
     }
 
     # HBM traffic and MFMA counters of the dominant kernels from the committed rocprofv3 PMC
@@ -543,13 +550,13 @@ def main():
         if kl:
             out["roofline"]["traffic"] = kl["hbm_bytes_per_launch"]
             out["roofline"]["traffic_source"] = pmc["file"]
-        kc = pmc["kernels"].get("cut_argmax2_kernel") or pmc["kernels"].get("cut_argmax_kernel")
+        kc = pmc["kernels"].get("cut_argmax3_kernel" if cut_fp32 else "cut_argmax2_kernel")
         if kc:
             out["cutgen"]["traffic"] = kc["hbm_bytes_per_launch"]
             if "hbm_bytes_per_launch_raw" in kc:
                 out["cutgen"]["traffic_raw"] = kc["hbm_bytes_per_launch_raw"]
             if "mfma_util" in kc:
-                out["cutgen"]["mfma_util"] = kc["mfma_util"]            # counted MFMA flops / time / 78.6 TF
+                out["cutgen"]["mfma_util"] = kc["mfma_util"]            # counted MFMA flops / time / the pass's peak
                 out["cutgen"]["mfma_busy_frac"] = kc.get("mfma_busy_frac")   # SQ_VALU_MFMA_BUSY_CYCLES / SIMD cycles
             out["cutgen"]["traffic_source"] = pmc["file"]
     if rank == 0 and world == 1 and args.spot > 0:

@@ -124,6 +124,10 @@ __global__ __launch_bounds__(kFtThreads) void pg_ftran_kernel(PgArgs A) {
     for (int t = tid; t < S.K; t += kFtThreads) etap[t] = S.etap[t];
     for (int t = tid; t <= S.K; t += kFtThreads) etaoff[t] = S.K > 0 ? S.etaoff[t] : 0;
     mark_touched<kFtThreads>(A, S, touched);
+    // bit 2: the etas' pivot rows (each is also one of its eta's rows, so already marked 1; two etas
+    // on one row both write 3)
+    for (int t = tid; t < S.K; t += kFtThreads) touched[S.etap[t]] = 3;
+    __syncthreads();
     double drop = 0.0;
     int *nzc = A.nzc + (size_t)a * m;
     if (PASS == 1) {
@@ -136,6 +140,54 @@ __global__ __launch_bounds__(kFtThreads) void pg_ftran_kernel(PgArgs A) {
     double amax = 0.0;
     int nzsum = 0;   // PASS 0, lane 0: nonzeros of this wave's columns
     for (int c = wv; c < m; c += kFtWaves) {
+        // a column of B_pb^{-1} with no entry in any eta's pivot row passes every eta unchanged (each
+        // E_t acts only when x at its pivot row is nonzero, and none of them writes it): its entries,
+        // rows ascending, are the FTRAN's result as they stand -- the same values and order the dense
+        // walk below produces, without it.  (storm: ~6 entries a column against ~8 pivot rows, so
+        // most columns; one wave step of up to 64 entries, checked ascending)
+        {
+            const int q0 = cp[c], q1 = cp[c + 1];
+            if (q1 - q0 <= 64) {
+                const int q = q0 + lane;
+                const bool has = q < q1;
+                const int i = has ? A.bci0[q] : 0x7fffffff;
+                const double v = has ? A.bcv0[q] : 0.0;
+                const int inext = __shfl_down(i, 1);
+                const bool bad = has && (((touched[i] & 2) != 0) || (lane < 63 && q + 1 < q1 && inext <= i));
+                if (__ballot(bad) == 0) {
+                    amax = fmax(amax, fabs(v));
+                    const bool nz = has && v != 0.0;
+                    const unsigned long long msk = __ballot(nz);
+                    const int cnt = __popcll(msk);
+                    if (PASS == 0) {
+                        if (lane == 0) nzc[c] = cnt;
+                        nzsum += cnt;
+                        if (A.sc_cap > 0) {
+                            int off = 0;
+                            if (lane == 0) off = atomicAdd(&sc_ctr, cnt);
+                            off = __shfl(off, 0);
+                            if ((long long)off + cnt <= A.sc_cap && nz) {
+                                const size_t at = (size_t)a * A.sc_cap + off + __popcll(msk & lanemask_lt(lane));
+                                A.sc_row[at] = i;
+                                A.sc_val[at] = v;
+                            }
+                            if (lane == 0) A.sc_off[(size_t)a * m + c] = off;
+                        }
+                    } else {
+                        const bool kk = has && (touched[i] ? fabs(v) > drop : v != 0.0);
+                        const unsigned long long km = __ballot(kk);
+                        if (kk) {
+                            const size_t at = (size_t)A.inter_off[a] + cstart[c] + __popcll(km & lanemask_lt(lane));
+                            A.inter_row[at] = i;
+                            A.inter_val[at] = v;
+                        }
+                        if (lane == 0) A.keptc[(size_t)a * m + c] = __popcll(km);
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    continue;
+                }
+            }
+        }
         for (int i = lane; i < m; i += 64) x[i] = 0.0;
         __builtin_amdgcn_wave_barrier();
         for (int q = cp[c] + lane; q < cp[c + 1]; q += 64) {

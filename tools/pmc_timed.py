@@ -28,8 +28,8 @@ from collections import defaultdict
 
 import numpy as np
 
-KERNELS = ["lp_hyper_kernel", "pool_refine_kernel", "pool_select_kernel", "cut_argmax2_kernel", "cut_fixup_kernel",
-           "pg_ftran_kernel", "pg_fill_kernel"]
+KERNELS = ["lp_hyper_kernel", "pool_refine_kernel", "pool_select_kernel", "cut_argmax3_kernel", "cut_argmax2_kernel",
+           "cut_fixup_kernel", "pg_ftran_kernel", "pg_fill_kernel"]
 
 
 def short(name):
@@ -65,6 +65,8 @@ def timed_steps(disp, K):
     """per timed step: {kernel: the dispatch (largest FETCH/any counter; by duration in a trace) of
     that kernel in the step}"""
     ids = sorted(disp)
+    # one cut per sub-step: its argmax launch (the fp32 pass, or the fp64 one; a cut launches both
+    # and the idle one returns at once, so the step boundary is the fp64 kernel, launched last)
     cuts = [i for i in ids if "cut_argmax2_kernel" in disp[i]["name"]]
     if len(cuts) < K + 1:
         return []
@@ -213,16 +215,20 @@ def main():
         e = {"duration_ms": ms, "FETCH_SIZE_KiB": f_kib, "WRITE_SIZE_KiB": w_kib,
              "hbm_bytes_per_launch": 1024.0 * (2 * f_kib + w_kib), "hbm_bytes_per_launch_raw": 1024.0 * (f_kib + w_kib),
              "scratch_bytes_per_lane": ent["meta"].get("scratch_bytes_per_lane")}
-        for cn in ("SQ_INSTS_VALU_MFMA_MOPS_F64", "SQ_INSTS_VALU_MFMA_F64", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES",
+        for cn in ("SQ_INSTS_VALU_MFMA_MOPS_F64", "SQ_INSTS_VALU_MFMA_F64", "SQ_INSTS_VALU_MFMA_MOPS_F32", "SQ_INSTS_VALU_MFMA_F32",
+                   "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES",
                    "GRBM_GUI_ACTIVE", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
                    "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA"):
             if cn in m:
                 e[cn] = m[cn]
-        if ms and m.get("SQ_INSTS_VALU_MFMA_MOPS_F64"):
-            fl = 512.0 * m["SQ_INSTS_VALU_MFMA_MOPS_F64"]
-            e["mfma_f64_flops"] = fl
-            e["mfma_f64_tflops_counted"] = fl / (ms * 1e-3) / 1e12
-            e["mfma_util"] = e["mfma_f64_tflops_counted"] / 78.6
+        f32 = bool(m.get("SQ_INSTS_VALU_MFMA_MOPS_F32"))
+        mops = m.get("SQ_INSTS_VALU_MFMA_MOPS_F32") if f32 else m.get("SQ_INSTS_VALU_MFMA_MOPS_F64")
+        if ms and mops:
+            fl = 512.0 * mops
+            tag = "f32" if f32 else "f64"
+            e[f"mfma_{tag}_flops"] = fl
+            e[f"mfma_{tag}_tflops_counted"] = fl / (ms * 1e-3) / 1e12
+            e["mfma_util"] = e[f"mfma_{tag}_tflops_counted"] / (157.3 if f32 else 78.6)
             if m.get("GRBM_GUI_ACTIVE"):
                 e["mfma_busy_frac"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["GRBM_GUI_ACTIVE"] / 8.0 * 1024.0)
         summ["kernels"][k] = e
