@@ -678,6 +678,9 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 template <int KB>
 __global__ void __launch_bounds__(256, TWOSD_CUT3_BPC) cut_argmax3_kernel(CutParams P) {
     if (*P.mode != 1) return;                       // the fp64 pass runs this cut (cut_argmax2_kernel)
+    // a register for the logs' first entries at 2 blocks per CU (as cut_argmax2_kernel); at 3 the
+    // entries are stored at once
+    constexpr bool kHold3 = TWOSD_CUT3_BPC <= 2;
     constexpr int KR = kr32(KB);
     __shared__ float Bs[2][KR * kLdsRow3];          // double-buffered chunk (k-major)
     extern __shared__ unsigned long long hl[];      // nv entries when P.hist_lds
@@ -760,8 +763,8 @@ __global__ void __launch_bounds__(256, TWOSD_CUT3_BPC) cut_argmax3_kernel(CutPar
 #pragma unroll
                 for (int r = 0; r < 8; ++r) {
                     const int v = vb + (r >> 2) * 16 + 4 * g + (r & 3);
-                    row_fast<false>(rb0, sc0[r], v, rel, band, lbase, log0);
-                    row_fast<false>(rb1, sc1[r], v, rel, band, lbase, log0 + lstep);
+                    row_fast<kHold3>(rb0, sc0[r], v, rel, band, lbase, log0);
+                    row_fast<kHold3>(rb1, sc1[r], v, rel, band, lbase, log0 + lstep);
                 }
             }
         };
@@ -810,6 +813,8 @@ __global__ void __launch_bounds__(256, TWOSD_CUT3_BPC) cut_argmax3_kernel(CutPar
         int pk0, pk1, nt0, nt1;
         combine_ex(rb0, rel, band, g, pk0, nt0);
         combine_ex(rb1, rel, band, g, pk1, nt1);
+        if (kHold3 && rb0.n > 0 && (tail || nt0 >= 2)) lbase[log0] = rb0.f;
+        if (kHold3 && rb1.n > 0 && (tail || nt1 >= 2)) lbase[log0 + lstep] = rb1.f;
         rb0.I = rb0.I >= 0 ? P.vmap[rb0.I] : -1;
         rb1.I = rb1.I >= 0 ? P.vmap[rb1.I] : -1;
         if (tail) {
@@ -836,25 +841,35 @@ __global__ void __launch_bounds__(256, TWOSD_CUT3_BPC) cut_argmax3_kernel(CutPar
         auto fin = [&](int sx, bool ok, int ai, double pp) -> double {
             const double *pk = P.PK + (size_t)(ai >= 0 ? ai : 0) * P.k4;
             const double pu = ok ? pp : 0.0;
-            double d64[KB];
+            // k-blocks in groups of 6 (their loads in flight together): the S_e terms (v2's xor
+            // tree) and dec_lane_chain's chain c_g, in the same order and arithmetic
+            constexpr int FG = 6;
+            double cg = 0.0;
 #pragma unroll
-            for (int kb = 0; kb < KB; ++kb) {
-                const int e = 4 * kb + g;
-                d64[kb] = (sx < P.N && e < P.k) ? P.dv[(size_t)sx * P.k + e] : 0.0;
-            }
+            for (int k0 = 0; k0 < KB; k0 += FG) {
+                double d64[FG], pke[FG];
 #pragma unroll
-            for (int kb = 0; kb < KB; ++kb) {
-                const int e = 4 * kb + g;
-                const double pke = e < P.k ? pk[e] : 0.0;
-                double v = (e < P.k) ? pu * pke * d64[kb] : 0.0;
+                for (int u = 0; u < FG; ++u) {
+                    const int e = 4 * (k0 + u) + g;
+                    const bool in = k0 + u < KB && e < P.k;
+                    d64[u] = (in && sx < P.N) ? P.dv[(size_t)sx * P.k + e] : 0.0;
+                    pke[u] = in ? pk[e] : 0.0;
+                }
 #pragma unroll
-                for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o);
-                if (j == (kb & 15)) {
-                    if (kb < 16) Sacc[0] += v;
-                    else Sacc[1] += v;
+                for (int u = 0; u < FG; ++u) {
+                    const int kb = k0 + u, e = 4 * kb + g;
+                    if (kb >= KB) break;
+                    if (e < P.k) cg = fma(pke[u] * P.coef[e], d64[u], cg);
+                    double v = (e < P.k) ? pu * pke[u] * d64[u] : 0.0;
+#pragma unroll
+                    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o);
+                    if (j == (kb & 15)) {
+                        if (kb < 16) Sacc[0] += v;
+                        else Sacc[1] += v;
+                    }
                 }
             }
-            return dec_combine(dec_lane_chain<KB>(P, pk, d64, g));
+            return dec_combine(cg);
         };
         const double tv0 = fin(sa, ok0, rb0.I, p0);
         const double tv1 = fin(sb, ok1, rb1.I, p1);

@@ -194,7 +194,10 @@ def main():
             for k, d in st.items():
                 dur[k].append(d["ms"])
     out["trace_ms"] = {k: float(np.mean(v)) for k, v in dur.items()}
-    with open(os.path.join(dst, "pmc_timed.json"), "w") as f:
+    kk = key or {"instance": "storm", "scenarios": 1_000_000, "vertices": 4096, "epigraphs": 1}
+    is_default = (kk["instance"], kk["scenarios"], kk["vertices"], kk["epigraphs"]) == ("storm", 1_000_000, 4096, 1)
+    suffix = "" if is_default else f"_{kk['instance']}_{kk['scenarios']}_V{kk['vertices']}_E{kk['epigraphs']}"
+    with open(os.path.join(dst, f"pmc_timed{suffix}.json"), "w") as f:
         json.dump(out, f, indent=1)
     # the summary bench.py reads (latest profiles/r*/pmc_summary.json): per kernel, the mean over
     # the timed launches of the driver's protocol
@@ -234,14 +237,8 @@ def main():
         summ["kernels"][k] = e
     if "lp_write_split" in out:
         summ["lp_write_split"] = out["lp_write_split"]["fit"]
-    k_ = summ["key"]
-    default = (k_["instance"], k_["scenarios"], k_["vertices"], k_["epigraphs"]) == ("storm", 1_000_000, 4096, 1)
-    name = "pmc_summary.json" if default else \
-        f"pmc_summary_{k_['instance']}_{k_['scenarios']}_V{k_['vertices']}_E{k_['epigraphs']}.json"
-    with open(os.path.join(dst, name), "w") as f:
+    with open(os.path.join(dst, f"pmc_summary{suffix}.json"), "w") as f:
         json.dump(summ, f, indent=1)
-    if not default:
-        os.replace(os.path.join(dst, "pmc_timed.json"), os.path.join(dst, name.replace("pmc_summary", "pmc_timed")))
     print(json.dumps({k: v["mean"] for k, v in out["kernels"].items()}, indent=1))
     if "lp_write_split" in out:
         print(json.dumps(out["lp_write_split"], indent=1))
