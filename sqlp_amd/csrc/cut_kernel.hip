@@ -74,11 +74,12 @@ struct CutParams {
     const int *vmap;       // the argmax's vertices (dominated twins left out), ascending: column c of PKTc is vertex vmap[c]
     const int *nvc;        // their count (device: set per x by cut_compact_kernel)
     const double *PKOc;    // PKO rows of the argmax's vertices (row c: vertex vmap[c]), per x
-    const double *basec;   // base of the argmax's vertices, per x
+    const double *basec;   // base of the argmax's vertices, per x (vcap32 entries; past nvc unused)
     const double *base;    // nv: pi_v . bvec in index order (the restatement's base dot)
     const int *eord;       // k: elements by ascending row (the restated score's order)
     const unsigned long long *band_bits;   // the ACTIVE band of this cut, as bits (cut_band_select_kernel)
     const unsigned long long *mode;        // 1: this cut's MFMA pass runs in fp32 (cut_argmax3_kernel), 0: fp64 (cut_argmax2_kernel)
+    const float *basec32;  // vcap32: basec rounded up to fp32 (-inf past nvc): the fp32 pass's prefilter
     const float *PKTc32;   // KR32 x vcap32: PKTc's element rows rounded to fp32, no base row (cut_argmax3_kernel's LDS-DMA source)
     double band_scale;     // 4 gamma_{k+4}: twice the 2 gamma bound
     int *arg; double *val; int *flag;   // N; flag != 0: re-decide (main rows: 4-bit log counts per lane group)
@@ -222,8 +223,13 @@ __global__ void cut_twin_sorted_kernel(int nv, int k4, const double *__restrict_
 // positions (its logs hold them), so its candidate loads need no translation
 __global__ void cut_compact_rows_kernel(int nv, int k4, const int *__restrict__ vmap, const int *__restrict__ nvc_p,
                                         const double *__restrict__ PKO, const double *__restrict__ base,
-                                        double *__restrict__ PKOc, double *__restrict__ basec) {
+                                        double *__restrict__ PKOc, double *__restrict__ basec, int vcap32, float *__restrict__ basec32) {
     const int nvc = *nvc_p;
+    // basec32[c] = the least float >= base[vmap[c]] (-inf past nvc): an upper bound of the base, so
+    // the fp32 prefilter of cut_argmax3_kernel never rejects a score the fp64 test would accept
+    if (basec32)
+        for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < vcap32; c += gridDim.x * blockDim.x)
+            basec32[c] = c < nvc ? __double2float_ru(base[vmap[c]]) : -INFINITY;
     const size_t total = (size_t)nv * k4;
     for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
         const int c = (int)(idx / k4), q = (int)(idx % k4);
@@ -355,7 +361,19 @@ __device__ __forceinline__ double band_floor(double M, double rel, double band) 
 // this lane's candidate log (kCandC + 1: overflowed), f = its first entry.  The first entry
 // stays in a register and is stored (log[0]) only for a row the fixup will read: most rows
 // just raise their maximum past the band again and again, and each raise restarts the log.
-struct RowEx { double M, thr; int I, n, f; };
+struct RowEx { double M, thr; int I, n, f; float thr32; };
+
+// the fp32 prefilter's floor of a row (cut_argmax3_kernel): a float at or below fl32(y) for every
+// y >= pred64(thr).  A score s = fl64(base + t) >= thr has base + t >= pred64(thr); with b32 >= base
+// (rounded up) and fp32 addition monotone, fl32(b32 + t) >= fl32(pred64(thr)) >= this floor.
+// f = RN32(thr) is within one float step of RD32(pred64(thr)); f - |f| 2^-21 (rounded) lies at least
+// three float steps lower, and the 2^-140 covers the subnormal range.  -inf stays -inf; past FLT_MAX
+// the floor is FLT_MAX (every y there rounds to +inf)
+__device__ __forceinline__ float thr32_of(double thr) {
+    const float f = (float)thr;
+    if (f == INFINITY) return 3.40282347e38f;
+    return fmaf(-fabsf(f), 0x1p-21f, f) - 0x1p-140f;
+}
 
 // s >= thr: s enters the band of the running max (or raises it).  HOLD: the first entry is kept
 // in b.f (stored at the end of the tile for the rows the fixup reads); otherwise it is stored at
@@ -376,7 +394,7 @@ __device__ __forceinline__ void row_log(RowEx &b, double s, int v, double rel, d
         else if (b.n < kCandC) lbase[lo + b.n] = v;
         b.n = min(b.n + 1, kCandC + 1);
     }
-    if (s > b.M) { b.M = s; b.I = v; b.thr = tn; }
+    if (s > b.M) { b.M = s; b.I = v; b.thr = tn; b.thr32 = thr32_of(tn); }
 }
 
 template <bool HOLD>
@@ -492,7 +510,7 @@ __global__ void __launch_bounds__(256, (TWOSD_CUT_LB3 && KB <= 22) ? 3 : 2) cut_
             if (e == P.k) a0[kb] = a1[kb] = 1.0;   // x the base row of the chunk
         }
         RowEx rb0, rb1;   // scenario s0 + j / s0 + 16 + j over this lane's vertices v0 + g + 4r (+16)
-        rb0.M = -INFINITY; rb0.thr = -INFINITY; rb0.I = -1; rb0.n = 0; rb0.f = 0;
+        rb0.M = -INFINITY; rb0.thr = -INFINITY; rb0.I = -1; rb0.n = 0; rb0.f = 0; rb0.thr32 = -INFINITY;
         rb1 = rb0;
         // this lane's candidate logs of the two scenarios (rows padded to whole tiles)
         // (a wave-uniform base and a 32-bit element offset: one VGPR per lane instead of a pointer pair)
@@ -678,11 +696,15 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 template <int KB>
 __global__ void __launch_bounds__(256, TWOSD_CUT3_BPC) cut_argmax3_kernel(CutParams P) {
     if (*P.mode != 1) return;                       // the fp64 pass runs this cut (cut_argmax2_kernel)
-    // a register for the logs' first entries at 2 blocks per CU (as cut_argmax2_kernel); at 3 the
-    // entries are stored at once
-    constexpr bool kHold3 = TWOSD_CUT3_BPC <= 2;
+    // the logs' first entries held in a register (as cut_argmax2_kernel at 2 blocks per CU): most
+    // candidate steps restart a log, and a held entry is stored only for the rows the fixup reads
+#ifndef TWOSD_CUT3_HOLD
+#define TWOSD_CUT3_HOLD 1                // first log entries in a register (storm argmax 8.28 -> 8.14 ms at 3 blocks per CU)
+#endif
+    constexpr bool kHold3 = TWOSD_CUT3_HOLD;
     constexpr int KR = kr32(KB);
     __shared__ float Bs[2][KR * kLdsRow3];          // double-buffered chunk (k-major)
+    __shared__ double Bb[3][kVT2];                  // the chunks' fp64 bases (ring of 3: finish reads chunk ch - 1)
     extern __shared__ unsigned long long hl[];      // nv entries when P.hist_lds
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -697,6 +719,9 @@ __global__ void __launch_bounds__(256, TWOSD_CUT3_BPC) cut_argmax3_kernel(CutPar
     const double rel = P.tie_rel;
     double pv_sum = 0.0;
     double Sacc[2] = {0.0, 0.0};   // lane (g, j): e = 4 kb + g for kb = j, j + 16
+#ifdef TWOSD_CUT3_COUNT
+    unsigned long long cnt_steps = 0, cnt_rare = 0, cnt_lanes = 0;
+#endif
 
     for (int unit = blockIdx.x; unit < nunits; unit += gridDim.x) {
         const bool tail = unit >= P.full_units;
@@ -714,7 +739,7 @@ __global__ void __launch_bounds__(256, TWOSD_CUT3_BPC) cut_argmax3_kernel(CutPar
             a1[kb] = (sb < P.N && e < P.k) ? (float)P.dv[(size_t)sb * P.k + e] : 0.0f;
         }
         RowEx rb0, rb1;
-        rb0.M = -INFINITY; rb0.thr = -INFINITY; rb0.I = -1; rb0.n = 0; rb0.f = 0;
+        rb0.M = -INFINITY; rb0.thr = -INFINITY; rb0.I = -1; rb0.n = 0; rb0.f = 0; rb0.thr32 = -INFINITY;
         rb1 = rb0;
         int *const lbase = tail ? P.tcand : P.cand;
         const unsigned log0 = tail ? (unsigned)(((((size_t)(s0 + j - P.full_units * kCutTile2)) * P.tail_S + range) * 4 + g) * kCandC)
@@ -724,61 +749,75 @@ __global__ void __launch_bounds__(256, TWOSD_CUT3_BPC) cut_argmax3_kernel(CutPar
         // LDS-DMA staging (global_load_lds_dwordx4): instruction i writes k-rows 8i .. 8i+7 (1 KiB,
         // lane-linear), lane L the 4 floats at LDS position 4 (L % 8) of row 8i + L/8; the source
         // vertices are that position with lds3's half swap applied
-        auto stage = [&](int buf, int v0) {
+        auto stage = [&](int buf, int bslot, int v0) {
             for (int i = wid; i < KR / 8; i += 4) {
                 const int kk = 8 * i + (lane >> 3);
                 const int vv = (4 * (lane & 7)) ^ (((kk >> 1) & 1) << 4);
                 __builtin_amdgcn_global_load_lds((const void *)(P.PKTc32 + (size_t)kk * P.vcap32 + v0 + vv),
                                                  (__attribute__((address_space(3))) void *)&Bs[buf][i * 8 * kLdsRow3], 16, 0, 0);
             }
+            // the 32 fp64 bases (256 bytes: lanes 0..15 of the last wave, 16 bytes each)
+            if (wid == 3 && lane < 16)
+                __builtin_amdgcn_global_load_lds((const void *)(P.basec + v0 + 2 * lane),
+                                                 (__attribute__((address_space(3))) void *)&Bb[bslot][0], 16, 0, 0);
         };
-        // the fp64 bases of this lane's 8 vertices of a chunk (positions v0 + 4g + r, v0 + 16 + 4g + r;
-        // -inf past the argmax's vertices), loaded one chunk ahead of their use
-        auto load_bases = [&](double (&bq)[8], int v0) {
+        // this lane's 8 vertices of a chunk (positions v0 + 4g + r, v0 + 16 + 4g + r) as prefilter
+        // bases (basec32: rounded up, -inf past the argmax's vertices), two 16-byte loads issued one
+        // chunk ahead of their use
+        auto load_bases = [&](float (&bq)[8], int v0) {
+            const f4 lo = *reinterpret_cast<const f4 *>(P.basec32 + v0 + 4 * g);
+            const f4 hi = *reinterpret_cast<const f4 *>(P.basec32 + v0 + 16 + 4 * g);
 #pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                const int c = v0 + (r >> 2) * 16 + 4 * g + (r & 3);
-                const double b = P.basec[c < nvc ? c : 0];
-                bq[r] = c < nvc ? b : -INFINITY;
-            }
+            for (int r = 0; r < 4; ++r) { bq[r] = lo[r]; bq[4 + r] = hi[r]; }
         };
-        // the chunk's 16 scores of this lane (base + MFMA), finished one chunk late: chunk ch's
-        // scores are tested and logged while chunk ch + 1's MFMAs run.  Most chunks raise no row's
-        // band floor and log nothing, so one wave-wide test (against the floors before the chunk:
-        // they only rise within it) skips the per-score steps
-        auto finish = [&](const f4 &q00, const f4 &q01, const f4 &q10, const f4 &q11, const double (&bb)[8], int vb) {
-            double sc0[8], sc1[8];
-            bool any = false;
+        // the chunk's 16 scores of this lane, finished one chunk late (under chunk ch + 1's MFMAs).
+        // Prefilter in fp32: b32 + t >= thr32 for every score the fp64 test (base + t >= thr, t the
+        // MFMA's fp32 value) accepts (thr32_of); most chunks raise no row's band floor, so one
+        // wave-wide test skips the rest.  A lane past it re-scores its 8 vertices exactly (fp64
+        // bases) and runs the decisions in vertex order
+        auto finish = [&](const f4 &q00, const f4 &q01, const f4 &q10, const f4 &q11, const float (&bb)[8], int vb, int bslot) {
+            // per row, the bit mask of this lane's vertices (r = 0..7, increasing vertex order) past
+            // the prefilter
+            unsigned m0 = 0, m1 = 0;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                sc0[r] = bb[r] + (double)q00[r];
-                sc1[r] = bb[r] + (double)q01[r];
-                sc0[4 + r] = bb[4 + r] + (double)q10[r];
-                sc1[4 + r] = bb[4 + r] + (double)q11[r];
+                m0 |= (unsigned)(bb[r] + q00[r] >= rb0.thr32) << r;
+                m1 |= (unsigned)(bb[r] + q01[r] >= rb1.thr32) << r;
+                m0 |= (unsigned)(bb[4 + r] + q10[r] >= rb0.thr32) << (4 + r);
+                m1 |= (unsigned)(bb[4 + r] + q11[r] >= rb1.thr32) << (4 + r);
             }
-#pragma unroll
-            for (int r = 0; r < 8; ++r) any |= (sc0[r] >= rb0.thr) | (sc1[r] >= rb1.thr);
-            if (__builtin_amdgcn_ballot_w64(any) != 0) {
-                // this lane's vertices in increasing order: vb + 4g + r, then vb + 16 + 4g + r
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    const int v = vb + (r >> 2) * 16 + 4 * g + (r & 3);
-                    row_fast<kHold3>(rb0, sc0[r], v, rel, band, lbase, log0);
-                    row_fast<kHold3>(rb1, sc1[r], v, rel, band, lbase, log0 + lstep);
-                }
+#ifdef TWOSD_CUT3_COUNT
+            ++cnt_steps;
+            if (__builtin_amdgcn_ballot_w64((m0 | m1) != 0) != 0) { ++cnt_rare; cnt_lanes += __popcll(__builtin_amdgcn_ballot_w64((m0 | m1) != 0)); }
+#endif
+            // the exact steps, one passing vertex per row and lane per round (lowest first: each
+            // row still sees its vertices in increasing order), the fp64 base from the chunk's LDS slot
+            while (__builtin_amdgcn_ballot_w64((m0 | m1) != 0) != 0) {
+                const int r0 = m0 ? __builtin_ctz(m0) : 0, r1 = m1 ? __builtin_ctz(m1) : 0;
+                const int o0 = (r0 >> 2) * 16 + 4 * g + (r0 & 3), o1 = (r1 >> 2) * 16 + 4 * g + (r1 & 3);
+                const double b0 = Bb[bslot][o0], b1 = Bb[bslot][o1];
+                const float t0 = r0 < 4 ? q00[r0 & 3] : q10[r0 & 3];
+                const float t1 = r1 < 4 ? q01[r1 & 3] : q11[r1 & 3];
+                const double s0 = (vb + o0 < nvc ? b0 : -INFINITY) + (double)t0;
+                const double s1 = (vb + o1 < nvc ? b1 : -INFINITY) + (double)t1;
+                if (m0) row_fast<kHold3>(rb0, s0, vb + o0, rel, band, lbase, log0);
+                if (m1) row_fast<kHold3>(rb1, s1, vb + o1, rel, band, lbase, log0 + lstep);
+                m0 &= m0 - 1;
+                m1 &= m1 - 1;
             }
         };
         f4 p00 = {0.0f, 0.0f, 0.0f, 0.0f}, p01 = p00, p10 = p00, p11 = p00;
-        double bp[8];
+        float bp[8];
         int pv0 = 0;
-        stage(0, c_lo * kVT2);
+        stage(0, 0, c_lo * kVT2);
         __syncthreads();
+        int bs = 0, bsp = 0;   // base ring slots of chunks ch and ch - 1
         for (int ch = c_lo; ch < c_hi; ++ch) {
             const int buf = (ch - c_lo) & 1;
             const int v0 = ch * kVT2;
-            double bq[8];
+            float bq[8];
             load_bases(bq, v0);                     // in flight under the MFMAs
-            if (ch + 1 < c_hi) stage(buf ^ 1, v0 + kVT2);
+            if (ch + 1 < c_hi) stage(buf ^ 1, bs == 2 ? 0 : bs + 1, v0 + kVT2);
             f4 c00 = {0.0f, 0.0f, 0.0f, 0.0f}, c01 = c00, c10 = c00, c11 = c00;
             constexpr int KG = TWOSD_CUT_KG;
 #pragma unroll
@@ -802,14 +841,16 @@ __global__ void __launch_bounds__(256, TWOSD_CUT3_BPC) cut_argmax3_kernel(CutPar
                 }
                 if (TWOSD_CUT_SB) __builtin_amdgcn_sched_barrier(0);
             }
-            if (ch > c_lo) finish(p00, p01, p10, p11, bp, pv0);   // the previous chunk, under these MFMAs
+            if (ch > c_lo) finish(p00, p01, p10, p11, bp, pv0, bsp);   // the previous chunk, under these MFMAs
             p00 = c00; p01 = c01; p10 = c10; p11 = c11;
 #pragma unroll
             for (int r = 0; r < 8; ++r) bp[r] = bq[r];
             pv0 = v0;
+            bsp = bs;
+            bs = bs == 2 ? 0 : bs + 1;
             __syncthreads();
         }
-        if (c_hi > c_lo) finish(p00, p01, p10, p11, bp, pv0);
+        if (c_hi > c_lo) finish(p00, p01, p10, p11, bp, pv0, bsp);
         int pk0, pk1, nt0, nt1;
         combine_ex(rb0, rel, band, g, pk0, nt0);
         combine_ex(rb1, rel, band, g, pk1, nt1);
@@ -901,6 +942,12 @@ __global__ void __launch_bounds__(256, TWOSD_CUT3_BPC) cut_argmax3_kernel(CutPar
         __syncthreads();
         for (int v = threadIdx.x; v < P.nv; v += 256) P.hist_part[(size_t)blockIdx.x * P.nv + v] = hl[v];
     }
+#ifdef TWOSD_CUT3_COUNT
+    if (lane == 0 && P.fstats) {
+        atomicAdd(&P.fstats[10], cnt_steps); atomicAdd(&P.fstats[11], cnt_rare);
+        atomicAdd(&P.fstats[12], cnt_lanes);
+    }
+#endif
     const int slot = blockIdx.x * 4 + wid;
     double *out = P.partial + (size_t)slot * (P.k + 1);
     if (lane == 0) out[0] = pv_sum;
@@ -1477,6 +1524,8 @@ struct CutWs {
     size_t pktc_cap = 0;
     float *PKTc32 = nullptr;               // the fp32 pass's chunk source
     size_t pktc32_cap = 0;
+    float *basec32 = nullptr;              // the fp32 pass's prefilter bases
+    size_t basec32_cap = 0;
     int pk_count = 0, pk_vcap = 0, pk_k4 = 0;
     size_t pk_cap = 0;
     int *rows = nullptr;
@@ -1522,7 +1571,7 @@ static CutWs *cws(twosd_ctx *c) {
 void cut_free(twosd_ctx *c) {
     if (!c->cut_ws) return;
     CutWs *w = (CutWs *)c->cut_ws;
-    hipFree(w->PK); hipFree(w->PKT); hipFree(w->PKO); hipFree(w->PKTc); hipFree(w->PKTc32); hipFree(w->rows); hipFree(w->eord); hipFree(w->coef); hipFree(w->bvec); hipFree(w->base);
+    hipFree(w->PK); hipFree(w->PKT); hipFree(w->PKO); hipFree(w->PKTc); hipFree(w->PKTc32); hipFree(w->basec32); hipFree(w->rows); hipFree(w->eord); hipFree(w->coef); hipFree(w->bvec); hipFree(w->base);
     hipFree(w->partial); hipFree(w->sums); hipFree(w->gpart); hipFree(w->g); hipFree(w->arg); hipFree(w->flag);
     hipFree(w->val); hipFree(w->hist); hipFree(w->part2); hipFree(w->hist_part);
     hipFree(w->tp_m); hipFree(w->tp_i); hipFree(w->tp_f);
@@ -1913,7 +1962,7 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
         }
         if (!w->nvc && (rc = realloc_dev(&w->nvc, 1))) return rc;
         if ((size_t)nv > w->pkoc_cap) {
-            if ((rc = realloc_dev(&w->PKOc, (size_t)nv * k4)) || (rc = realloc_dev(&w->basec, nv))) return rc;
+            if ((rc = realloc_dev(&w->PKOc, (size_t)nv * k4)) || (rc = realloc_dev(&w->basec, (size_t)vcap32))) return rc;
             w->pkoc_cap = nv;
         }
         hipLaunchKernelGGL(cut_compact_kernel, dim3(1), dim3(1024), 0, c->stream, nv, w->base, twins ? w->tprev : nullptr, w->vmap,
@@ -1923,13 +1972,19 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
             if ((rc = realloc_dev(&w->PKTc32, (size_t)rows32 * vcap32))) return rc;
             w->pktc32_cap = (size_t)rows32 * vcap32;
         }
+        if (want32 && (size_t)vcap32 > w->basec32_cap) {
+            if ((rc = realloc_dev(&w->basec32, (size_t)vcap32))) return rc;
+            w->basec32_cap = vcap32;
+        }
         const size_t tot2 = (size_t)std::max(rows, rows32) * vcap32;
         hipLaunchKernelGGL(cut_pktc_kernel, dim3((unsigned)std::min<size_t>(4096, (tot2 + 255) / 256)), dim3(256), 0, c->stream, k,
                            rows, w->pk_vcap, vcap32, w->PKT, w->coef, w->base, w->vmap, w->nvc, w->PKTc, rows32,
                            want32 ? w->PKTc32 : nullptr);
         P.PKTc32 = w->PKTc32;
         hipLaunchKernelGGL(cut_compact_rows_kernel, dim3((unsigned)std::min<size_t>(2048, ((size_t)nv * k4 + 255) / 256)), dim3(256), 0,
-                           c->stream, nv, k4, w->vmap, w->nvc, w->PKO, w->base, w->PKOc, w->basec);
+                           c->stream, nv, k4, w->vmap, w->nvc, w->PKO, w->base, w->PKOc, w->basec, vcap32,
+                           want32 ? w->basec32 : nullptr);
+        P.basec32 = w->basec32;
         P.PKTc = w->PKTc;
         P.vcap32 = vcap32;
         P.vmap = w->vmap;
@@ -2062,6 +2117,8 @@ extern "C" int twosd_cut_stats(twosd_ctx *c, int64_t *out) {
     HIPCHK(hipMemcpy(h, w->fstats, sizeof(h), hipMemcpyDeviceToHost));
     for (int i = 0; i < 3; ++i) out[i] = (int64_t)h[i];
     out[3] = (int64_t)h[9];
+    if (getenv("TWOSD_CUT3_COUNT_PRINT"))   // diagnostic build -DTWOSD_CUT3_COUNT only
+        fprintf(stderr, "argmax3: chunk steps %llu, past the prefilter %llu, lanes past it %llu\n", h[10], h[11], h[12]);
     if (getenv("TWOSD_FIX_STAMPS_PRINT"))
         fprintf(stderr, "fixup stamps (cycles summed over waves): rows/setup %llu deltas %llu list %llu chains %llu decide %llu sums %llu\n",
                 h[3], h[4], h[5], h[6], h[7], h[8]);
