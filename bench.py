@@ -382,7 +382,8 @@ def main():
         step(xs[(i - args.warmup) % X])
     barrier()
     acc = {"lp": 0.0, "dd": 0.0, "cut": 0.0, "fin": 0.0, "sel": 0.0, "flops": 0.0, "piv": 0, "pmax": 0, "eta": 0, "retries": 0}
-    per_x = [{"piv": 0, "n": 0, "lp": 0.0, "wall": 0.0, "steps": 0, "alpha": None, "refresh": 0.0, "eta": 0} for _ in xs]
+    per_x = [{"piv": 0, "n": 0, "lp": 0.0, "wall": 0.0, "steps": 0, "alpha": None, "refresh": 0.0, "eta": 0, "reps": 0, "full": 0}
+             for _ in xs]
     cur = {"xi": 0, "piv": 0, "lp": 0.0}
 
     def record():
@@ -396,6 +397,8 @@ def main():
         acc["piv"] += ps; acc["pmax"] = max(acc["pmax"], pm)
         px = per_x[cur["xi"]]
         px["piv"] += ps; px["n"] += n_local; px["lp"] += tm[0]; px["eta"] += eta
+        if not args.no_dedup:
+            px["reps"] += ctx.last_push_reps(); px["full"] += ctx.last_push_mode()
         cur["piv"] += ps; cur["lp"] += tm[0]
     t0 = time.perf_counter()
     step_log = []    # per timed step: x index, wall ms, refresh ms, LP kernel ms, mean pivots
@@ -478,6 +481,10 @@ def main():
                  "lp_kernel_ms": px["lp"] / 1e3 / max(px["steps"], 1),
                  "lp_pivots_mean": px["piv"] / max(px["n"], 1),
                  "lp_eta_entries": px["eta"] / max(px["steps"], 1),
+                 # the keyed push: duals recovered per epigraph pass, and the passes that recovered
+                 # every dual in the main solve instead of re-solving the representatives
+                 "push_representatives": px["reps"] / max(px["steps"] * E, 1),
+                 "push_full_passes": px["full"],
                  "alpha": px["alpha"],
                  "incumbent_objective": px.get("objective")}
                 for it, xx, px in zip(x_iters, xs, per_x)]

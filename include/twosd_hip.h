@@ -255,6 +255,11 @@ int twosd_solve_push(twosd_ctx *ctx, int epi, const double *x, int first, int co
  * each distinct optimal dual vertex of the batch (every later scenario at a vertex pushes an
  * equal vector, a no-op of push!, dual_set.jl:84-94); `count` with TWOSD_PUSH_ALL=1. */
 int twosd_last_push_reps(twosd_ctx *ctx, int *reps);
+/* How the last twosd_solve_push obtained the representatives' duals: 0 = re-solved with dual
+ * recovery after the keyed main pass; 1 = recovered for every scenario in the main pass and
+ * gathered (chosen when the previous keyed push re-solved more than a quarter of its batch;
+ * TWOSD_PUSH_MODE=1 / 2 forces one or the other).  The pushed rows are the same either way. */
+int twosd_last_push_mode(twosd_ctx *ctx, int *full);
 
 /*
  * build_sasa_cut (epigraph.jl:125-146) incl. argmax_procedure (subprob.jl:141-169) over

@@ -60,6 +60,7 @@ SIGNATURES = [
     ("twosd_dvs_fingerprint", I, [P, P]),
     ("twosd_solve_push", I, [P, I, P, I, I, P, P, P]),
     ("twosd_last_push_reps", I, [P, P]),
+    ("twosd_last_push_mode", I, [P, P]),
     ("twosd_build_cut", I, [P, I, P, D, P, P, P, P, P]),
     ("twosd_cut_partial_len", I, [P, P, P]),
     ("twosd_cut_partial", I, [P, I, P, D, D, P, P, P, P]),

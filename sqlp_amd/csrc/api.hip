@@ -285,7 +285,7 @@ static void free_template(twosd_ctx *c) {
     dfree(c->d_fixedmask); dfree(c->d_ubmask);
     dfree(c->d_hb0); dfree(c->d_basic0);
     dfree(c->d_xbase); dfree(c->d_queue); dfree(c->d_lpstats);
-    dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_ops); dfree(c->d_etan);
+    dfree(c->d_obj); dfree(c->d_pi); dfree(c->d_pi_rep); dfree(c->d_y); dfree(c->d_status); dfree(c->d_iters); dfree(c->d_ops); dfree(c->d_etan);
     dfree(c->d_dvtmp);
     dfree(c->d_bnnz); dfree(c->d_sel_cinf); dfree(c->d_sel_ptr); dfree(c->d_sel_code); c->sel_code_cap = 0; dfree(c->d_head_out); dfree(c->d_pool_pick); dfree(c->d_cpick); dfree(c->d_order); dfree(c->d_sort_tmp);
     dfree(c->d_cand); dfree(c->d_sel_key); dfree(c->d_sel_pkey); dfree(c->d_sel_ppick); c->sel_pcap = 0; c->key_cap = 0; c->pool_l1 = c->pool_ncand = 0; c->order_cap = 0; c->sort_tmp_bytes = 0; c->head_cap = 0; c->pick_cap = 0; c->pool.clear();
@@ -2718,6 +2718,15 @@ extern "C" int twosd_last_lp_ops(twosd_ctx *c, int64_t *row_ops, int *row_width)
     return TWOSD_OK;
 }
 
+// rows list[0..U) of pi (m doubles each) gathered in list order (the push of a full-mode solve_push)
+__global__ void gather_rows_kernel(int U, int m, const int *__restrict__ list, const double *__restrict__ pi, double *__restrict__ out) {
+    const size_t tot = (size_t)U * m;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (size_t)gridDim.x * blockDim.x) {
+        const int u = (int)(i / m), r = (int)(i % m);
+        out[i] = pi[(size_t)list[u] * m + r];
+    }
+}
+
 // non-optimal statuses among the scenarios of a list-mode re-solve (status is by scenario)
 __global__ void list_status_kernel(int U, const int *__restrict__ list, const int *__restrict__ st,
                                    unsigned long long *bad) {
@@ -2739,8 +2748,16 @@ extern "C" int twosd_solve_push(twosd_ctx *c, int epi, const double *x, int firs
     // TWOSD_PUSH_ALL=1: recover and push the dual of every scenario (the pre-key path, kept for
     // the equivalence test); default: vertex keys, first occurrences, re-solve of those only
     const bool all = getenv("TWOSD_PUSH_ALL") && atoi(getenv("TWOSD_PUSH_ALL")) != 0;
+    // Full mode: the main pass recovers every scenario's dual (and its key), and the representatives'
+    // rows are gathered from it -- the same rows the re-solve would produce (same start, same pivots,
+    // same recovery), without solving them twice.  Chosen when the last keyed push re-solved more
+    // than a quarter of its scenarios (ssn: ~every scenario its own vertex; storm: < 1 %).
+    // TWOSD_PUSH_MODE: 0 auto (default), 1 always re-solve, 2 always full.
+    const int pmode = getenv("TWOSD_PUSH_MODE") ? atoi(getenv("TWOSD_PUSH_MODE")) : 0;
+    const bool full = !all && (pmode == 2 || (pmode == 0 && c->push_rep_frac > 0.25));
+    c->last_push_full = full ? 1 : 0;
     LpRun o;
-    o.want_pi = all;
+    o.want_pi = all || full;
     o.want_key = !all;
     int rc = run_lp_ex(c, x, d_dv, count, o);
     if (rc) return rc;
@@ -2768,7 +2785,23 @@ extern "C" int twosd_solve_push(twosd_ctx *c, int epi, const double *x, int firs
         HIPCHK(hipEventSynchronize(c->ev[6]));
         hipEventElapsedTime(&ms_key, c->ev[5], c->ev[6]);
         c->last_push_reps = U;
-        if (U > 0) {
+        c->push_rep_frac = (double)U / count;
+        if (U > 0 && full) {
+            const int m = c->L.m;
+            if ((size_t)U > c->pi_rep_cap) {
+                if ((rc = dalloc(&c->d_pi_rep, (size_t)U * m))) return rc;
+                c->pi_rep_cap = U;
+            }
+            hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)std::min<size_t>(4096, ((size_t)U * m + 255) / 256)), dim3(256), 0,
+                               c->stream, U, m, d_list, c->d_pi, c->d_pi_rep);
+            HIPCHK(hipGetLastError());
+            c->t_us[0] = t_lp;
+            HIPCHK(hipEventRecord(c->ev[2], c->stream));
+            if ((rc = dvs_push_device(c, U, c->d_pi_rep, nullptr))) return rc;
+            HIPCHK(hipEventRecord(c->ev[3], c->stream));
+            HIPCHK(hipEventSynchronize(c->ev[3]));
+            hipEventElapsedTime(&ms, c->ev[2], c->ev[3]);
+        } else if (U > 0) {
             LpRun r;
             r.want_pi = true;
             r.d_list = d_list;
@@ -2801,6 +2834,12 @@ extern "C" int twosd_solve_push(twosd_ctx *c, int epi, const double *x, int firs
     c->last_obj_wsum = obj_wsum; c->last_obj_w = obj_w;   // of the batch, not of the representatives' re-solve
     c->t_us[1] = 1e3 * (ms + ms_key);
     if (new_size) *new_size = c->dvs.size;
+    return TWOSD_OK;
+}
+
+extern "C" int twosd_last_push_mode(twosd_ctx *c, int *full) {
+    if (!c || !full) return fail(TWOSD_E_ARG, "last_push_mode: NULL");
+    *full = c->last_push_full;
     return TWOSD_OK;
 }
 

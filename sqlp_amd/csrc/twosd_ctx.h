@@ -201,6 +201,10 @@ struct twosd_ctx {
     size_t stage_bytes[16] = {};
     std::map<const void *, size_t> dcap;   // element capacity of grow-only device arrays (by member address)
     int last_push_reps = 0;       // representatives re-solved by the last solve_push
+    double push_rep_frac = 0.0;   // representatives / scenarios of the last keyed solve_push (push mode choice)
+    int last_push_full = 0;       // 1: the last solve_push recovered every dual in its main pass
+    double *d_pi_rep = nullptr;   // the representatives' dual rows gathered for the push (full mode)
+    size_t pi_rep_cap = 0;
 };
 
 namespace twosd {

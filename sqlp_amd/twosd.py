@@ -355,6 +355,13 @@ class SDContext:
         check(self.lib.twosd_last_push_reps(self.h, C.byref(r)))
         return r.value
 
+    def last_push_mode(self) -> int:
+        """1 if the last solve_push recovered every dual in its main pass (full mode), 0 if it
+        re-solved the representatives (twosd_last_push_mode)."""
+        r = C.c_int()
+        check(self.lib.twosd_last_push_mode(self.h, C.byref(r)))
+        return r.value
+
     def lp_flops(self):
         """Counted fp64 FLOPs of the last LP batch (2 * row width per executed row op)."""
         ops = C.c_int64()

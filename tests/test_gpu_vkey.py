@@ -53,6 +53,53 @@ def test_keyed_push_equals_push_all(name, N, pool, monkeypatch):
     print(f"{name}: N={N} |V|={len(V_key)} representatives re-solved {r_key}")
 
 
+@pytest.mark.parametrize("name,N,pool", [("ssn", 12000, 1), ("storm", 30000, 512), ("transship", 6000, 1)])
+def test_push_full_mode_equals_resolve(name, N, pool, monkeypatch):
+    """The two ways solve_push gets the representatives' duals -- re-solving them after the keyed
+    main pass (TWOSD_PUSH_MODE=1), or recovering every dual in the main pass and gathering
+    (TWOSD_PUSH_MODE=2) -- and the automatic choice push the same ordered V, bit for bit; the
+    automatic choice switches to full mode after a batch whose representatives exceed a quarter."""
+    from sqlp_amd import smps, twosd
+    inst = I.load(name)
+    ctx = twosd.SDContext(inst["sp2"], inst["sto"])
+    x = I.x_ev(name)
+    ctx.compute_basis(x, smps.mean_values(inst["sto"]))
+    if pool > 1:
+        tr = twosd.sdEpigraph(ctx, 1.0, 0.0)
+        twosd.add_scenarios(tr, I.sample(name, 4 * pool, seed=5))
+        ctx.pool_build(tr, x, 0, 4 * pool, pool)
+    epi = twosd.sdEpigraph(ctx, 1.0, 0.0)
+    twosd.add_scenarios(epi, I.sample(name, N, seed=17))
+    V = twosd.sdDualVertexSet(ctx)
+    third = N // 3
+    runs = {}
+    for mode in ("1", "2", "0"):
+        monkeypatch.setenv("TWOSD_PUSH_MODE", mode)
+        V.clear()
+        objs, reps, modes = [], [], []
+        for lo, hi in ((0, third), (third, 2 * third), (2 * third, N)):
+            obj, st, _ = twosd.solve_push(epi, x, lo, hi - lo)
+            assert (st == 0).all()
+            objs.append(obj)
+            reps.append(ctx.last_push_reps())
+            modes.append(ctx.last_push_mode())
+        runs[mode] = (np.concatenate(objs), V.matrix(), reps, modes)
+    o1, V1, r1, m1 = runs["1"]
+    for mode in ("2", "0"):
+        o, Vm, r, _ = runs[mode]
+        np.testing.assert_array_equal(o, o1)
+        assert Vm.shape == V1.shape
+        np.testing.assert_array_equal(Vm, V1)
+        assert r == r1
+    assert m1 == [0, 0, 0] and runs["2"][3] == [1, 1, 1]
+    # automatic: full mode when the context's previous keyed push re-solved > 1/4 of its batch (the
+    # auto run follows the mode-2 run's last batch)
+    sizes = (third, third, N - 2 * third)
+    frac = [r_ / n_ for r_, n_ in zip(r1, sizes)]
+    assert runs["0"][3] == [int(frac[2] > 0.25), int(frac[0] > 0.25), int(frac[1] > 0.25)]
+    print(f"{name}: representatives {r1}, auto modes {runs['0'][3]}")
+
+
 def test_keyed_push_nonoptimal_refused():
     """A batch with a non-optimal scenario pushes nothing on the keyed path (as on the direct
     one): TWOSD_E_LP, V unchanged."""
