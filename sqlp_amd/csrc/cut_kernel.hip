@@ -1849,8 +1849,10 @@ static int cut_partial_impl(twosd_ctx *c, int epi, const double *x, double tie_r
     }
     const int nunits = full + (ntiles - full) * S;
     const int nblocks = std::max(1, std::min(nunits, B));
-    // the fixup takes 64 scenarios per wave step: enough waves that every SIMD holds several
-    static const int fix_per_cu = getenv("TWOSD_FIX_BPC") ? std::max(1, atoi(getenv("TWOSD_FIX_BPC"))) : 4;
+    // the fixup takes 64 scenarios per wave step: enough waves that every SIMD holds several; 3 blocks
+    // per CU = its resident occupancy (launch bounds, LDS), so no block waits for a second round
+    // (storm 1M at x_EV: 0.88 ms at 4, 0.69 at 3, 0.86 at 2, 0.82 at 8: profiles/r06/ab_fixup_grid.txt)
+    static const int fix_per_cu = getenv("TWOSD_FIX_BPC") ? std::max(1, atoi(getenv("TWOSD_FIX_BPC"))) : 3;
     // scenarios per wave step: 64, or 32 / 16 when 64 would leave fewer waves than 3 resident blocks
     // per CU hold (a 125k shard at N = 8: 1953 waves of one step each, every flagged row's batch
     // latency in series)
